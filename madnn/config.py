@@ -1,0 +1,117 @@
+"""Typed configuration for madnn.
+
+Precedence: explicit kwargs > ``MADNN_*`` environment variables > defaults
+(SURVEY §5.6).  The reference's hard-coded module flags are kept as named
+options:
+
+* ``shuffle_shards``  <- ``dataShuffle``  (reference datamodule.lua:3)
+* ``sync``            <- ``syncPrototype`` (datamodule.lua:4): ``"params"`` is
+  the reference's periodic parameter+gradient averaging, ``"grads"`` is
+  synchronous gradient averaging (DDP semantics), ``"manual"`` is
+  ``batchSize = -1`` (datamodule.lua:45).
+* ``debug_shapes``    <- ``printDims`` (nodemodule.lua:3)
+* ``tp_backward``     <- ``syncTanh``/``syncReshape`` (nodemodule.lua:4-5); the
+  corrected all-gather is the only mode, the flag is accepted for parity.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+
+def _env(name: str, default, cast):
+    v = os.environ.get(f"MADNN_{name.upper()}")
+    if v is None:
+        return default
+    if cast is bool:
+        return v.lower() in ("1", "true", "yes", "on")
+    return cast(v)
+
+
+@dataclass
+class Config:
+    # strategy: auto | dp | pp | dp_pp | tp | none
+    strategy: str = "auto"
+    # data parallel
+    sync: str = "grads"                  # grads | params | manual
+    sync_every: Optional[int] = None     # period K for sync="params" (None => reference heuristic)
+    bucket_mb: float = 64.0              # gradient bucket cap (MB of reduce dtype)
+    overlap: bool = True                 # overlap bucket all-reduce with backward on a comm stream
+    reduce_dtype: str = "float32"        # dtype of the gradient all-reduce buffers
+    broadcast_buffers: bool = True       # broadcast module buffers (BN stats) at wrap time
+    find_unused: bool = True             # flush buckets holding params that got no grad
+    # mixed precision
+    dtype: str = "bfloat16"              # compute/parameter dtype of the wrapped model
+    keep_fp32_norms: bool = True         # BatchNorm/LayerNorm params stay fp32
+    channels_last: Optional[bool] = None  # None => auto (conv nets)
+    # pipeline parallel
+    pp_stages: Optional[int] = None
+    microbatches: Optional[int] = None
+    schedule: str = "1f1b"               # gpipe | 1f1b
+    # tensor parallel
+    tp_size: int = 1
+    tp_backward: str = "allgather"
+    # activation checkpointing: none | auto | all
+    checkpointing: str = "auto"
+    # memory model
+    hbm_gb: float = 288.0
+    mem_headroom: float = 0.85
+    # data
+    shuffle_shards: bool = False
+    remainder: str = "drop"              # drop | last | pad
+    # debug / robustness
+    debug_shapes: bool = False
+    check_collectives: bool = False
+    sync_comm: bool = False              # run comm on the compute stream (race debugging)
+    timeout_s: float = 600.0
+    seed: int = 0
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def from_env(cls, **overrides) -> "Config":
+        cfg = cls()
+        for f in dataclasses.fields(cls):
+            if f.name == "extra":
+                continue
+            cur = getattr(cfg, f.name)
+            if cur is None:
+                cast = int if f.name in ("sync_every", "pp_stages", "microbatches") else str
+                if f.name == "channels_last":
+                    cast = bool
+            else:
+                cast = type(cur)
+            setattr(cfg, f.name, _env(f.name, cur, cast))
+        for k, v in overrides.items():
+            if v is None:
+                continue
+            if not hasattr(cfg, k):
+                cfg.extra[k] = v
+            else:
+                setattr(cfg, k, v)
+        cfg.validate()
+        return cfg
+
+    def validate(self):
+        if self.strategy not in ("auto", "dp", "pp", "dp_pp", "tp", "none"):
+            raise ValueError(f"unknown strategy {self.strategy!r}")
+        if self.sync not in ("grads", "params", "manual"):
+            raise ValueError(f"unknown sync mode {self.sync!r}")
+        if self.schedule not in ("gpipe", "1f1b"):
+            raise ValueError(f"unknown pipeline schedule {self.schedule!r}")
+        if self.remainder not in ("drop", "last", "pad"):
+            raise ValueError(f"unknown remainder policy {self.remainder!r}")
+        if self.checkpointing not in ("none", "auto", "all"):
+            raise ValueError(f"unknown checkpointing policy {self.checkpointing!r}")
+        if self.bucket_mb <= 0:
+            raise ValueError("bucket_mb must be > 0")
+
+
+def torch_dtype(name):
+    import torch
+
+    if isinstance(name, torch.dtype):
+        return name
+    return {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float32": torch.float32, "fp32": torch.float32,
+            "float16": torch.float16, "fp16": torch.float16}[name]

@@ -1,0 +1,269 @@
+// torch.ops.madnn.* registration for the hand-written gfx950 kernels.
+//
+// The kernels live in bucket.hip / optim.hip / norm.hip behind a C ABI; this
+// file only validates tensors, fetches the current HIP stream and launches.
+// Registered for the CUDA dispatch key, which is what ROCm PyTorch uses for
+// HIP device tensors.  CPU tensors never reach this file: the Python layer
+// (madnn/ops/__init__.py) routes CPU tensors to the eager reference.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+extern "C" {
+hipError_t madnn_bucket_pack(void* const*, const int64_t*, const int64_t*, int, void*, int, int, float, hipStream_t);
+hipError_t madnn_bucket_unpack(void* const*, const int64_t*, const int64_t*, int, void*, int, int, float, hipStream_t);
+hipError_t madnn_flat_scale_cast(const void*, void*, int64_t, int, int, float, hipStream_t);
+hipError_t madnn_sgd_step(float*, const void*, int, float*, void*, int, int64_t, float, float, float, float, int, int,
+                          float, const float*, hipStream_t);
+hipError_t madnn_adam_step(float*, const void*, int, float*, float*, void*, int, int64_t, float, float, float, float,
+                           float, int, float, float, float, const float*, hipStream_t);
+int madnn_sqnorm_grid(int64_t);
+hipError_t madnn_sqnorm_partial(const void*, int, int64_t, float, float*, int, hipStream_t);
+hipError_t madnn_norm_finalize(const float*, int, float, float*, hipStream_t);
+hipError_t madnn_norm_fwd(const void*, const void*, const void*, const void*, void*, void*, float*, float*, int64_t,
+                          int, float, int, int, int, hipStream_t);
+int64_t madnn_norm_bwd_workspace(int64_t, int);
+hipError_t madnn_norm_bwd(const void*, const void*, const void*, const float*, const float*, const void*, void*, void*,
+                          void*, float*, int64_t, int, int, int, int, hipStream_t);
+}
+
+namespace {
+
+int dt_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    default: TORCH_CHECK(false, "madnn: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+hipStream_t cur_stream(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "madnn HIP kernel ", what, " failed: ", hipGetErrorString(e));
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "madnn: ", name, " must be a HIP device tensor");
+}
+
+// A tensor whose storage is one dense block (any stride permutation, e.g.
+// channels_last) can be packed as raw memory in its physical order.
+void check_dense(const at::Tensor& t) {
+  TORCH_CHECK(t.is_non_overlapping_and_dense(), "madnn bucket op: tensor must be non-overlapping and dense");
+}
+
+void bucket_copy(bool pack, at::TensorList tensors, const at::Tensor& flat, at::IntArrayRef offsets, double scale) {
+  check_dev(flat, "flat");
+  TORCH_CHECK(flat.is_contiguous(), "flat bucket must be contiguous");
+  TORCH_CHECK(tensors.size() == offsets.size(), "tensors/offsets length mismatch");
+  if (tensors.empty()) return;
+  c10::hip::HIPGuard guard(flat.device());
+  const int tdt = dt_code(tensors[0]);
+  std::vector<void*> ptrs;
+  std::vector<int64_t> numels, offs;
+  ptrs.reserve(tensors.size());
+  for (size_t i = 0; i < tensors.size(); ++i) {
+    const auto& t = tensors[i];
+    check_dev(t, "bucket tensor");
+    check_dense(t);
+    TORCH_CHECK(dt_code(t) == tdt, "bucket tensors must share one dtype");
+    TORCH_CHECK(offsets[i] >= 0 && offsets[i] + t.numel() <= flat.numel(), "bucket offset out of range");
+    ptrs.push_back(t.data_ptr());
+    numels.push_back(t.numel());
+    offs.push_back(offsets[i]);
+  }
+  auto fn = pack ? madnn_bucket_pack : madnn_bucket_unpack;
+  check(fn(ptrs.data(), offs.data(), numels.data(), (int)ptrs.size(), flat.data_ptr(), tdt, dt_code(flat),
+           (float)scale, cur_stream(flat)),
+        pack ? "bucket_pack" : "bucket_unpack");
+}
+
+void bucket_pack(at::TensorList srcs, at::Tensor flat, at::IntArrayRef offsets, double scale) {
+  bucket_copy(true, srcs, flat, offsets, scale);
+}
+
+void bucket_unpack(at::TensorList dsts, at::Tensor flat, at::IntArrayRef offsets, double scale) {
+  bucket_copy(false, dsts, flat, offsets, scale);
+}
+
+void flat_scale_cast(const at::Tensor& src, at::Tensor dst, double scale) {
+  check_dev(src, "src");
+  check_dev(dst, "dst");
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "flat_scale_cast needs contiguous tensors");
+  TORCH_CHECK(src.numel() == dst.numel(), "flat_scale_cast size mismatch");
+  c10::hip::HIPGuard guard(src.device());
+  check(madnn_flat_scale_cast(src.data_ptr(), dst.data_ptr(), src.numel(), dt_code(src), dt_code(dst), (float)scale,
+                              cur_stream(src)),
+        "flat_scale_cast");
+}
+
+const float* opt_scale(const c10::optional<at::Tensor>& s) {
+  if (!s.has_value()) return nullptr;
+  TORCH_CHECK(s->scalar_type() == at::kFloat && s->is_cuda(), "device scale must be a float HIP tensor");
+  return s->data_ptr<float>();
+}
+
+void sgd_step(at::Tensor master, const at::Tensor& grad, const c10::optional<at::Tensor>& mom,
+              const c10::optional<at::Tensor>& model, double lr, double momentum, double dampening,
+              double weight_decay, bool nesterov, bool first_step, double grad_scale,
+              const c10::optional<at::Tensor>& dscale) {
+  check_dev(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master must be contiguous fp32");
+  TORCH_CHECK(grad.is_contiguous() && grad.numel() == master.numel(), "grad must be contiguous and match master");
+  if (momentum != 0.0) TORCH_CHECK(mom.has_value() && mom->numel() == master.numel(), "momentum buffer required");
+  if (model.has_value()) TORCH_CHECK(model->is_contiguous() && model->numel() == master.numel(), "model copy size");
+  c10::hip::HIPGuard guard(master.device());
+  check(madnn_sgd_step(master.data_ptr<float>(), grad.data_ptr(), dt_code(grad),
+                       mom.has_value() ? mom->data_ptr<float>() : nullptr,
+                       model.has_value() ? model->data_ptr() : nullptr, model.has_value() ? dt_code(*model) : -1,
+                       master.numel(), (float)lr, (float)momentum, (float)dampening, (float)weight_decay,
+                       nesterov ? 1 : 0, first_step ? 1 : 0, (float)grad_scale, opt_scale(dscale),
+                       cur_stream(master)),
+        "sgd_step");
+}
+
+void adam_step(at::Tensor master, const at::Tensor& grad, at::Tensor m1, at::Tensor m2,
+               const c10::optional<at::Tensor>& model, double lr, double beta1, double beta2, double eps,
+               double weight_decay, bool adamw, int64_t step, double grad_scale,
+               const c10::optional<at::Tensor>& dscale) {
+  check_dev(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master must be contiguous fp32");
+  TORCH_CHECK(grad.is_contiguous() && grad.numel() == master.numel(), "grad must be contiguous and match master");
+  TORCH_CHECK(m1.numel() == master.numel() && m2.numel() == master.numel(), "adam state size");
+  if (model.has_value()) TORCH_CHECK(model->is_contiguous() && model->numel() == master.numel(), "model copy size");
+  TORCH_CHECK(step >= 1, "adam step must be >= 1");
+  c10::hip::HIPGuard guard(master.device());
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  check(madnn_adam_step(master.data_ptr<float>(), grad.data_ptr(), dt_code(grad), m1.data_ptr<float>(),
+                        m2.data_ptr<float>(), model.has_value() ? model->data_ptr() : nullptr,
+                        model.has_value() ? dt_code(*model) : -1, master.numel(), (float)lr, (float)beta1,
+                        (float)beta2, (float)eps, (float)weight_decay, adamw ? 1 : 0, (float)bc1,
+                        (float)std::sqrt(bc2), (float)grad_scale, opt_scale(dscale), cur_stream(master)),
+        "adam_step");
+}
+
+// Returns a 2-element fp32 device tensor [global L2 norm, clip coefficient].
+at::Tensor grad_norm(at::TensorList flats, double max_norm, double scale) {
+  TORCH_CHECK(!flats.empty(), "grad_norm needs at least one tensor");
+  c10::hip::HIPGuard guard(flats[0].device());
+  std::vector<int> grids;
+  int total = 0;
+  for (const auto& f : flats) {
+    check_dev(f, "grad");
+    TORCH_CHECK(f.is_contiguous(), "grad_norm inputs must be contiguous");
+    grids.push_back(madnn_sqnorm_grid(f.numel()));
+    total += grids.back();
+  }
+  auto opts = flats[0].options().dtype(at::kFloat);
+  at::Tensor partial = at::empty({std::max(total, 1)}, opts);
+  at::Tensor out = at::empty({2}, opts);
+  hipStream_t s = cur_stream(flats[0]);
+  int off = 0;
+  for (size_t i = 0; i < flats.size(); ++i) {
+    check(madnn_sqnorm_partial(flats[i].data_ptr(), dt_code(flats[i]), flats[i].numel(), (float)scale,
+                               partial.data_ptr<float>() + off, grids[i], s),
+          "sqnorm_partial");
+    off += grids[i];
+  }
+  if (total == 0) partial.zero_();
+  check(madnn_norm_finalize(partial.data_ptr<float>(), std::max(total, 1), (float)max_norm, out.data_ptr<float>(), s),
+        "norm_finalize");
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Tensor& x,
+                                                                    const c10::optional<at::Tensor>& res,
+                                                                    const at::Tensor& w,
+                                                                    const c10::optional<at::Tensor>& b, double eps,
+                                                                    bool rms) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "norm input must be contiguous");
+  const int64_t H = w.numel();
+  TORCH_CHECK(x.size(-1) == H && w.is_contiguous(), "norm weight / hidden size mismatch");
+  TORCH_CHECK(H % 8 == 0 && H <= 16384, "madnn norm kernel needs H % 8 == 0 and H <= 16384, got ", H);
+  const int64_t rows = x.numel() / H;
+  c10::hip::HIPGuard guard(x.device());
+  at::Tensor y = at::empty_like(x);
+  at::Tensor sum;
+  if (res.has_value()) {
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous() && res->scalar_type() == x.scalar_type(),
+                "residual must match x");
+    sum = at::empty_like(x);
+  }
+  auto fopts = x.options().dtype(at::kFloat);
+  at::Tensor mean = rms ? at::empty({0}, fopts) : at::empty({rows}, fopts);
+  at::Tensor rstd = at::empty({rows}, fopts);
+  if (b.has_value()) TORCH_CHECK(b->numel() == H && b->scalar_type() == w.scalar_type(), "norm bias mismatch");
+  check(madnn_norm_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, w.data_ptr(),
+                       b.has_value() ? b->data_ptr() : nullptr, y.data_ptr(), sum.defined() ? sum.data_ptr() : nullptr,
+                       rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)H, (float)eps,
+                       rms ? 1 : 0, dt_code(x), dt_code(w), cur_stream(x)),
+        "norm_fwd");
+  if (!sum.defined()) sum = at::empty({0}, x.options());
+  return {y, sum, mean, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x,
+                                                        const at::Tensor& w, const at::Tensor& mean,
+                                                        const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
+                                                        bool rms, bool has_bias) {
+  check_dev(x, "x");
+  const int64_t H = w.numel();
+  const int64_t rows = x.numel() / H;
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "norm_bwd: dy/x mismatch");
+  c10::hip::HIPGuard guard(x.device());
+  at::Tensor dyc = dy.scalar_type() == x.scalar_type() ? dy : dy.to(x.scalar_type());
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dw = at::empty_like(w);
+  at::Tensor db = has_bias ? at::empty_like(w) : at::empty({0}, w.options());
+  at::Tensor ws = at::empty({madnn_norm_bwd_workspace(rows, (int)H)}, x.options().dtype(at::kFloat));
+  at::Tensor dr;
+  if (dres.has_value() && dres->defined()) {
+    dr = dres->scalar_type() == x.scalar_type() ? dres->contiguous() : dres->to(x.scalar_type()).contiguous();
+  }
+  check(madnn_norm_bwd(dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
+                       rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr(),
+                       has_bias ? db.data_ptr() : nullptr, ws.data_ptr<float>(), rows, (int)H, rms ? 1 : 0,
+                       dt_code(x), dt_code(w), cur_stream(x)),
+        "norm_bwd");
+  return {dx, dw, db};
+}
+
+}  // namespace
+
+TORCH_LIBRARY(madnn, m) {
+  m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
+  m.def("bucket_unpack(Tensor(a!)[] dsts, Tensor flat, int[] offsets, float scale) -> ()");
+  m.def("flat_scale_cast(Tensor src, Tensor(a!) dst, float scale) -> ()");
+  m.def(
+      "sgd_step(Tensor(a!) master, Tensor grad, Tensor(b!)? mom, Tensor(c!)? model, float lr, float momentum, "
+      "float dampening, float weight_decay, bool nesterov, bool first_step, float grad_scale, Tensor? dscale) -> ()");
+  m.def(
+      "adam_step(Tensor(a!) master, Tensor grad, Tensor(b!) m1, Tensor(c!) m2, Tensor(d!)? model, float lr, "
+      "float beta1, float beta2, float eps, float weight_decay, bool adamw, int step, float grad_scale, "
+      "Tensor? dscale) -> ()");
+  m.def("grad_norm(Tensor[] flats, float max_norm, float scale) -> Tensor");
+  m.def("norm_fwd(Tensor x, Tensor? res, Tensor w, Tensor? b, float eps, bool rms) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dres, bool rms, bool has_bias) -> "
+      "(Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
+  m.impl("bucket_pack", bucket_pack);
+  m.impl("bucket_unpack", bucket_unpack);
+  m.impl("flat_scale_cast", flat_scale_cast);
+  m.impl("sgd_step", sgd_step);
+  m.impl("adam_step", adam_step);
+  m.impl("grad_norm", grad_norm);
+  m.impl("norm_fwd", norm_fwd);
+  m.impl("norm_bwd", norm_bwd);
+}

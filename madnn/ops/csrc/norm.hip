@@ -1,0 +1,328 @@
+// K3 — LayerNorm / RMSNorm forward + backward for gfx950 (bf16 or f32 I/O,
+// fp32 statistics), with an optional fused residual add.
+//
+// North-star kernel; the reference has no normalisation layer
+// of its own.  Layout decisions for CDNA4:
+//  * TPR lanes own one row (TPR = 64 for H <= 1024: one row per wave, the row
+//    reduction is a pure wave shuffle; TPR = 128/256 for wider rows, finished
+//    through a 16-byte-aligned LDS slab).  Each lane keeps NC x 8 elements of
+//    its row in registers, loaded with 16-byte vector accesses, so x is read
+//    from HBM exactly once and the variance is an exact two-pass over registers.
+//  * Backward accumulates dgamma/dbeta for its columns in registers across the
+//    rows of a grid-stride loop, reduces the row groups of the workgroup in
+//    LDS, and writes ONE fp32 partial row per workgroup; a second small kernel
+//    reduces the partial slab column-parallel.  No float atomics anywhere
+//    (MI355X_MICROARCH.md "Global float atomics": contended adds are ~1.3 TB/s
+//    chip-wide and non-deterministic).
+//  * The XCD swizzle is deliberately absent: there is no inter-block reuse on a
+//    row-wise op (cdna_hip_programming.md T1 "Transfer: 0% on LayerNorm").
+#include "common.h"
+
+namespace madnn {
+
+constexpr int kNormThreads = 256;
+
+template <int TPR>
+__device__ __forceinline__ float row_sum(float v, float* red) {
+  v = wave_sum(v);
+  if constexpr (TPR == kWave) {
+    return v;
+  } else {
+    constexpr int WPR = TPR / kWave;  // waves per row
+    const int wid = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    const int first = (wid / WPR) * WPR;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < WPR; ++k) s += red[first + k];
+    return s;
+  }
+}
+
+template <int XDT, int WDT, int TPR, int NC>
+__global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
+    const void* __restrict__ x, const void* __restrict__ res, const void* __restrict__ w, const void* __restrict__ b,
+    void* __restrict__ y, void* __restrict__ sum_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    int64_t rows, int H, float eps, int rms) {
+  __shared__ __attribute__((aligned(16))) float red[kNormThreads / kWave];
+  constexpr int RPB = kNormThreads / TPR;
+  const int sub = threadIdx.x / TPR;
+  const int t = threadIdx.x % TPR;
+  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += (int64_t)gridDim.x * RPB) {
+    const int64_t row = row0 + sub;
+    const bool live = row < rows;  // uniform per row group; all lanes still join the LDS reduction
+    float v[NC][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (live && col < H) {
+        load8<XDT>(x, row * H + col, v[c]);
+        if (res) {
+          float r[8];
+          load8<XDT>(res, row * H + col, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+          store8<XDT>(sum_out, row * H + col, v[c]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[c][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      }
+    }
+    const float inv_h = 1.f / (float)H;
+    float mean = 0.f;
+    if (!rms) mean = row_sum<TPR>(s, red) * inv_h;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (live && col < H) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[c][j] - mean;
+          q += d * d;
+        }
+      }
+    }
+    const float rstd = __builtin_amdgcn_rsqf(row_sum<TPR>(q, red) * inv_h + eps);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (live && col < H) {
+        float wv[8], bv[8], o[8];
+        load8<WDT>(w, col, wv);
+        if (b) load8<WDT>(b, col, bv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[j] + (b ? bv[j] : 0.f);
+        store8<XDT>(y, row * H + col, o);
+      }
+    }
+    if (live && t == 0) {
+      if (mean_out) mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// dx = rstd * (w*dy - mean(w*dy) - xhat * mean(xhat*w*dy))     (LayerNorm)
+// dx = rstd * (w*dy - xhat * mean(xhat*w*dy))                  (RMSNorm)
+// partial[blk][0:H] = sum_rows dy*xhat, partial[blk][H:2H] = sum_rows dy
+template <int XDT, int WDT, int TPR, int NC>
+__global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const void* __restrict__ dres,
+    void* __restrict__ dx, float* __restrict__ partial, int64_t rows, int H, int rms, int has_bias) {
+  __shared__ __attribute__((aligned(16))) float red[kNormThreads / kWave];
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [RPB][2][NC*TPR*8] when RPB > 1
+  constexpr int RPB = kNormThreads / TPR;
+  const int sub = threadIdx.x / TPR;
+  const int t = threadIdx.x % TPR;
+  float dg[NC][8], db[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+
+  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += (int64_t)gridDim.x * RPB) {
+    const int64_t row = row0 + sub;
+    const bool live = row < rows;
+    const float mean = (live && !rms) ? mean_in[row] : 0.f;
+    const float rstd = live ? rstd_in[row] : 0.f;
+    float xh[NC][8], wdy[NC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (live && col < H) {
+        float xv[8], gv[8], wv[8];
+        load8<XDT>(x, row * H + col, xv);
+        load8<XDT>(dy, row * H + col, gv);
+        load8<WDT>(w, col, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[c][j] = (xv[j] - mean) * rstd;
+          wdy[c][j] = wv[j] * gv[j];
+          s1 += xh[c][j] * wdy[c][j];
+          s2 += wdy[c][j];
+          dg[c][j] += gv[j] * xh[c][j];
+          db[c][j] += gv[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xh[c][j] = wdy[c][j] = 0.f;
+      }
+    }
+    const float inv_h = 1.f / (float)H;
+    const float c1 = row_sum<TPR>(s1, red) * inv_h;
+    const float c2 = rms ? 0.f : row_sum<TPR>(s2, red) * inv_h;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (live && col < H) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (wdy[c][j] - c2 - xh[c][j] * c1);
+        if (dres) {
+          float r[8];
+          load8<XDT>(dres, row * H + col, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        store8<XDT>(dx, row * H + col, o);
+      }
+    }
+  }
+
+  // Reduce the RPB row groups of this workgroup, then one partial row out.
+  constexpr int W = NC * TPR * 8;
+  if constexpr (RPB > 1) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int lc = c * TPR * 8 + t * 8 + j;
+        slab[(sub * 2 + 0) * W + lc] = dg[c][j];
+        slab[(sub * 2 + 1) * W + lc] = db[c][j];
+      }
+    __syncthreads();
+    // each thread finalises a strided set of columns
+    for (int lc = threadIdx.x; lc < W; lc += kNormThreads) {
+      if (lc >= H) continue;
+      float a = 0.f, bb = 0.f;
+#pragma unroll
+      for (int r = 0; r < RPB; ++r) {
+        a += slab[(r * 2 + 0) * W + lc];
+        bb += slab[(r * 2 + 1) * W + lc];
+      }
+      partial[(int64_t)blockIdx.x * 2 * H + lc] = a;
+      if (has_bias) partial[(int64_t)blockIdx.x * 2 * H + H + lc] = bb;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (col < H) {
+        store8<kF32>(partial, (int64_t)blockIdx.x * 2 * H + col, dg[c]);
+        if (has_bias) store8<kF32>(partial, (int64_t)blockIdx.x * 2 * H + H + col, db[c]);
+      }
+    }
+  }
+}
+
+// Column-parallel reduction of the [G][2H] partial slab: block = 32 columns x
+// 8 row-slices.
+template <int WDT>
+__global__ __launch_bounds__(256) void norm_wgrad_finalize_kernel(const float* __restrict__ partial, int G, int H,
+                                                                  int has_bias, void* __restrict__ dw,
+                                                                  void* __restrict__ dbias) {
+  __shared__ float red[8][33];
+  const int lc = threadIdx.x & 31;
+  const int ls = threadIdx.x >> 5;
+  const int col2 = blockIdx.x * 32 + lc;  // column in [0, 2H)
+  float acc = 0.f;
+  if (col2 < 2 * H)
+    for (int g = ls; g < G; g += 8) acc += partial[(int64_t)g * 2 * H + col2];
+  red[ls][lc] = acc;
+  __syncthreads();
+  if (ls == 0 && col2 < 2 * H) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][lc];
+    if (col2 < H) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dw), col2, s);
+    else if (has_bias) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dbias), col2 - H, s);
+  }
+}
+
+struct NormCfg { int tpr, nc; };
+static NormCfg pick_cfg(int H) {
+  if (H <= 512) return {64, 1};
+  if (H <= 1024) return {64, 2};
+  if (H <= 2048) return {128, 2};
+  if (H <= 4096) return {256, 2};
+  if (H <= 8192) return {256, 4};
+  return {256, 8};  // <= 16384
+}
+
+#define MADNN_NORM_CFG(H, TPR, NC, ...)                                          \
+  do {                                                                           \
+    NormCfg _c = pick_cfg(H);                                                    \
+    if (_c.tpr == 64 && _c.nc == 1) { constexpr int TPR = 64, NC = 1; __VA_ARGS__; } \
+    else if (_c.tpr == 64 && _c.nc == 2) { constexpr int TPR = 64, NC = 2; __VA_ARGS__; } \
+    else if (_c.tpr == 128) { constexpr int TPR = 128, NC = 2; __VA_ARGS__; }  \
+    else if (_c.nc == 2) { constexpr int TPR = 256, NC = 2; __VA_ARGS__; }      \
+    else if (_c.nc == 4) { constexpr int TPR = 256, NC = 4; __VA_ARGS__; }      \
+    else { constexpr int TPR = 256, NC = 8; __VA_ARGS__; }                       \
+  } while (0)
+
+#define MADNN_DISPATCH_XW(xdt, wdt, XDT, WDT, ...)                               \
+  if (xdt == kF32 && wdt == kF32) { constexpr int XDT = kF32, WDT = kF32; __VA_ARGS__; } \
+  else if (xdt == kBF16 && wdt == kBF16) { constexpr int XDT = kBF16, WDT = kBF16; __VA_ARGS__; } \
+  else if (xdt == kBF16 && wdt == kF32) { constexpr int XDT = kBF16, WDT = kF32; __VA_ARGS__; } \
+  else if (xdt == kF32 && wdt == kBF16) { constexpr int XDT = kF32, WDT = kBF16; __VA_ARGS__; } \
+  else return hipErrorInvalidValue;
+
+}  // namespace madnn
+
+extern "C" {
+
+int madnn_norm_max_h() { return 16384; }
+
+hipError_t madnn_norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* sum_out,
+                          float* mean_out, float* rstd_out, int64_t rows, int H, float eps, int rms, int xdt, int wdt,
+                          hipStream_t stream) {
+  using namespace madnn;
+  if (rows <= 0) return hipSuccess;
+  if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
+  MADNN_DISPATCH_XW(xdt, wdt, XDT, WDT, {
+    MADNN_NORM_CFG(H, TPR, NC, {
+      constexpr int RPB = kNormThreads / TPR;
+      int64_t blocks = (rows + RPB - 1) / RPB;
+      const int grid = blocks > 16 * kNumCU ? 16 * kNumCU : (int)blocks;
+      hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w, b,
+                         y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
+    });
+  });
+  return hipGetLastError();
+}
+
+// Workspace size (floats) the backward needs for its dgamma/dbeta partials.
+int64_t madnn_norm_bwd_workspace(int64_t rows, int H) {
+  using namespace madnn;
+  NormCfg c = pick_cfg(H);
+  const int RPB = kNormThreads / c.tpr;
+  int64_t blocks = (rows + RPB - 1) / RPB;
+  int64_t G = blocks < 2 * kNumCU ? blocks : 2 * kNumCU;
+  if (G < 1) G = 1;
+  return G * 2 * (int64_t)H;
+}
+
+hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const float* mean_in, const float* rstd_in,
+                          const void* dres, void* dx, void* dw, void* dbias, float* workspace, int64_t rows, int H,
+                          int rms, int xdt, int wdt, hipStream_t stream) {
+  using namespace madnn;
+  if (rows <= 0) return hipSuccess;
+  if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
+  const int has_bias = dbias != nullptr;
+  const int G = (int)(madnn_norm_bwd_workspace(rows, H) / (2 * (int64_t)H));
+  MADNN_DISPATCH_XW(xdt, wdt, XDT, WDT, {
+    MADNN_NORM_CFG(H, TPR, NC, {
+      constexpr int RPB = kNormThreads / TPR;
+      const size_t lds = RPB > 1 ? (size_t)RPB * 2 * NC * TPR * 8 * sizeof(float) : 0;
+      hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC>), dim3(G), dim3(kNormThreads), lds, stream, dy, x, w,
+                         mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      MADNN_HIP_CHECK(hipGetLastError());
+      const int fgrid = (2 * H + 31) / 32;
+      hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(256), 0, stream, workspace, G, H,
+                         has_bias, dw, dbias);
+    });
+  });
+  return hipGetLastError();
+}
+
+}  // extern "C"

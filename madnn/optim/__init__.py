@@ -1,0 +1,232 @@
+"""Fused optimizers over flat buckets (K1 FusedSGD, K2 FusedAdam/AdamW).
+
+Reference: Torch7's ``accUpdateGradParameters`` — the gradient step fused into
+the weight update, run once per sample by the patched trainer
+(datamodule.lua:142).  Here one kernel launch per bucket reads the
+flat gradient (already averaged by the DP reducer, or packed locally), updates
+the fp32 master and optimizer state, and writes the bf16 model copy the next
+forward reads.
+
+The classes subclass ``torch.optim.Optimizer`` so LR schedulers, param groups
+and ``state_dict()`` work as usual; the state dict is emitted in per-parameter
+form (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq``), i.e. the same shape
+as ``torch.optim.SGD``/``AdamW`` state, which keeps checkpoints
+strategy-agnostic.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from .. import ops
+from ..parallel.flat import FlatBucket, FlatParamSpace, _phys_view
+
+
+class _FlatOptimizer(torch.optim.Optimizer):
+    _state_names: tuple = ()
+
+    def __init__(self, params, defaults):
+        super().__init__(params, defaults)
+        self.space: Optional[FlatParamSpace] = None
+        self.grad_source = None          # engine that provides reduced flat grads (DP reducer)
+        self.flat_state: Dict[int, Dict[str, torch.Tensor]] = {}
+        self.bucket_steps: Dict[int, int] = {}
+        self._dscale: Optional[torch.Tensor] = None
+        self._pending_load = None
+
+    # ----------------------------------------------------------------- binding
+    def bind(self, space: FlatParamSpace):
+        """Adopt a FlatParamSpace built over this optimizer's param groups."""
+        self.space = space
+        self.flat_state = {}
+        for bk in space.buckets:
+            self.flat_state[bk.index] = {n: torch.zeros_like(bk.master) for n in self._state_names}
+            self.bucket_steps[bk.index] = 0
+        if self._pending_load is not None:
+            sd, self._pending_load = self._pending_load, None
+            self.load_state_dict(sd)
+
+    def _bind_local(self):
+        groups = [g["params"] for g in self.param_groups]
+        dev = groups[0][0].device
+        space = FlatParamSpace(groups, dtype_of=lambda p: p.dtype, bucket_cap_mb=256.0,
+                               reduce_dtype=torch.float32, device=dev)
+        self.bind(space)
+
+    def _reduced_by_engine(self) -> bool:
+        return self.grad_source is not None and getattr(self.grad_source, "sync", None) == "grads"
+
+    def _grads(self, bk: FlatBucket) -> torch.Tensor:
+        if not self._reduced_by_engine():
+            return self.space.pack_grads(bk, 1.0)
+        return self.space.grad_buffer(bk)
+
+    # -------------------------------------------------------------- clipping
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global-norm clipping fused into the next step (device-side coefficient, no host sync)."""
+        if self.space is None:
+            self._bind_local()
+        if self._reduced_by_engine():
+            self.grad_source.finalize_grads()
+        flats = [self._grads(bk) for bk in self.space.buckets]
+        self._grads_cached = flats
+        out = ops.grad_norm(flats, max_norm=max_norm)
+        self._dscale = out[1:2]
+        return out[0]
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if self.space is None:
+            self._bind_local()
+        if self._reduced_by_engine():
+            self.grad_source.finalize_grads()
+        cached = getattr(self, "_grads_cached", None)
+        for i, bk in enumerate(self.space.buckets):
+            g = cached[i] if cached is not None else self._grads(bk)
+            group = self.param_groups[bk.group_id]
+            self.bucket_steps[bk.index] += 1
+            self._update(bk, g, group, self.flat_state[bk.index], self.bucket_steps[bk.index])
+        self._grads_cached = None
+        self._dscale = None
+        if self.grad_source is not None:
+            self.grad_source.after_step()
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        for group in self.param_groups:
+            for p in group["params"]:
+                if p.grad is not None:
+                    if set_to_none:
+                        p.grad = None
+                    else:
+                        p.grad.zero_()
+
+    def _model_out(self, bk: FlatBucket):
+        return bk.model if bk.has_master_copy else None
+
+    def _update(self, bk, grad, group, st, step):  # pragma: no cover - abstract
+        raise NotImplementedError
+
+    # ------------------------------------------------------------ state dict
+    def _param_index(self):
+        idx, k = {}, 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                idx[id(p)] = k
+                k += 1
+        return idx
+
+    def state_dict(self):
+        groups = []
+        k = 0
+        for g in self.param_groups:
+            d = {key: v for key, v in g.items() if key != "params"}
+            d["params"] = list(range(k, k + len(g["params"])))
+            k += len(g["params"])
+            groups.append(d)
+        state = {}
+        if self.space is not None:
+            idx = self._param_index()
+            for bk in self.space.buckets:
+                st = self.flat_state[bk.index]
+                for p, off in zip(bk.params, bk.offsets):
+                    cl = self.space.param_info[id(p)][2]
+                    entry = {n: _phys_view(st[n][off:off + p.numel()], p.shape, cl).clone() for n in st}
+                    entry["step"] = torch.tensor(float(self.bucket_steps[bk.index]))
+                    state[idx[id(p)]] = self._export_names(entry)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            for key, v in sg.items():
+                if key != "params":
+                    g[key] = v
+        if self.space is None:
+            self._pending_load = sd
+            return
+        idx = self._param_index()
+        for bk in self.space.buckets:
+            st = self.flat_state[bk.index]
+            for p, off in zip(bk.params, bk.offsets):
+                e = sd["state"].get(idx[id(p)]) or sd["state"].get(str(idx[id(p)]))
+                if e is None:
+                    continue
+                e = self._import_names(e)
+                cl = self.space.param_info[id(p)][2]
+                for n in st:
+                    if n in e:
+                        _phys_view(st[n][off:off + p.numel()], p.shape, cl).copy_(e[n])
+                if "step" in e:
+                    self.bucket_steps[bk.index] = int(float(e["step"]))
+
+    def _export_names(self, e):
+        return e
+
+    def _import_names(self, e):
+        return e
+
+
+class FusedSGD(_FlatOptimizer):
+    """SGD with momentum / dampening / nesterov / weight decay (torch.optim.SGD semantics)."""
+
+    _state_names = ("momentum",)
+
+    def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+
+    def bind(self, space):
+        super().bind(space)
+        if all(g["momentum"] == 0 for g in self.param_groups):
+            for st in self.flat_state.values():
+                st.pop("momentum", None)
+
+    def _update(self, bk, grad, group, st, step):
+        ops.sgd_step(bk.master, grad, st.get("momentum"), self._model_out(bk), lr=group["lr"],
+                     momentum=group["momentum"], dampening=group["dampening"],
+                     weight_decay=group["weight_decay"], nesterov=group["nesterov"], first_step=(step == 1),
+                     grad_scale=1.0, dscale=self._dscale)
+
+    def _export_names(self, e):
+        if "momentum" in e:
+            e["momentum_buffer"] = e.pop("momentum")
+        return e
+
+    def _import_names(self, e):
+        e = dict(e)
+        if "momentum_buffer" in e:
+            e["momentum"] = e.pop("momentum_buffer")
+        return e
+
+
+class FusedAdam(_FlatOptimizer):
+    """Adam / AdamW (decoupled weight decay when ``adamw=True``), torch semantics."""
+
+    _state_names = ("exp_avg", "exp_avg_sq")
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 adamw: bool = True):
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, adamw=adamw))
+
+    def _update(self, bk, grad, group, st, step):
+        b1, b2 = group["betas"]
+        ops.adam_step(bk.master, grad, st["exp_avg"], st["exp_avg_sq"], self._model_out(bk), lr=group["lr"],
+                      beta1=b1, beta2=b2, eps=group["eps"], weight_decay=group["weight_decay"],
+                      adamw=group["adamw"], step=step, grad_scale=1.0, dscale=self._dscale)
+
+
+def FusedAdamW(params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2):
+    return FusedAdam(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=True)
+
+
+__all__ = ["FusedSGD", "FusedAdam", "FusedAdamW"]

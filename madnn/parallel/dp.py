@@ -1,0 +1,238 @@
+"""Data-parallel engine: bucketed, backward-overlapped gradient averaging over
+RCCL, plus the reference's periodic parameter averaging (local SGD).
+
+Reference behaviour:
+* ``synchronizeModel`` (datamodule.lua:211-224) all-reduces and averages every
+  parameter and gradient tensor, one blocking collective per tensor, after
+  backward, every K samples (the "batchSize" period, datamodule.lua:102,151);
+* that hook is installed by globally monkey-patching ``nn.Sequential:backward``
+  and ``nn.StochasticGradient:train`` (datamodule.lua:83,117).
+
+MI355X-native redesign:
+* hooks are installed on the wrapped root's parameters only
+  (``register_post_accumulate_grad_hook``) — no global patching (SURVEY A-8);
+* gradients are averaged in flat buckets: as soon as the last gradient of a
+  bucket is accumulated, the K4 pack kernel (1/W fused) runs on a dedicated
+  high-priority HIP stream and the bucket's RCCL all-reduce is issued
+  asynchronously, so communication overlaps the rest of backward;
+* the fused optimizer consumes the reduced flat buffers directly;
+* ``sync="params"`` keeps the reference's period-K model averaging (A-3),
+  ``sync="manual"`` mirrors ``batchSize = -1`` (datamodule.lua:45).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .. import comm
+from .. import runtime as rt
+from ..utils.logging import get_logger
+from .flat import FlatBucket, FlatParamSpace
+
+
+def default_sync_period(local_size: int) -> int:
+    """Reference sync-period heuristic (datamodule.lua:68-78): 1/10/50/100 samples."""
+    if local_size < 1000:
+        return 1
+    if local_size < 2500:
+        return 10
+    if local_size < 5000:
+        return 50
+    return 100
+
+
+def _cast_inputs(obj, dtype, channels_last):
+    if isinstance(obj, torch.Tensor):
+        if obj.is_floating_point() and dtype is not None and obj.dtype != dtype:
+            obj = obj.to(dtype)
+        if channels_last and obj.dim() == 4 and obj.is_floating_point():
+            obj = obj.contiguous(memory_format=torch.channels_last)
+        return obj
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_cast_inputs(o, dtype, channels_last) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _cast_inputs(v, dtype, channels_last) for k, v in obj.items()}
+    return obj
+
+
+class DataParallel(nn.Module):
+    """Wraps a module whose parameters live in a :class:`FlatParamSpace`."""
+
+    def __init__(self, module: nn.Module, space: FlatParamSpace, *, group=None, src_rank: int = 0,
+                 sync: str = "grads", sync_every: int = 1, overlap: bool = True,
+                 cast_dtype: Optional[torch.dtype] = None, channels_last: bool = False,
+                 unpack_grads: bool = False, broadcast_buffers: bool = True, find_unused: bool = True,
+                 sync_comm: bool = False):
+        super().__init__()
+        self.module = module
+        self.space = space
+        self.group = group
+        self.src_rank = src_rank
+        self.world = rt.get_world_size(group)
+        self.sync = sync
+        self.sync_every = max(int(sync_every), 1)
+        self.cast_dtype = cast_dtype
+        self.channels_last = channels_last
+        self.unpack_grads = unpack_grads
+        self.find_unused = find_unused
+        dev = space.buckets[0].model.device if space.buckets else torch.device("cpu")
+        self.is_cuda = dev.type == "cuda"
+        self.comm_stream = None
+        if self.is_cuda and overlap and not sync_comm:
+            # high priority so the pack + RCCL enqueue is not starved by backward kernels
+            self.comm_stream = torch.cuda.Stream(device=dev, priority=-1)
+        self._sync_enabled = True
+        self._in_backward = False
+        self._needs_finalize = False
+        self._steps = 0
+        self._backwards = 0
+        self._hooks = []
+        self.stats = {"buckets_launched": 0, "bytes_reduced": 0}
+        self.broadcast_state(broadcast_buffers)
+        if sync == "grads":
+            self._install_hooks()
+
+    # ---------------------------------------------------------------- setup
+    @torch.no_grad()
+    def broadcast_state(self, buffers: bool = True):
+        """Identical start on every replica (fixes SURVEY A-6: always broadcast)."""
+        if self.world == 1:
+            return
+        for bk in self.space.buckets:
+            comm.broadcast(bk.master, src=self.src_rank, group=self.group)
+        self.space.sync_model_from_master()
+        if buffers:
+            for b in self.module.buffers():
+                if b.is_floating_point() or b.dtype in (torch.int64, torch.long):
+                    comm.broadcast(b, src=self.src_rank, group=self.group)
+
+    def _install_hooks(self):
+        for bk in self.space.buckets:
+            bk.pending = len(bk.params)
+            for p in bk.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bk)))
+
+    def _make_hook(self, bk: FlatBucket):
+        def hook(_p):
+            if not self._sync_enabled:
+                return
+            if not self._in_backward:
+                self._in_backward = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._on_backward_end)
+            bk.pending -= 1
+            if bk.pending == 0 and not bk.launched:
+                self._launch(bk)
+
+        return hook
+
+    # ------------------------------------------------------------ reduction
+    def _launch(self, bk: FlatBucket):
+        scale = 1.0 / self.world
+        if self.comm_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(bk.model.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                for p in bk.params:
+                    if p.grad is not None:
+                        p.grad.record_stream(self.comm_stream)
+                buf = self.space.pack_grads(bk, scale)
+                bk.work = comm.all_reduce(buf, "sum", group=self.group, async_op=True)
+        else:
+            buf = self.space.pack_grads(bk, scale)
+            bk.work = comm.all_reduce(buf, "sum", group=self.group, async_op=True)
+        bk.launched = True
+        self.stats["buckets_launched"] += 1
+        self.stats["bytes_reduced"] += buf.numel() * buf.element_size()
+
+    def _on_backward_end(self):
+        self._in_backward = False
+        self._backwards += 1
+        for bk in self.space.buckets:
+            if not bk.launched:
+                if not self.find_unused:
+                    raise RuntimeError(f"bucket {bk.index} had parameters without gradients; "
+                                       "set find_unused=True")
+                self._launch(bk)
+        self._needs_finalize = True
+
+    def finalize_grads(self):
+        """Make the current stream wait for every bucket's reduction (idempotent)."""
+        if not self._needs_finalize:
+            return
+        cur = torch.cuda.current_stream() if self.is_cuda else None
+        for bk in self.space.buckets:
+            if bk.work is not None:
+                bk.work.wait()
+                bk.work = None
+            bk.launched = False
+            bk.pending = len(bk.params)
+        if self.comm_stream is not None:
+            cur.wait_stream(self.comm_stream)
+        for bk in self.space.buckets:
+            if self.unpack_grads:
+                self.space.unpack_grads_to_params(bk)
+            else:
+                for p in bk.params:
+                    p.grad = None
+        self._needs_finalize = False
+
+    def after_step(self):
+        """Called by the fused optimizer after each step (sync="params" period)."""
+        self._steps += 1
+        if self.sync == "params" and self._steps % self.sync_every == 0:
+            self.average_parameters()
+
+    @torch.no_grad()
+    def average_parameters(self):
+        """Reference periodic model averaging (datamodule.lua:214-218), bucketed."""
+        if self.world == 1:
+            return
+        for bk in self.space.buckets:
+            comm.all_reduce(bk.master, "sum", group=self.group)
+            bk.master.mul_(1.0 / self.world)
+        self.space.sync_model_from_master()
+
+    # -------------------------------------------------------------- forward
+    def forward(self, *args, **kwargs):
+        if self.cast_dtype is not None or self.channels_last:
+            args = _cast_inputs(args, self.cast_dtype, self.channels_last)
+            kwargs = _cast_inputs(kwargs, self.cast_dtype, self.channels_last)
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (microbatching) without reducing."""
+        prev = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
+    def state_dict(self, *args, **kwargs):
+        return self.module.state_dict(*args, **kwargs)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        res = self.module.load_state_dict(sd, strict=strict)
+        self.space.sync_master_from_model()
+        return res
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+    def extra_repr(self) -> str:
+        return (f"world={self.world}, sync={self.sync}, period={self.sync_every}, "
+                f"buckets={len(self.space.buckets)}, overlap={self.comm_stream is not None}")
+
+
+def log_plan(engine: DataParallel):
+    log = get_logger()
+    for bk in engine.space.buckets:
+        log.info("bucket %d: %s x %d params, %.1f MB", bk.index, bk.dtype, len(bk.params),
+                 bk.numel * torch.tensor([], dtype=engine.space.reduce_dtype).element_size() / 2**20)

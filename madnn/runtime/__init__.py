@@ -1,0 +1,198 @@
+"""Process/device runtime: the ``mpi.start(true)`` equivalent.
+
+Reference: ``mpi.start(true)`` (datamodule.lua:27; README.md:34,86) starts MPI,
+binds a GPU and creates the communicator; ``mpi.rank()/size()/barrier()`` are
+used throughout.  MI355X-native replacement: one process per GPU,
+``torch.distributed`` with backend ``"nccl"`` (= RCCL over xGMI on ROCm) for
+device tensors and ``gloo`` for CPU runs, plus named sub-groups for the
+dp / pp / tp axes of a hybrid layout (the reference has a single world
+communicator, which is why its DP and MP cannot be combined — SURVEY A-15).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import random
+import subprocess
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils.logging import get_logger
+
+_STATE = {"initialized": False, "device": None, "backend": None}
+
+
+def is_initialized() -> bool:
+    return _STATE["initialized"]
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None) -> None:
+    """Bind this process to its GPU and join the process group (idempotent).
+
+    Reads the torchrun / ``madnn.launch`` environment (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  A process started without a
+    launcher is a world of one and creates no process group.
+    """
+    if _STATE["initialized"]:
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and device != "cpu"
+    if use_gpu:
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev  # eager RCCL communicator init bound to this GPU
+        dist.init_process_group(**kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    _STATE.update(initialized=True, device=dev, backend=backend)
+    get_logger().debug("madnn.init rank=%d world=%d device=%s backend=%s", rank, world, dev, backend)
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _STATE.update(initialized=False, device=None, backend=None)
+    ProcessGroups._cache.clear()
+
+
+def get_rank(group=None) -> int:
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+def get_world_size(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def get_local_rank() -> int:
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def device() -> torch.device:
+    if _STATE["device"] is None:
+        init()
+    return _STATE["device"]
+
+
+def backend() -> str:
+    if _STATE["backend"] is None:
+        init()
+    return _STATE["backend"]
+
+
+def barrier(group=None) -> None:
+    """Global barrier (reference ``mpi.barrier()``, datamodule.lua:50)."""
+    if not dist.is_initialized():
+        return
+    if dist.get_backend(group) == "nccl":
+        dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier(group=group)
+
+
+def seed_all(seed: int, rank_offset: bool = False) -> None:
+    """Same seed on every rank (as the reference example, sgd-...-cifar.lua:48)."""
+    s = seed + (get_rank() if rank_offset else 0)
+    random.seed(s)
+    torch.manual_seed(s)
+    try:
+        import numpy as np
+
+        np.random.seed(s % (2**32))
+    except Exception:
+        pass
+
+
+@dataclass(frozen=True)
+class Mesh:
+    dp: int
+    pp: int
+    tp: int
+
+    @property
+    def size(self) -> int:
+        return self.dp * self.pp * self.tp
+
+    def coords(self, rank: int):
+        """rank -> (dp_idx, pp_idx, tp_idx); tp innermost, then pp, then dp."""
+        tp_i = rank % self.tp
+        pp_i = (rank // self.tp) % self.pp
+        dp_i = rank // (self.tp * self.pp)
+        return dp_i, pp_i, tp_i
+
+    def rank_of(self, dp_i: int, pp_i: int, tp_i: int) -> int:
+        return (dp_i * self.pp + pp_i) * self.tp + tp_i
+
+
+class ProcessGroups:
+    """dp / pp / tp sub-groups over the world (every rank creates every group
+    in the same order, as torch.distributed requires).
+
+    On one MI355X node all 8 GPUs are xGMI peers (7 links each), so no axis is
+    placed for hop count; the DP all-reduce (same stage, different replicas)
+    and the PP send/recv (adjacent stages) use disjoint links.
+    """
+
+    _cache: dict = {}
+
+    def __init__(self, mesh: Mesh):
+        world = get_world_size()
+        if mesh.size != world:
+            raise ValueError(f"mesh {mesh} does not cover world size {world}")
+        self.mesh = mesh
+        self.rank = get_rank()
+        self.dp_idx, self.pp_idx, self.tp_idx = mesh.coords(self.rank)
+        self.dp_group = self.pp_group = self.tp_group = None
+        self.dp_ranks = [mesh.rank_of(d, self.pp_idx, self.tp_idx) for d in range(mesh.dp)]
+        self.pp_ranks = [mesh.rank_of(self.dp_idx, p, self.tp_idx) for p in range(mesh.pp)]
+        self.tp_ranks = [mesh.rank_of(self.dp_idx, self.pp_idx, t) for t in range(mesh.tp)]
+        if not dist.is_initialized():
+            return
+        for axis in ("dp", "pp", "tp"):
+            for ranks in self._all_groups(axis):
+                key = tuple(ranks)
+                if key not in ProcessGroups._cache:
+                    ProcessGroups._cache[key] = dist.new_group(list(ranks)) if len(ranks) < world else None
+                if self.rank in ranks:
+                    setattr(self, f"{axis}_group", ProcessGroups._cache[key])
+
+    def _all_groups(self, axis):
+        m = self.mesh
+        out = []
+        if axis == "dp":
+            for p in range(m.pp):
+                for t in range(m.tp):
+                    out.append([m.rank_of(d, p, t) for d in range(m.dp)])
+        elif axis == "pp":
+            for d in range(m.dp):
+                for t in range(m.tp):
+                    out.append([m.rank_of(d, p, t) for p in range(m.pp)])
+        else:
+            for d in range(m.dp):
+                for p in range(m.pp):
+                    out.append([m.rank_of(d, p, t) for t in range(m.tp)])
+        return out
+
+
+def topology() -> dict:
+    """Best-effort GPU link topology (rocm-smi); informational only."""
+    info = {"gpus": torch.cuda.device_count() if torch.cuda.is_available() else 0}
+    try:
+        out = subprocess.run(["rocm-smi", "--showtopotype"], capture_output=True, text=True, timeout=20)
+        info["xgmi"] = "XGMI" in out.stdout
+        info["raw"] = out.stdout[-2000:]
+    except Exception:
+        info["xgmi"] = None
+    return info

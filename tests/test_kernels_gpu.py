@@ -1,0 +1,179 @@
+"""Numerics of the hand-written gfx950 kernels against fp32 PyTorch references.
+
+Each HIP kernel (K1 FusedSGD, K2 FusedAdam, K3 LayerNorm/RMSNorm, K4 bucket
+pack/unpack/scale-cast, grad-norm) is compared with madnn.ops.reference, the
+eager fp32 implementation of the same op.  Shapes include odd sizes,
+non-multiples of 8/64/256, channels_last tensors and empty tensors.
+"""
+import math
+
+import pytest
+import torch
+
+import madnn
+from madnn import ops
+from madnn.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("tdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16])
+def test_bucket_pack_unpack(cuda, tdt, fdt):
+    torch.manual_seed(0)
+    shapes = [(7,), (64,), (3, 5), (1000, 3), (2049,), (0,), (33, 17, 5)]
+    ts = [torch.randn(s, device=cuda).to(tdt) for s in shapes]
+    offs, n = [], 0
+    for t in ts:
+        offs.append(n)
+        n += (t.numel() + 15) // 16 * 16
+    flat = torch.zeros(n, device=cuda, dtype=fdt)
+    ops.bucket_pack(ts, flat, offs, 0.5)
+    ref = torch.zeros(n, dtype=fdt)
+    R.bucket_pack([t.cpu() for t in ts], ref, offs, 0.5)
+    tol = 1e-2 if torch.bfloat16 in (tdt, fdt) else 1e-6
+    torch.testing.assert_close(flat.cpu().float(), ref.float(), atol=tol, rtol=tol)
+    outs = [torch.empty_like(t) for t in ts]
+    ops.bucket_unpack(outs, flat, offs, 2.0)
+    for o, t in zip(outs, ts):
+        torch.testing.assert_close(o.float(), t.float(), atol=2 * tol, rtol=2 * tol)
+
+
+def test_bucket_channels_last_and_many_tensors(cuda):
+    torch.manual_seed(1)
+    ts = [torch.randn(8, 3 + i % 5, 3, 3, device=cuda).contiguous(memory_format=torch.channels_last)
+          for i in range(120)]  # > 48 tensors: multiple launches
+    offs, n = [], 0
+    for t in ts:
+        offs.append(n)
+        n += (t.numel() + 15) // 16 * 16
+    flat = torch.zeros(n, device=cuda)
+    ops.bucket_pack(ts, flat, offs, 1.0)
+    ref = torch.zeros(n)
+    R.bucket_pack([t.cpu() for t in ts], ref, offs, 1.0)
+    torch.testing.assert_close(flat.cpu(), ref)
+    outs = [torch.empty_like(t) for t in ts]
+    ops.bucket_unpack(outs, flat, offs, 1.0)
+    for o, t in zip(outs, ts):
+        torch.testing.assert_close(o, t)
+
+
+def test_flat_scale_cast(cuda):
+    x = torch.randn(100003, device=cuda)
+    y = torch.empty(100003, device=cuda, dtype=torch.bfloat16)
+    ops.flat_scale_cast(x, y, 0.25)
+    torch.testing.assert_close(y.float(), (x * 0.25).bfloat16().float())
+
+
+@pytest.mark.parametrize("n", [1, 31, 4096, 1_000_003])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_sgd_step(cuda, n, gdt, nesterov):
+    torch.manual_seed(2)
+    p = torch.randn(n, device=cuda)
+    g = torch.randn(n, device=cuda).to(gdt)
+    m = torch.randn(n, device=cuda)
+    model = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+    pr, mr = p.cpu().clone(), m.cpu().clone()
+    for first in (True, False):
+        ops.sgd_step(p, g, m, model, lr=0.1, momentum=0.9, dampening=0.0, weight_decay=1e-2, nesterov=nesterov,
+                     first_step=first, grad_scale=0.5)
+        R.sgd_step(pr, g.cpu(), mr, None, lr=0.1, momentum=0.9, dampening=0.0, weight_decay=1e-2,
+                   nesterov=nesterov, first_step=first, grad_scale=0.5)
+    torch.testing.assert_close(p.cpu(), pr, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m.cpu(), mr, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(model.float(), p.bfloat16().float())
+
+
+@pytest.mark.parametrize("n", [5, 4096, 777_777])
+@pytest.mark.parametrize("adamw", [True, False])
+def test_adam_step(cuda, n, adamw):
+    torch.manual_seed(3)
+    p = torch.randn(n, device=cuda)
+    m1 = torch.zeros(n, device=cuda)
+    m2 = torch.zeros(n, device=cuda)
+    model = torch.empty(n, device=cuda, dtype=torch.bfloat16)
+    pr, m1r, m2r = p.cpu().clone(), m1.cpu().clone(), m2.cpu().clone()
+    for step in range(1, 4):
+        g = torch.randn(n, device=cuda).bfloat16()
+        ops.adam_step(p, g, m1, m2, model, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1,
+                      adamw=adamw, step=step, grad_scale=1.0)
+        R.adam_step(pr, g.cpu(), m1r, m2r, None, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1,
+                    adamw=adamw, step=step)
+    torch.testing.assert_close(p.cpu(), pr, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m1.cpu(), m1r, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(m2.cpu(), m2r, atol=1e-6, rtol=1e-5)
+    torch.testing.assert_close(model.float(), p.bfloat16().float())
+
+
+def test_grad_norm_and_device_clip(cuda):
+    a = torch.randn(1_000_000, device=cuda)
+    b = torch.randn(3333, device=cuda).bfloat16()
+    out = ops.grad_norm([a, b], max_norm=1.0)
+    ref = math.sqrt(float(a.double().pow(2).sum() + b.double().pow(2).sum()))
+    assert abs(float(out[0]) - ref) / ref < 1e-4
+    assert abs(float(out[1]) - 1.0 / (ref + 1e-6)) < 1e-6
+    # dscale path: the clip coefficient multiplies the gradient inside the SGD kernel
+    p = torch.zeros(1_000_000, device=cuda)
+    ops.sgd_step(p, a, None, None, lr=1.0, dscale=out[1:2])
+    torch.testing.assert_close(p, -a * out[1], atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("H", [64, 768, 1024, 1536, 4096, 8192])
+@pytest.mark.parametrize("xdt,wdt", [(torch.bfloat16, torch.float32), (torch.float32, torch.float32),
+                                     (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_fwd_bwd(cuda, H, xdt, wdt, rms):
+    torch.manual_seed(4)
+    rows = 257
+    x = (torch.randn(rows, H, device=cuda) * 2 + 0.5).to(xdt).requires_grad_(True)
+    w = (torch.rand(H, device=cuda) + 0.5).to(wdt).requires_grad_(True)
+    b = None if rms else (torch.randn(H, device=cuda) * 0.1).to(wdt).requires_grad_(True)
+    dy = torch.randn(rows, H, device=cuda).to(xdt)
+    y = ops.rms_norm(x, w, eps=1e-6) if rms else ops.layer_norm(x, w, b, eps=1e-5)
+    y.backward(dy)
+    # fp32 reference of the same op
+    xr = x.detach().float().cpu().requires_grad_(True)
+    wr = w.detach().float().cpu().requires_grad_(True)
+    br = None if rms else b.detach().float().cpu().requires_grad_(True)
+    yr = R.norm(xr, wr, br, 1e-6 if rms else 1e-5, rms)
+    yr.backward(dy.float().cpu())
+    tol = 2e-2 if xdt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float().cpu(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(x.grad.float().cpu(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    gtol = 5e-2 if (xdt == torch.bfloat16 or wdt == torch.bfloat16) else 1e-3
+    torch.testing.assert_close(w.grad.float().cpu(), wr.grad, atol=gtol * math.sqrt(rows), rtol=gtol)
+    if not rms:
+        torch.testing.assert_close(b.grad.float().cpu(), br.grad, atol=gtol * math.sqrt(rows), rtol=gtol)
+
+
+def test_norm_fused_residual(cuda):
+    torch.manual_seed(5)
+    x = torch.randn(4, 33, 1024, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(4, 33, 1024, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.rand(1024, device=cuda, requires_grad=True)
+    b = torch.randn(1024, device=cuda, requires_grad=True)
+    y, s = ops.layer_norm(x, w, b, residual=r)
+    (y.float().pow(2).sum() + s.float().sum()).backward()
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    sr = xr + rr
+    yr = torch.nn.functional.layer_norm(sr, (1024,), wr, br, 1e-5)
+    (yr.pow(2).sum() + sr.sum()).backward()
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=8e-2, rtol=5e-2)
+    torch.testing.assert_close(r.grad.float(), rr.grad, atol=8e-2, rtol=5e-2)
+
+
+def test_norm_large_rows_multi_pass(cuda):
+    # rows >> grid cap: every workgroup loops over several rows (grid-stride path)
+    x = torch.randn(20000, 1024, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.ones(1024, device=cuda, requires_grad=True)
+    b = torch.zeros(1024, device=cuda, requires_grad=True)
+    y = ops.layer_norm(x, w, b)
+    y.float().sum().backward()
+    ref = torch.nn.functional.layer_norm(x.detach().float(), (1024,))
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    assert torch.isfinite(w.grad).all()
