@@ -1,0 +1,97 @@
+"""Shared transformer pieces.
+
+Attention goes through ``F.scaled_dot_product_attention`` (PyTorch-ROCm's
+flash/AOTriton kernels on MI355X); QKV is one fused projection GEMM
+(hipBLASLt); norms are the madnn K3 kernel with the residual add fused in.
+
+Every transformer in the zoo exposes ``pipeline_layers()``: a list of modules
+whose sequential composition equals ``forward`` (embedding -> blocks -> head),
+each taking and returning ONE tensor.  That is the spine the planner
+partitions into pipeline stages.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+def causal_lm_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    """Next-token cross entropy (shifted); fp32 accumulation inside the loss."""
+    v = logits.size(-1)
+    return F.cross_entropy(logits[:, :-1].reshape(-1, v).float(), targets[:, 1:].reshape(-1))
+
+
+def mlm_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    v = logits.size(-1)
+    return F.cross_entropy(logits.reshape(-1, v).float(), targets.reshape(-1), ignore_index=-100)
+
+
+class SelfAttention(nn.Module):
+    """Multi-head (optionally grouped-query) self-attention with one QKV GEMM."""
+
+    def __init__(self, hidden: int, heads: int, kv_heads: int = None, bias: bool = True, causal: bool = True,
+                 dropout: float = 0.0, rope=None):
+        super().__init__()
+        self.hidden, self.heads = hidden, heads
+        self.kv_heads = kv_heads or heads
+        self.head_dim = hidden // heads
+        self.causal, self.dropout, self.rope = causal, dropout, rope
+        self.qkv = nn.Linear(hidden, (heads + 2 * self.kv_heads) * self.head_dim, bias=bias)
+        self.proj = nn.Linear(heads * self.head_dim, hidden, bias=bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b, s, _ = x.shape
+        qkv = self.qkv(x).view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
+        q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        if self.rope is not None:
+            q, k = self.rope(q, k)
+        gqa = self.kv_heads != self.heads
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=self.causal,
+                                           dropout_p=self.dropout if self.training else 0.0, enable_gqa=gqa)
+        return self.proj(o.transpose(1, 2).reshape(b, s, self.heads * self.head_dim))
+
+
+class RotaryEmbedding(nn.Module):
+    """RoPE with a host-precomputed cos/sin table (no on-device trig per element:
+    cdna_hip_programming.md Appendix B, "Element-wise")."""
+
+    def __init__(self, head_dim: int, theta: float = 10000.0, max_pos: int = 8192):
+        super().__init__()
+        inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+        t = torch.arange(max_pos, dtype=torch.float64)
+        f = torch.outer(t, inv)
+        self.register_buffer("cos", torch.cat([f.cos(), f.cos()], -1).float(), persistent=False)
+        self.register_buffer("sin", torch.cat([f.sin(), f.sin()], -1).float(), persistent=False)
+
+    @staticmethod
+    def _rot(x):
+        x1, x2 = x.chunk(2, dim=-1)
+        return torch.cat([-x2, x1], dim=-1)
+
+    def forward(self, q, k):
+        s = q.size(-2)
+        cos = self.cos[:s].to(q.dtype)
+        sin = self.sin[:s].to(q.dtype)
+        return q * cos + self._rot(q) * sin, k * cos + self._rot(k) * sin
+
+
+def init_normal_(module: nn.Module, std: float = 0.02):
+    for m in module.modules():
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, std)
+
+
+def scale_residual_proj_(blocks, names, n_layer: int, std: float = 0.02):
+    """GPT-2 style 1/sqrt(2L) init of residual output projections."""
+    for blk in blocks:
+        for n, p in blk.named_parameters():
+            if any(n.endswith(x) for x in names):
+                nn.init.normal_(p, 0.0, std / math.sqrt(2 * n_layer))

@@ -1,0 +1,123 @@
+"""GPT-2 (small .. xl), random init from config — BASELINE config 3:
+"GPT-2 medium auto pipeline-parallel, 4 stages over xGMI (P2P microbatching)".
+
+Pre-LN blocks; the second LayerNorm of every block fuses the attention
+residual add (one K3 kernel returns both LN(x + a) and x + a).  The LM head is
+tied to the token embedding; when the pipeline puts them on different stages
+the engine all-reduces the tied gradient between first and last stage
+(SURVEY N8).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..nn.norm import FusedLayerNorm
+from .common import SelfAttention, causal_lm_loss, init_normal_, scale_residual_proj_
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    dropout: float = 0.0
+    layer_norm_eps: float = 1e-5
+
+
+_SIZES = {
+    "gpt2": dict(n_embd=768, n_layer=12, n_head=12),
+    "gpt2-medium": dict(n_embd=1024, n_layer=24, n_head=16),
+    "gpt2-large": dict(n_embd=1280, n_layer=36, n_head=20),
+    "gpt2-xl": dict(n_embd=1600, n_layer=48, n_head=25),
+    "gpt2-tiny": dict(n_embd=64, n_layer=4, n_head=4, vocab_size=512, n_positions=128),
+}
+
+
+def gpt2_config(name: str = "gpt2-medium", **over) -> GPT2Config:
+    d = dict(_SIZES[name])
+    d.update(over)
+    return GPT2Config(**d)
+
+
+class GPT2Embed(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        pos = torch.arange(ids.size(1), device=ids.device)
+        return self.drop(self.wte(ids) + self.wpe(pos))
+
+
+class GPT2MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, x):
+        return self.drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+
+
+class GPT2Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.ln_1 = FusedLayerNorm(cfg.n_embd, eps=cfg.layer_norm_eps)
+        self.attn = SelfAttention(cfg.n_embd, cfg.n_head, causal=True, dropout=cfg.dropout)
+        self.ln_2 = FusedLayerNorm(cfg.n_embd, eps=cfg.layer_norm_eps)
+        self.mlp = GPT2MLP(cfg)
+        self.drop = nn.Dropout(cfg.dropout)
+
+    def forward(self, x):
+        a = self.drop(self.attn(self.ln_1(x)))
+        y, h = self.ln_2(a, residual=x)      # h = x + a, y = LN(h): one kernel
+        return h + self.mlp(y)
+
+
+class GPT2Head(nn.Module):
+    def __init__(self, cfg: GPT2Config, wte: nn.Embedding):
+        super().__init__()
+        self.ln_f = FusedLayerNorm(cfg.n_embd, eps=cfg.layer_norm_eps)
+        self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+        self.lm_head.weight = wte.weight      # tied
+
+    def forward(self, x):
+        return self.lm_head(self.ln_f(x))
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.config = cfg
+        self.embed = GPT2Embed(cfg)
+        self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
+        self.head = GPT2Head(cfg, self.embed.wte)
+        init_normal_(self)
+        scale_residual_proj_(self.h, ("attn.proj.weight", "mlp.c_proj.weight"), cfg.n_layer)
+
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        x = self.embed(ids)
+        for blk in self.h:
+            x = blk(x)
+        return self.head(x)
+
+    def pipeline_layers(self):
+        return [self.embed, *self.h, self.head]
+
+    @staticmethod
+    def loss_fn(logits, targets):
+        return causal_lm_loss(logits, targets)
+
+    def flops_per_token(self) -> float:
+        c = self.config
+        n = sum(p.numel() for p in self.parameters()) - c.n_positions * c.n_embd
+        return 6.0 * n + 12.0 * c.n_layer * c.n_embd * c.n_positions

@@ -1,0 +1,74 @@
+"""LayerNorm / RMSNorm modules backed by the gfx950 K3 kernel.
+
+Drop-in for ``nn.LayerNorm`` (same parameter names ``weight``/``bias``, so
+state dicts interchange).  On HIP tensors they call ``madnn.ops.layer_norm`` /
+``rms_norm`` (one fused kernel each way, optional fused residual add); on CPU
+the eager reference.  ``swap_layernorms(model)`` replaces every eligible
+``nn.LayerNorm`` of an arbitrary model in place (the planner does this).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .. import ops
+
+
+class FusedLayerNorm(nn.Module):
+    def __init__(self, normalized_shape, eps: float = 1e-5, elementwise_affine: bool = True, bias: bool = True,
+                 device=None, dtype=None):
+        super().__init__()
+        if isinstance(normalized_shape, int):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = tuple(normalized_shape)
+        if len(self.normalized_shape) != 1:
+            raise ValueError("FusedLayerNorm normalises the last dimension only")
+        self.eps = eps
+        h = self.normalized_shape[0]
+        self.weight = nn.Parameter(torch.ones(h, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.zeros(h, device=device, dtype=dtype)) if bias else None
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
+        """LN(x) or, with ``residual``, (LN(x + residual), x + residual) in one kernel."""
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual=residual)
+
+    def extra_repr(self):
+        return f"{self.normalized_shape}, eps={self.eps}, kernel=madnn.K3"
+
+
+class FusedRMSNorm(nn.Module):
+    def __init__(self, hidden: int, eps: float = 1e-6, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
+        if residual is not None and residual.dtype != x.dtype:
+            residual = residual.to(x.dtype)
+        return ops.rms_norm(x, self.weight, self.eps, residual=residual)
+
+    def extra_repr(self):
+        return f"{self.weight.numel()}, eps={self.eps}, kernel=madnn.K3"
+
+
+def swap_layernorms(model: nn.Module) -> int:
+    """Replace eligible ``nn.LayerNorm`` modules by :class:`FusedLayerNorm` (weights kept)."""
+    n = 0
+    for name, child in list(model.named_children()):
+        if type(child) is nn.LayerNorm and len(child.normalized_shape) == 1 and child.elementwise_affine \
+                and ops.hidden_supported(child.normalized_shape[0]):
+            new = FusedLayerNorm(child.normalized_shape, child.eps, bias=child.bias is not None,
+                                 device=child.weight.device, dtype=child.weight.dtype)
+            with torch.no_grad():
+                new.weight.copy_(child.weight)
+                if child.bias is not None:
+                    new.bias.copy_(child.bias)
+            setattr(model, name, new)
+            n += 1
+        else:
+            n += swap_layernorms(child)
+    return n

@@ -7,8 +7,8 @@
 // (madnn/ops/__init__.py) routes CPU tensors to the eager reference.
 #include <torch/library.h>
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -43,7 +43,10 @@ int dt_code(const at::Tensor& t) {
   return -1;
 }
 
-hipStream_t cur_stream(const at::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+hipStream_t cur_stream(const at::Tensor& t) {
+  // ROCm PyTorch labels HIP devices "cuda": use the masquerading stream/guard API.
+  return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
 
 void check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "madnn HIP kernel ", what, " failed: ", hipGetErrorString(e));
@@ -64,7 +67,7 @@ void bucket_copy(bool pack, at::TensorList tensors, const at::Tensor& flat, at::
   TORCH_CHECK(flat.is_contiguous(), "flat bucket must be contiguous");
   TORCH_CHECK(tensors.size() == offsets.size(), "tensors/offsets length mismatch");
   if (tensors.empty()) return;
-  c10::hip::HIPGuard guard(flat.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(flat.device());
   const int tdt = dt_code(tensors[0]);
   std::vector<void*> ptrs;
   std::vector<int64_t> numels, offs;
@@ -98,7 +101,7 @@ void flat_scale_cast(const at::Tensor& src, at::Tensor dst, double scale) {
   check_dev(dst, "dst");
   TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "flat_scale_cast needs contiguous tensors");
   TORCH_CHECK(src.numel() == dst.numel(), "flat_scale_cast size mismatch");
-  c10::hip::HIPGuard guard(src.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   check(madnn_flat_scale_cast(src.data_ptr(), dst.data_ptr(), src.numel(), dt_code(src), dt_code(dst), (float)scale,
                               cur_stream(src)),
         "flat_scale_cast");
@@ -119,7 +122,7 @@ void sgd_step(at::Tensor master, const at::Tensor& grad, const c10::optional<at:
   TORCH_CHECK(grad.is_contiguous() && grad.numel() == master.numel(), "grad must be contiguous and match master");
   if (momentum != 0.0) TORCH_CHECK(mom.has_value() && mom->numel() == master.numel(), "momentum buffer required");
   if (model.has_value()) TORCH_CHECK(model->is_contiguous() && model->numel() == master.numel(), "model copy size");
-  c10::hip::HIPGuard guard(master.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   check(madnn_sgd_step(master.data_ptr<float>(), grad.data_ptr(), dt_code(grad),
                        mom.has_value() ? mom->data_ptr<float>() : nullptr,
                        model.has_value() ? model->data_ptr() : nullptr, model.has_value() ? dt_code(*model) : -1,
@@ -139,7 +142,7 @@ void adam_step(at::Tensor master, const at::Tensor& grad, at::Tensor m1, at::Ten
   TORCH_CHECK(m1.numel() == master.numel() && m2.numel() == master.numel(), "adam state size");
   if (model.has_value()) TORCH_CHECK(model->is_contiguous() && model->numel() == master.numel(), "model copy size");
   TORCH_CHECK(step >= 1, "adam step must be >= 1");
-  c10::hip::HIPGuard guard(master.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(master.device());
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
   check(madnn_adam_step(master.data_ptr<float>(), grad.data_ptr(), dt_code(grad), m1.data_ptr<float>(),
@@ -153,7 +156,7 @@ void adam_step(at::Tensor master, const at::Tensor& grad, at::Tensor m1, at::Ten
 // Returns a 2-element fp32 device tensor [global L2 norm, clip coefficient].
 at::Tensor grad_norm(at::TensorList flats, double max_norm, double scale) {
   TORCH_CHECK(!flats.empty(), "grad_norm needs at least one tensor");
-  c10::hip::HIPGuard guard(flats[0].device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(flats[0].device());
   std::vector<int> grids;
   int total = 0;
   for (const auto& f : flats) {
@@ -190,7 +193,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Te
   TORCH_CHECK(x.size(-1) == H && w.is_contiguous(), "norm weight / hidden size mismatch");
   TORCH_CHECK(H % 8 == 0 && H <= 16384, "madnn norm kernel needs H % 8 == 0 and H <= 16384, got ", H);
   const int64_t rows = x.numel() / H;
-  c10::hip::HIPGuard guard(x.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = at::empty_like(x);
   at::Tensor sum;
   if (res.has_value()) {
@@ -219,7 +222,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, co
   const int64_t H = w.numel();
   const int64_t rows = x.numel() / H;
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.sizes() == x.sizes(), "norm_bwd: dy/x mismatch");
-  c10::hip::HIPGuard guard(x.device());
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor dyc = dy.scalar_type() == x.scalar_type() ? dy : dy.to(x.scalar_type());
   at::Tensor dx = at::empty_like(x);
   at::Tensor dw = at::empty_like(w);

@@ -1,0 +1,225 @@
+"""T1: data parallelism on CPU/gloo, world_size 2 (BASELINE config 1: 2-layer MLP auto-DP).
+
+Parity criteria: ws=2 with per-rank batch b equals one process
+with batch 2b; the reference's periodic parameter averaging with K=1 and plain
+SGD equals gradient averaging (Appendix A-3); reference sharding semantics.
+"""
+import copy
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from dist_utils import run_dist
+
+pytestmark = pytest.mark.slow
+
+B = 8
+
+
+def _data(seed=0, n=4 * B):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, 32, generator=g), torch.randint(10, (n,), generator=g)
+
+
+def _ref_model():
+    from madnn.models import MLP
+
+    torch.manual_seed(0)
+    return MLP(32, 64, 10)
+
+
+def _check_same_across_ranks(t):
+    ts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(ts, t.contiguous())
+    for o in ts[1:]:
+        torch.testing.assert_close(o, ts[0], rtol=0, atol=0)
+
+
+def _w_dp_parity(rank, world, opt_kind, bucket_mb, sync):
+    import madnn
+    from madnn.optim import FusedAdam, FusedSGD
+
+    model = _ref_model()
+    ref = copy.deepcopy(model)
+    if rank == 1:  # replicas start different: the engine must broadcast rank 0's weights
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(1.0)
+    if opt_kind == "sgd":
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-3)
+        ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-3)
+    elif opt_kind == "adam":
+        opt = FusedAdam(model.parameters(), lr=1e-2, weight_decay=1e-2)
+        ropt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=1e-2)
+    else:  # plain torch optimizer through the engine's unpack path
+        opt = torch.optim.SGD(model.parameters(), lr=0.1)
+        ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    dm, opt = madnn.distribute(model, opt, strategy="dp", bucket_mb=bucket_mb, sync=sync, sync_every=1)
+    x, y = _data()
+    for step in range(4):
+        xs = x[step * B:(step + 1) * B]
+        ys = y[step * B:(step + 1) * B]
+        half = B // world
+        loss = F.cross_entropy(dm(xs[rank * half:(rank + 1) * half]), ys[rank * half:(rank + 1) * half])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        rl = F.cross_entropy(ref(xs), ys)
+        rl.backward()
+        ropt.step()
+        ropt.zero_grad()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), atol=2e-5, rtol=2e-5)
+        _check_same_across_ranks(p.detach())
+
+
+@pytest.mark.parametrize("opt_kind", ["sgd", "adam", "torch"])
+def test_dp_grad_parity_ws2(opt_kind):
+    run_dist(_w_dp_parity, 2, opt_kind, 64.0, "grads")
+
+
+def test_dp_many_small_buckets_ws2():
+    run_dist(_w_dp_parity, 2, "sgd", 0.0005, "grads")  # ~128 fp32 elems per bucket => one bucket per tensor
+
+
+def _w_params_mode(rank, world):
+    """A-3: periodic parameter averaging with K=1 and vanilla SGD == gradient averaging."""
+    import madnn
+    from madnn.optim import FusedSGD
+
+    x, y = _data(1)
+    outs = {}
+    for sync in ("grads", "params"):
+        model = _ref_model()
+        opt = FusedSGD(model.parameters(), lr=0.05)
+        dm, opt = madnn.distribute(model, opt, strategy="dp", sync=sync, sync_every=1)
+        for step in range(3):
+            xs = x[step * B + rank * 4: step * B + rank * 4 + 4]
+            ys = y[step * B + rank * 4: step * B + rank * 4 + 4]
+            F.cross_entropy(dm(xs), ys).backward()
+            opt.step()
+            opt.zero_grad()
+        outs[sync] = [p.detach().clone() for p in model.parameters()]
+    for a, b in zip(outs["grads"], outs["params"]):
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-5)
+
+
+def test_params_mode_equals_grads_mode_k1():
+    run_dist(_w_params_mode, 2)
+
+
+def _w_no_sync(rank, world):
+    import madnn
+    from madnn.optim import FusedSGD
+
+    model = _ref_model()
+    ref = copy.deepcopy(model)
+    opt = FusedSGD(model.parameters(), lr=0.1)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    dm, opt = madnn.distribute(model, opt, strategy="dp")
+    x, y = _data(2)
+    # two micro-batches per rank accumulated locally, reduced once
+    with dm.no_sync():
+        F.cross_entropy(dm(x[rank * 4:rank * 4 + 4]), y[rank * 4:rank * 4 + 4]).backward()
+    F.cross_entropy(dm(x[8 + rank * 4:8 + rank * 4 + 4]), y[8 + rank * 4:8 + rank * 4 + 4]).backward()
+    opt.step()
+    l1 = F.cross_entropy(ref(x[0:8]), y[0:8])
+    l2 = F.cross_entropy(ref(x[8:16]), y[8:16])
+    ((l1 + l2)).backward()
+    ropt.step()
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), atol=2e-5, rtol=2e-5)
+
+
+def test_no_sync_accumulation():
+    run_dist(_w_no_sync, 2)
+
+
+def _w_unused(rank, world):
+    import madnn
+    from madnn.optim import FusedSGD
+
+    class Two(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(4, 4)
+            self.b = torch.nn.Linear(4, 4)  # never used
+
+        def forward(self, x):
+            return self.a(x)
+
+    torch.manual_seed(0)
+    m = Two()
+    opt = FusedSGD(m.parameters(), lr=0.1)
+    dm, opt = madnn.distribute(m, opt, strategy="dp", bucket_mb=0.00001)
+    before = m.b.weight.detach().clone()
+    dm(torch.randn(3, 4)).sum().backward()
+    opt.step()
+    torch.testing.assert_close(m.b.weight.detach(), before)
+
+
+def test_unused_parameters():
+    run_dist(_w_unused, 2)
+
+
+# ------------------------------------------------------------- reference API
+def _w_synchronize_model(rank, world):
+    import madnn
+
+    torch.manual_seed(rank)
+    m = torch.nn.Sequential(torch.nn.Linear(5, 7), torch.nn.Tanh(), torch.nn.Linear(7, 3))
+    for p in m.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    mine = [p.detach().clone() for p in m.parameters()]
+    allp = [[torch.empty_like(t) for _ in range(world)] for t in mine]
+    for t, lst in zip(mine, allp):
+        dist.all_gather(lst, t)
+    madnn.synchronize_model(m)
+    for p, lst in zip(m.parameters(), allp):
+        torch.testing.assert_close(p.detach(), sum(lst) / world, atol=1e-6, rtol=1e-6)
+        torch.testing.assert_close(p.grad, torch.full_like(p, 1.5))
+
+
+def test_synchronize_model_averages_params_and_grads():
+    run_dist(_w_synchronize_model, 2)
+
+
+def _w_parallelize(rank, world, sync_every):
+    import madnn
+    from madnn.models import MLP
+
+    torch.manual_seed(10 + rank)  # different init per rank: parallelize must broadcast
+    g = torch.Generator().manual_seed(0)
+    n = 203
+    w_true = torch.randn(16, 3, generator=g)
+    data = torch.randn(n, 16, generator=g)
+    targets = (data @ w_true).argmax(1)
+    model = MLP(16, 32, 3)
+    d, t, size = madnn.parallelize(data, targets, model, sync_every=sync_every, verbose=False)
+    assert size == n // world == len(d) == len(t)
+    torch.testing.assert_close(d, data[rank * size:(rank + 1) * size])  # contiguous stripe, remainder dropped
+    if sync_every is None:
+        assert model._madnn_sync.period == 1  # heuristic: local size < 1000
+    trainer = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.5, max_iteration=6,
+                            batch_size=16, verbose=False)
+    hist = trainer.train(d, t)
+    assert hist[-1] < hist[0]
+    if sync_every == -1:
+        madnn.synchronize_model(model)
+    for p in model.parameters():
+        _check_same_across_ranks(p.detach())
+
+
+@pytest.mark.parametrize("sync_every", [None, 3, -1])
+def test_parallelize_trainer(sync_every):
+    run_dist(_w_parallelize, 2, sync_every)
+
+
+def _w_ws4(rank, world):
+    _w_dp_parity(rank, world, "sgd", 64.0, "grads")
+
+
+def test_dp_parity_ws4():
+    run_dist(_w_ws4, 4)
