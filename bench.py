@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--miopen-benchmark", type=int, default=1,
+                    help="torch.backends.cudnn.benchmark (MIOpen find-mode kernel search for each conv shape)")
     return ap.parse_args()
 
 
@@ -137,6 +139,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     import madnn
 
+    torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
     madnn.init()
     rank = madnn.get_rank()
     if args.model == "resnet50":

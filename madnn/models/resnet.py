@@ -2,9 +2,12 @@
 torchvision is not installed.  BASELINE config 2:
 "ResNet-50 auto data-parallel bf16 on 8xMI355X".
 
-Convolutions, BatchNorm and pooling run on MIOpen through PyTorch-ROCm; the
-network is meant to run channels_last (NHWC) in bf16 with fp32 BatchNorm
-parameters, which is the layout MIOpen's gfx950 implicit-GEMM kernels prefer.
+Convolutions and pooling run on MIOpen through PyTorch-ROCm; every
+BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
+end of each block, the residual add folded in: ``relu(bn3(conv3(h)) + idt)`` is
+one kernel forward and one backward.  The network runs channels_last (NHWC) in
+bf16 with fp32 BatchNorm parameters — the layout MIOpen's gfx950 implicit-GEMM
+convolutions prefer.
 """
 from __future__ import annotations
 
@@ -12,6 +15,8 @@ from typing import List, Optional, Type
 
 import torch
 from torch import nn
+
+from ..nn.norm import FusedBatchNorm2d as BN
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -28,17 +33,15 @@ class BasicBlock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BN(planes)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BN(planes)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), residual=idt, relu=True)
 
 
 class Bottleneck(nn.Module):
@@ -47,20 +50,18 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv1x1(inplanes, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = BN(planes)
         self.conv2 = conv3x3(planes, planes, stride)   # stride on the 3x3 (v1.5)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BN(planes)
         self.conv3 = conv1x1(planes, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BN(planes * 4)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
+        return self.bn3(self.conv3(out), residual=idt, relu=True)   # relu(bn3 + idt): one kernel
 
 
 class ResNet(nn.Module):
@@ -69,8 +70,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = width
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(width)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BN(width)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, width, layers[0])
         self.layer2 = self._make_layer(block, width * 2, layers[1], stride=2)
@@ -81,7 +81,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # FusedBatchNorm2d included
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -95,14 +95,14 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       nn.BatchNorm2d(planes * block.expansion))
+                                       BN(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, downsample)]
         self.inplanes = planes * block.expansion
         layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -72,3 +72,19 @@ def swap_layernorms(model: nn.Module) -> int:
         else:
             n += swap_layernorms(child)
     return n
+
+
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` whose forward optionally fuses a residual add and a ReLU:
+    ``act(BN(x) + residual)``; NHWC (channels_last) HIP tensors run the K5 kernel,
+    everything else the eager composition.  Same parameters/buffers as
+    ``nn.BatchNorm2d`` (state dicts interchange; ``isinstance`` holds)."""
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
+        training = self.training or not self.track_running_stats
+        return ops.batch_norm_act(x, self.weight, self.bias,
+                                  self.running_mean if (not self.training or self.track_running_stats) else None,
+                                  self.running_var if (not self.training or self.track_running_stats) else None,
+                                  self.num_batches_tracked if (self.training and self.track_running_stats) else None,
+                                  training=training, momentum=self.momentum, eps=self.eps, relu=relu,
+                                  residual=residual)

@@ -167,13 +167,72 @@ def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = No
     return _norm(x, weight, None, eps, True, residual)
 
 
+# ---------------------------------------------------------------------- K5
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu):
+        y, mean, invstd, scale, shift = torch.ops.madnn.bn_fwd(x, residual, weight, bias, running_mean,
+                                                                running_var, nbt, bool(training), float(momentum),
+                                                                float(eps), bool(relu))
+        ctx.save_for_backward(x, residual, weight, mean, invstd, scale, shift)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.has_w = weight is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, residual, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, residual if ctx.has_res else None, weight, mean, invstd,
+                                                  scale, shift, ctx.relu, need_w)
+        return (dx, dw if need_w else None, db if need_w else None, dres if ctx.has_res else None,
+                None, None, None, None, None, None, None)
+
+
+def bn_supported(x: torch.Tensor, weight: Optional[torch.Tensor]) -> bool:
+    """Shapes/layouts the fused NHWC BatchNorm kernel handles."""
+    if x.device.type != "cuda" or x.dtype not in (torch.bfloat16, torch.float32, torch.float16):
+        return False
+    c = x.size(1)
+    if c % 8 or c > 2048:
+        return False
+    if weight is not None and weight.dtype != torch.float32:
+        return False
+    if x.dim() == 2:
+        return x.is_contiguous()
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked=None, *, training: bool,
+                   momentum: float = 0.1, eps: float = 1e-5, relu: bool = False,
+                   residual: Optional[torch.Tensor] = None):
+    """act(BN(x) + residual) for NHWC activations in one fused kernel per direction.
+
+    Device tensors of a supported layout use the K5 HIP kernels (batch statistics,
+    running-stat update and num_batches_tracked increment included); anything else
+    (CPU, NCHW, unsupported C, eval-mode backward) uses the eager composition.
+    """
+    needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
+                                              or (residual is not None and residual.requires_grad))
+    fused = bn_supported(x, weight) and (training or not needs_grad) and momentum is not None
+    if fused and residual is not None:
+        fused = residual.dtype == x.dtype and residual.shape == x.shape and residual.stride() == x.stride()
+    if fused:
+        _need_native("batch_norm_act")
+        return _BNFn.apply(x, weight, bias, residual, running_mean, running_var,
+                           num_batches_tracked if training else None, training, momentum, eps, relu)
+    return reference.batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked,
+                                    training=training, momentum=momentum, eps=eps, relu=relu, residual=residual)
+
+
 def hidden_supported(h: int) -> bool:
     return h % 8 == 0 and h <= 16384
 
 
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
-    "rms_norm", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "rms_norm", "batch_norm_act", "bn_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

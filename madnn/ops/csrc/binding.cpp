@@ -29,6 +29,13 @@ hipError_t madnn_norm_fwd(const void*, const void*, const void*, const void*, vo
 int64_t madnn_norm_bwd_workspace(int64_t, int);
 hipError_t madnn_norm_bwd(const void*, const void*, const void*, const float*, const float*, const void*, void*, void*,
                           void*, float*, int64_t, int, int, int, int, hipStream_t);
+int madnn_bn_supported(int);
+int madnn_bn_partial_rows(int64_t, int);
+hipError_t madnn_bn_fwd(const void*, const void*, void*, int64_t, int, int, int, int, float, float, const float*,
+                        const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*, hipStream_t);
+hipError_t madnn_bn_bwd(const void*, const void*, const void*, void*, void*, int64_t, int, int, int, const float*,
+                        const float*, const float*, const float*, const float*, float*, float*, float*, float*,
+                        hipStream_t);
 }
 
 namespace {
@@ -240,9 +247,99 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, co
   return {dx, dw, db};
 }
 
+// ---- K5 fused BatchNorm(+add)(+ReLU), NHWC -------------------------------
+// x viewed as a dense [M, C] matrix: 2-D [N, C] contiguous or 4-D channels_last.
+int64_t bn_rows(const at::Tensor& x, int64_t C) {
+  if (x.dim() == 2) {
+    TORCH_CHECK(x.is_contiguous(), "bn: 2-D input must be contiguous");
+  } else {
+    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn: 4-D input must be channels_last");
+  }
+  TORCH_CHECK(x.size(1) == C, "bn: channel mismatch");
+  return x.numel() / C;
+}
+
+const float* optf(const c10::optional<at::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "bn: affine/stat tensors must be fp32");
+  return t->data_ptr<float>();
+}
+
+float* optf_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(optf(t)); }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fwd(
+    const at::Tensor& x, const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& w,
+    const c10::optional<at::Tensor>& b, const c10::optional<at::Tensor>& run_mean,
+    const c10::optional<at::Tensor>& run_var, const c10::optional<at::Tensor>& nbt, bool training, double momentum,
+    double eps, bool relu) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  TORCH_CHECK(madnn_bn_supported((int)C), "bn kernel needs C % 8 == 0 and C <= 2048, got ", C);
+  const int64_t M = bn_rows(x, C);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty_like(x);
+  if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes() && res->strides() == x.strides(), "bn residual layout");
+  if (!training) TORCH_CHECK(run_mean.has_value() && run_var.has_value(), "bn eval needs running stats");
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor save_mean = at::empty({C}, fo), save_invstd = at::empty({C}, fo);
+  at::Tensor scale = at::empty({C}, fo), shift = at::empty({C}, fo);
+  at::Tensor ws = at::empty({training ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C : 1}, fo);
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "num_batches_tracked must be an int64 device tensor");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  check(madnn_bn_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, y.data_ptr(), M, (int)C, dt_code(x),
+                     relu ? 1 : 0, training ? 1 : 0, (float)eps, (float)momentum, optf(w), optf(b),
+                     training ? optf_mut(run_mean) : const_cast<float*>(optf(run_mean)), optf_mut(run_var),
+                     training ? nb : nullptr, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                     scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(x)),
+        "bn_fwd");
+  return {y, save_mean, save_invstd, scale, shift};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
+    const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& res,
+    const c10::optional<at::Tensor>& w, const at::Tensor& save_mean, const at::Tensor& save_invstd,
+    const at::Tensor& scale, const at::Tensor& shift, bool relu, bool need_wgrad) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = bn_rows(x, C);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor dyc = dy;
+  if (dy.strides() != x.strides() || dy.scalar_type() != x.scalar_type()) {
+    dyc = at::empty_like(x);
+    dyc.copy_(dy);
+  }
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor dres = res.has_value() ? at::empty_like(x) : at::Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor dw = at::empty({C}, fo), db = at::empty({C}, fo);
+  at::Tensor coef = at::empty({3 * C}, fo);
+  at::Tensor ws = at::empty({(int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
+  check(madnn_bn_bwd(dyc.data_ptr(), x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, dx.data_ptr(),
+                     dres.defined() ? dres.data_ptr() : nullptr, M, (int)C, dt_code(x), relu ? 1 : 0, optf(w),
+                     save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                     shift.data_ptr<float>(), need_wgrad ? dw.data_ptr<float>() : nullptr,
+                     need_wgrad ? db.data_ptr<float>() : nullptr, coef.data_ptr<float>(), ws.data_ptr<float>(),
+                     cur_stream(x)),
+        "bn_bwd");
+  if (!dres.defined()) dres = at::empty({0}, x.options());
+  return {dx, dw, db, dres};
+}
+
+bool bn_supported(int64_t C) { return madnn_bn_supported((int)C) != 0; }
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
+  m.def(
+      "bn_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
+      "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "bn_bwd(Tensor dy, Tensor x, Tensor? res, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, "
+      "Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
   m.def("bucket_unpack(Tensor(a!)[] dsts, Tensor flat, int[] offsets, float scale) -> ()");
   m.def("flat_scale_cast(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -269,4 +366,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("grad_norm", grad_norm);
   m.impl("norm_fwd", norm_fwd);
   m.impl("norm_bwd", norm_bwd);
+  m.impl("bn_fwd", bn_fwd);
+  m.impl("bn_bwd", bn_bwd);
 }

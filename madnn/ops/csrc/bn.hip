@@ -1,0 +1,388 @@
+// K5 — fused BatchNorm (+ residual add) (+ ReLU) for channels_last (NHWC)
+// activations, training and inference, forward and backward.
+//
+// Why: on the first MI355X profile of ResNet-50 (profiles/r1_resnet50_dp1_*)
+// MIOpen's NHWC bf16 BatchNorm kernels took 35 % of the step and the separate
+// ReLU / residual-add / ReLU-backward passes another 24 %.  All of it is
+// HBM-bound streaming, so the win is in passes: this file does
+//   forward : 1 read for the statistics + 1 read/1 write for
+//             y = relu(x*scale + shift + residual)
+//   backward: 1 read (dy, x[, res]) for the two channel reductions + 1 read /
+//             1 write for dx (and d_residual), the ReLU mask recomputed from x
+//             instead of stored.
+// Layout: an NHWC tensor is a dense [M = N*H*W, C] matrix.  A lane owns 8
+// consecutive channels (16-byte bf16 access), TPR = C/8 lanes cover a row and
+// a 256-lane workgroup covers RPI = 256/TPR rows per iteration; grid-stride over
+// rows.  Channel sums are reduced across the workgroup's row slots in LDS and
+// written as ONE fp32 partial row per workgroup; a finalize kernel reduces the
+// partial slab column-parallel in double (no float atomics: MI355X_MICROARCH.md
+// "Global float atomics") and produces the per-channel affine coefficients, the
+// running-stat update and the num_batches_tracked increment (so no extra host
+// launches per layer).
+#include "common.h"
+
+namespace madnn {
+
+constexpr int kBnThreads = 256;
+
+struct BnGeom {
+  int tpr, rpi;
+};
+
+__host__ __device__ inline BnGeom bn_geom(int C) {
+  BnGeom g;
+  g.tpr = C / 8;
+  g.rpi = kBnThreads / g.tpr;
+  return g;
+}
+
+// partial[blk][0:C] = sum x, partial[blk][C:2C] = sum x^2
+template <int XDT>
+__global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const void* __restrict__ x, int64_t M, int C,
+                                                               float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [rpi][2][C]
+  const BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg = t % g.tpr;
+  const int rs = t / g.tpr;
+  const bool active = rs < g.rpi;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  if (active) {
+    for (int64_t r = (int64_t)blockIdx.x * g.rpi + rs; r < M; r += (int64_t)gridDim.x * g.rpi) {
+      float v[8];
+      load8<XDT>(x, r * C + cg * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[j];
+        q[j] += v[j] * v[j];
+      }
+    }
+  }
+  if (g.rpi == 1) {
+    if (active) {
+      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + cg * 8, s);
+      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + C + cg * 8, q);
+    }
+    return;
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      slab[(rs * 2 + 0) * C + cg * 8 + j] = s[j];
+      slab[(rs * 2 + 1) * C + cg * 8 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < 2 * C; c += kBnThreads) {
+    const int which = c / C, ch = c % C;
+    float a = 0.f;
+    for (int r = 0; r < g.rpi; ++r) a += slab[(r * 2 + which) * C + ch];
+    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+  }
+}
+
+// Reduce [G][2][C] partials per channel (double), then:
+//   mean, invstd -> save_mean/save_invstd
+//   scale = w*invstd, shift = b - mean*scale
+//   running stats update (unbiased var), nbt += 1
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(
+    const float* __restrict__ partial, int G, int C, int64_t M, float eps, float momentum,
+    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ run_mean, float* __restrict__ run_var, int64_t* __restrict__ nbt) {
+  __shared__ double red[2][8][33];
+  const int lc = threadIdx.x & 31, ls = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lc;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int k = ls; k < G; k += 8) {
+      s += partial[(int64_t)k * 2 * C + c];
+      q += partial[(int64_t)k * 2 * C + C + c];
+    }
+  red[0][ls][lc] = s;
+  red[1][ls][lc] = q;
+  __syncthreads();
+  if (ls == 0 && c < C) {
+    s = q = 0.0;
+    for (int k = 0; k < 8; ++k) {
+      s += red[0][k][lc];
+      q += red[1][k][lc];
+    }
+    const double mean = s / (double)M;
+    double var = q / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    save_mean[c] = (float)mean;
+    save_invstd[c] = invstd;
+    const float wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+    scale[c] = wc * invstd;
+    shift[c] = bc - (float)mean * wc * invstd;
+    if (run_mean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unbiased;
+    }
+  }
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+}
+
+// eval-mode coefficients from running statistics
+__global__ void bn_eval_coef_kernel(int C, float eps, const float* __restrict__ w, const float* __restrict__ b,
+                                    const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = 1.f / __builtin_sqrtf(run_var[c] + eps);
+  const float wc = w ? w[c] : 1.f, bc = b ? b[c] : 0.f;
+  scale[c] = wc * invstd;
+  shift[c] = bc - run_mean[c] * wc * invstd;
+}
+
+// y = act(x*scale + shift + res)
+template <int XDT, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, void* __restrict__ y,
+                                                       int64_t total, int C) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
+    const int c0 = (int)(i % C);
+    float v[8], sc[8], sh[8];
+    load8<XDT>(x, i, v);
+    load8<kF32>(scale, c0, sc);
+    load8<kF32>(shift, c0, sh);
+    float r[8];
+    if constexpr (RES) load8<XDT>(res, i, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] * sc[j] + sh[j];
+      if constexpr (RES) z += r[j];
+      if constexpr (RELU) z = z > 0.f ? z : 0.f;
+      v[j] = z;
+    }
+    store8<XDT>(y, i, v);
+  }
+}
+
+// Backward reduction: g = dy * [z > 0] (ReLU mask recomputed from x),
+// partial[blk][0:C] = sum g, partial[blk][C:2C] = sum g * x
+template <int XDT, bool RELU, bool RES>
+__global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ res,
+    const float* __restrict__ scale, const float* __restrict__ shift, int64_t M, int C,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float slab[];
+  const BnGeom g = bn_geom(C);
+  const int t = threadIdx.x;
+  const int cg = t % g.tpr;
+  const int rs = t / g.tpr;
+  const bool active = rs < g.rpi;
+  float sg[8], sgx[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+  if (active) {
+    if constexpr (RELU) {
+      load8<kF32>(scale, cg * 8, sc);
+      load8<kF32>(shift, cg * 8, sh);
+    }
+    for (int64_t r = (int64_t)blockIdx.x * g.rpi + rs; r < M; r += (int64_t)gridDim.x * g.rpi) {
+      float dv[8], xv[8], rv[8];
+      load8<XDT>(dy, r * C + cg * 8, dv);
+      load8<XDT>(x, r * C + cg * 8, xv);
+      if constexpr (RELU && RES) load8<XDT>(res, r * C + cg * 8, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float gj = dv[j];
+        if constexpr (RELU) {
+          float z = xv[j] * sc[j] + sh[j];
+          if constexpr (RES) z += rv[j];
+          gj = z > 0.f ? gj : 0.f;
+        }
+        sg[j] += gj;
+        sgx[j] += gj * xv[j];
+      }
+    }
+  }
+  if (g.rpi == 1) {
+    if (active) {
+      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + cg * 8, sg);
+      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + C + cg * 8, sgx);
+    }
+    return;
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      slab[(rs * 2 + 0) * C + cg * 8 + j] = sg[j];
+      slab[(rs * 2 + 1) * C + cg * 8 + j] = sgx[j];
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < 2 * C; c += kBnThreads) {
+    const int which = c / C, ch = c % C;
+    float a = 0.f;
+    for (int r = 0; r < g.rpi; ++r) a += slab[(r * 2 + which) * C + ch];
+    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+  }
+}
+
+// dbeta = sum g ; dgamma = sum g*xhat = invstd*(sum g*x - mean*sum g)
+// dx = w*invstd*(g - dbeta/M - xhat*dgamma/M) = A*g + Bc*x + Cc  (per channel)
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+    const float* __restrict__ partial, int G, int C, int64_t M, const float* __restrict__ w,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dw,
+    float* __restrict__ db, float* __restrict__ ca, float* __restrict__ cb, float* __restrict__ cc) {
+  __shared__ double red[2][8][33];
+  const int lc = threadIdx.x & 31, ls = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lc;
+  double s = 0.0, q = 0.0;
+  if (c < C)
+    for (int k = ls; k < G; k += 8) {
+      s += partial[(int64_t)k * 2 * C + c];
+      q += partial[(int64_t)k * 2 * C + C + c];
+    }
+  red[0][ls][lc] = s;
+  red[1][ls][lc] = q;
+  __syncthreads();
+  if (ls == 0 && c < C) {
+    s = q = 0.0;
+    for (int k = 0; k < 8; ++k) {
+      s += red[0][k][lc];
+      q += red[1][k][lc];
+    }
+    const double mu = mean[c], is = invstd[c];
+    const double dbeta = s;
+    const double dgamma = is * (q - mu * s);
+    if (dw) dw[c] = (float)dgamma;
+    if (db) db[c] = (float)dbeta;
+    const double wc = w ? w[c] : 1.0;
+    const double A = wc * is;
+    const double k2 = dbeta / (double)M, k3 = dgamma / (double)M;
+    // dx = A*(g - k2 - (x-mu)*is*k3) = A*g - A*is*k3*x + A*(is*k3*mu - k2)
+    ca[c] = (float)A;
+    cb[c] = (float)(-A * is * k3);
+    cc[c] = (float)(A * (is * k3 * mu - k2));
+  }
+}
+
+template <int XDT, bool RELU, bool RES>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ res,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ ca,
+    const float* __restrict__ cb, const float* __restrict__ cc, void* __restrict__ dx, void* __restrict__ dres,
+    int64_t total, int C) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
+    const int c0 = (int)(i % C);
+    float dv[8], xv[8], rv[8], a[8], b[8], c[8];
+    load8<XDT>(dy, i, dv);
+    load8<XDT>(x, i, xv);
+    load8<kF32>(ca, c0, a);
+    load8<kF32>(cb, c0, b);
+    load8<kF32>(cc, c0, c);
+    if constexpr (RELU) {
+      float sc[8], sh[8];
+      load8<kF32>(scale, c0, sc);
+      load8<kF32>(shift, c0, sh);
+      if constexpr (RES) load8<XDT>(res, i, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = xv[j] * sc[j] + sh[j];
+        if constexpr (RES) z += rv[j];
+        dv[j] = z > 0.f ? dv[j] : 0.f;
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = a[j] * dv[j] + b[j] * xv[j] + c[j];
+    store8<XDT>(dx, i, o);
+    if constexpr (RES) store8<XDT>(dres, i, dv);
+  }
+}
+
+static int bn_grid_rows(int64_t M, int C) {
+  const BnGeom g = bn_geom(C);
+  int64_t iters = (M + g.rpi - 1) / g.rpi;
+  return (int)(iters < 2048 ? (iters < 1 ? 1 : iters) : 2048);
+}
+
+}  // namespace madnn
+
+#define MADNN_BN_VARIANT(relu, res, RELU, RES, ...)                              \
+  if (relu && res) { constexpr bool RELU = true, RES = true; __VA_ARGS__; }      \
+  else if (relu) { constexpr bool RELU = true, RES = false; __VA_ARGS__; }       \
+  else if (res) { constexpr bool RELU = false, RES = true; __VA_ARGS__; }        \
+  else { constexpr bool RELU = false, RES = false; __VA_ARGS__; }
+
+extern "C" {
+
+int madnn_bn_supported(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 : 0; }
+
+int madnn_bn_partial_rows(int64_t M, int C) { return madnn::bn_grid_rows(M, C); }
+
+// Forward. training: compute batch stats (+ running update); else use running stats.
+hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int xdt, int relu,
+                        int training, float eps, float momentum, const float* w, const float* b, float* run_mean,
+                        float* run_var, int64_t* nbt, float* save_mean, float* save_invstd, float* scale,
+                        float* shift, float* workspace, hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const int G = bn_grid_rows(M, C);
+  const BnGeom g = bn_geom(C);
+  const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
+  if (training) {
+    MADNN_DISPATCH_DT(xdt, XDT, {
+      hipLaunchKernelGGL((bn_stats_kernel<XDT>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
+    });
+    MADNN_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, workspace, G, C, M, eps,
+                       momentum, w, b, save_mean, save_invstd, scale, shift, run_mean, run_var, nbt);
+  } else {
+    hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, eps, w, b, run_mean,
+                       run_var, scale, shift);
+  }
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int64_t total = M * C;
+  const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
+  MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, res != nullptr, RELU, RES, {
+    hipLaunchKernelGGL((bn_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, x, res, scale, shift, y,
+                       total, C);
+  }));
+  return hipGetLastError();
+}
+
+hipError_t madnn_bn_bwd(const void* dy, const void* x, const void* res, void* dx, void* dres, int64_t M, int C,
+                        int xdt, int relu, const float* w, const float* save_mean, const float* save_invstd,
+                        const float* scale, const float* shift, float* dw, float* db, float* coef,
+                        float* workspace, hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const int G = bn_grid_rows(M, C);
+  const BnGeom g = bn_geom(C);
+  const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
+  const bool has_res = res != nullptr;
+  MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<XDT, RELU, RES>), dim3(G), dim3(kBnThreads), lds, stream, dy, x, res,
+                       scale, shift, M, C, workspace);
+  }));
+  MADNN_HIP_CHECK(hipGetLastError());
+  float* ca = coef;
+  float* cb = coef + C;
+  float* cc = coef + 2 * C;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, workspace, G, C, M, w,
+                     save_mean, save_invstd, dw, db, ca, cb, cc);
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int64_t total = M * C;
+  const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
+  MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, dy, x, res, scale,
+                       shift, ca, cb, cc, dx, dres, total, C);
+  }));
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -115,3 +115,20 @@ def norm(x, weight, bias, eps, rms, residual=None):
         y = y + bias.float()
     y = y.to(x.dtype)
     return (y, s) if residual is not None else y
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked=None, *, training, momentum=0.1,
+                   eps=1e-5, relu=False, residual=None):
+    import torch.nn.functional as F
+
+    if training and num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
+        if momentum is None:
+            momentum = 1.0 / float(num_batches_tracked)
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum if momentum is not None else 0.0,
+                     eps)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = torch.relu(y)
+    return y

@@ -177,3 +177,84 @@ def test_norm_large_rows_multi_pass(cuda):
     ref = torch.nn.functional.layer_norm(x.detach().float(), (1024,))
     torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
     assert torch.isfinite(w.grad).all()
+
+
+@pytest.mark.parametrize("C", [8, 64, 256, 1000, 2048])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True), (False, True)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_batchnorm_fused_nhwc(cuda, C, relu, res, dt):
+    """K5 vs eager fp32 act(BN(x) + residual): outputs, running stats, nbt and all grads."""
+    torch.manual_seed(6)
+    N, H, W = 4, 7, 5
+    x = (torch.randn(N, C, H, W, device=cuda) * 1.5 + 0.3).to(dt).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    r = None
+    if res:
+        r = torch.randn(N, C, H, W, device=cuda).to(dt).contiguous(memory_format=torch.channels_last)
+        r.requires_grad_(True)
+    w = (torch.rand(C, device=cuda) + 0.5).requires_grad_(True)
+    b = (torch.randn(C, device=cuda) * 0.1).requires_grad_(True)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    nbt = torch.zeros((), dtype=torch.long, device=cuda)
+    y = ops.batch_norm_act(x, w, b, rm, rv, nbt, training=True, momentum=0.1, eps=1e-5, relu=relu, residual=r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    # fp32 eager reference
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if res else None
+    wr = w.detach().clone().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    rmr, rvr = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yr = torch.nn.functional.batch_norm(xr, rmr, rvr, wr, br, True, 0.1, 1e-5)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    tol = 3e-2 if dt == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(rm, rmr, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rv, rvr, atol=1e-4, rtol=1e-4)
+    assert int(nbt) == 1
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 3, rtol=tol * 3)
+    gt = 0.15 if dt == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(w.grad, wr.grad, atol=gt, rtol=gt)
+    torch.testing.assert_close(b.grad, br.grad, atol=gt, rtol=gt)
+    if res:
+        torch.testing.assert_close(r.grad.float(), rr.grad, atol=tol, rtol=tol)
+
+
+def test_batchnorm_fused_eval_and_large(cuda):
+    torch.manual_seed(7)
+    C = 256
+    x = torch.randn(64, C, 56, 56, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    w, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    rm, rv = torch.randn(C, device=cuda), torch.rand(C, device=cuda) + 0.5
+    with torch.no_grad():
+        y = ops.batch_norm_act(x, w, b, rm, rv, training=False, relu=True)
+        yr = torch.relu(torch.nn.functional.batch_norm(x.float(), rm, rv, w, b, False, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    # training stats over 200k rows: exact-ish mean/var vs fp64
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    ops.batch_norm_act(x, w, b, rm2, rv2, training=True, momentum=1.0)
+    xd = x.double().permute(0, 2, 3, 1).reshape(-1, C)
+    torch.testing.assert_close(rm2.double(), xd.mean(0), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rv2.double(), xd.var(0, unbiased=True), atol=1e-4, rtol=1e-4)
+
+
+def test_fused_resnet_block_matches_eager(cuda):
+    """A Bottleneck with fused BN vs the same weights through eager nn ops (fp32)."""
+    from madnn.models.resnet import Bottleneck
+
+    torch.manual_seed(8)
+    blk = Bottleneck(64, 16).to(cuda)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    x = torch.randn(8, 64, 14, 14, device=cuda).contiguous(memory_format=torch.channels_last)
+    blk = blk.to(memory_format=torch.channels_last)
+    y = blk(x)  # fused (fp32 NHWC)
+    blk_cpu = Bottleneck(64, 16)
+    blk_cpu.load_state_dict({k: v.cpu() for k, v in blk.state_dict().items()})
+    yr = blk_cpu(x.cpu())  # eager path
+    torch.testing.assert_close(y.cpu(), yr, atol=1e-3, rtol=1e-3)
