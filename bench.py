@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--miopen-benchmark", type=int, default=1,
+    ap.add_argument("--miopen-benchmark", type=int, default=0,
                     help="torch.backends.cudnn.benchmark (MIOpen find-mode kernel search for each conv shape)")
     return ap.parse_args()
 

@@ -24,6 +24,8 @@
 namespace madnn {
 
 constexpr int kBnThreads = 256;
+constexpr int kFinSlices = 32;   // finalize: 32 channels x 32 partial-row slices per 1024-lane block
+constexpr int kBnMaxPartials = 2 * kNumCU;
 
 struct BnGeom {
   int tpr, rpi;
@@ -50,7 +52,22 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const void* __rest
 #pragma unroll
   for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
   if (active) {
-    for (int64_t r = (int64_t)blockIdx.x * g.rpi + rs; r < M; r += (int64_t)gridDim.x * g.rpi) {
+    const int64_t step = (int64_t)gridDim.x * g.rpi;
+    int64_t r = (int64_t)blockIdx.x * g.rpi + rs;
+    // 4 rows in flight per lane: memory-level parallelism for the HBM stream
+    for (; r + 3 * step < M; r += 4 * step) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8<XDT>(x, (r + u * step) * C + cg * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += v[u][j];
+          q[j] += v[u][j] * v[u][j];
+        }
+    }
+    for (; r < M; r += step) {
       float v[8];
       load8<XDT>(x, r * C + cg * 8, v);
 #pragma unroll
@@ -87,26 +104,42 @@ __global__ __launch_bounds__(kBnThreads) void bn_stats_kernel(const void* __rest
 //   mean, invstd -> save_mean/save_invstd
 //   scale = w*invstd, shift = b - mean*scale
 //   running stats update (unbiased var), nbt += 1
-__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(
+__global__ __launch_bounds__(1024) void bn_stats_finalize_kernel(
     const float* __restrict__ partial, int G, int C, int64_t M, float eps, float momentum,
     const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ run_mean, float* __restrict__ run_var, int64_t* __restrict__ nbt) {
-  __shared__ double red[2][8][33];
+  __shared__ double red[2][kFinSlices][33];
   const int lc = threadIdx.x & 31, ls = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + lc;
   double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int k = ls; k < G; k += 8) {
+  if (c < C) {
+    // independent loads in flight: the slab read is latency-bound, not bandwidth-bound
+    float fs[4] = {0.f, 0.f, 0.f, 0.f}, fq[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = ls;
+    for (; k + 3 * kFinSlices < G; k += 4 * kFinSlices) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fs[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + c];
+        fq[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += fs[u];
+        q += fq[u];
+      }
+    }
+    for (; k < G; k += kFinSlices) {
       s += partial[(int64_t)k * 2 * C + c];
       q += partial[(int64_t)k * 2 * C + C + c];
     }
+  }
   red[0][ls][lc] = s;
   red[1][ls][lc] = q;
   __syncthreads();
   if (ls == 0 && c < C) {
     s = q = 0.0;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kFinSlices; ++k) {
       s += red[0][k][lc];
       q += red[1][k][lc];
     }
@@ -147,8 +180,10 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
                                                        const float* __restrict__ shift, void* __restrict__ y,
                                                        int64_t total, int C) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
-    const int c0 = (int)(i % C);
+  const int sC = (int)(stride % C);  // channel advance per grid-stride step (no 64-bit modulo in the loop)
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  int c0 = (int)(i % C);
+  for (; i < total; i += stride, c0 = (c0 + sC >= C) ? c0 + sC - C : c0 + sC) {
     float v[8], sc[8], sh[8];
     load8<XDT>(x, i, v);
     load8<kF32>(scale, c0, sc);
@@ -187,11 +222,9 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
       load8<kF32>(scale, cg * 8, sc);
       load8<kF32>(shift, cg * 8, sh);
     }
-    for (int64_t r = (int64_t)blockIdx.x * g.rpi + rs; r < M; r += (int64_t)gridDim.x * g.rpi) {
-      float dv[8], xv[8], rv[8];
-      load8<XDT>(dy, r * C + cg * 8, dv);
-      load8<XDT>(x, r * C + cg * 8, xv);
-      if constexpr (RELU && RES) load8<XDT>(res, r * C + cg * 8, rv);
+    const int64_t step = (int64_t)gridDim.x * g.rpi;
+    int64_t r = (int64_t)blockIdx.x * g.rpi + rs;
+    auto body = [&](const float (&dv)[8], const float (&xv)[8], const float (&rv)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float gj = dv[j];
@@ -203,6 +236,24 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
         sg[j] += gj;
         sgx[j] += gj * xv[j];
       }
+    };
+    for (; r + step < M; r += 2 * step) {  // 2 rows x (dy, x[, res]) in flight per lane
+      float dv[2][8], xv[2][8], rv[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        load8<XDT>(dy, (r + u * step) * C + cg * 8, dv[u]);
+        load8<XDT>(x, (r + u * step) * C + cg * 8, xv[u]);
+        if constexpr (RELU && RES) load8<XDT>(res, (r + u * step) * C + cg * 8, rv[u]);
+      }
+      body(dv[0], xv[0], rv[0]);
+      body(dv[1], xv[1], rv[1]);
+    }
+    for (; r < M; r += step) {
+      float dv[8], xv[8], rv[8];
+      load8<XDT>(dy, r * C + cg * 8, dv);
+      load8<XDT>(x, r * C + cg * 8, xv);
+      if constexpr (RELU && RES) load8<XDT>(res, r * C + cg * 8, rv);
+      body(dv, xv, rv);
     }
   }
   if (g.rpi == 1) {
@@ -230,25 +281,41 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
 
 // dbeta = sum g ; dgamma = sum g*xhat = invstd*(sum g*x - mean*sum g)
 // dx = w*invstd*(g - dbeta/M - xhat*dgamma/M) = A*g + Bc*x + Cc  (per channel)
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int G, int C, int64_t M, const float* __restrict__ w,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dw,
     float* __restrict__ db, float* __restrict__ ca, float* __restrict__ cb, float* __restrict__ cc) {
-  __shared__ double red[2][8][33];
+  __shared__ double red[2][kFinSlices][33];
   const int lc = threadIdx.x & 31, ls = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + lc;
   double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int k = ls; k < G; k += 8) {
+  if (c < C) {
+    // independent loads in flight: the slab read is latency-bound, not bandwidth-bound
+    float fs[4] = {0.f, 0.f, 0.f, 0.f}, fq[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = ls;
+    for (; k + 3 * kFinSlices < G; k += 4 * kFinSlices) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fs[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + c];
+        fq[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += fs[u];
+        q += fq[u];
+      }
+    }
+    for (; k < G; k += kFinSlices) {
       s += partial[(int64_t)k * 2 * C + c];
       q += partial[(int64_t)k * 2 * C + C + c];
     }
+  }
   red[0][ls][lc] = s;
   red[1][ls][lc] = q;
   __syncthreads();
   if (ls == 0 && c < C) {
     s = q = 0.0;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kFinSlices; ++k) {
       s += red[0][k][lc];
       q += red[1][k][lc];
     }
@@ -274,8 +341,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ cb, const float* __restrict__ cc, void* __restrict__ dx, void* __restrict__ dres,
     int64_t total, int C) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
-    const int c0 = (int)(i % C);
+  const int sC = (int)(stride % C);
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  int c0 = (int)(i % C);
+  for (; i < total; i += stride, c0 = (c0 + sC >= C) ? c0 + sC - C : c0 + sC) {
     float dv[8], xv[8], rv[8], a[8], b[8], c[8];
     load8<XDT>(dy, i, dv);
     load8<XDT>(x, i, xv);
@@ -305,7 +374,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 static int bn_grid_rows(int64_t M, int C) {
   const BnGeom g = bn_geom(C);
   int64_t iters = (M + g.rpi - 1) / g.rpi;
-  return (int)(iters < 2048 ? (iters < 1 ? 1 : iters) : 2048);
+  return (int)(iters < kBnMaxPartials ? (iters < 1 ? 1 : iters) : kBnMaxPartials);
 }
 
 }  // namespace madnn
@@ -338,7 +407,7 @@ hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, int64_t M, int 
       hipLaunchKernelGGL((bn_stats_kernel<XDT>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
     });
     MADNN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, workspace, G, C, M, eps,
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C, M, eps,
                        momentum, w, b, save_mean, save_invstd, scale, shift, run_mean, run_var, nbt);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, eps, w, b, run_mean,
@@ -373,7 +442,7 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const void* res, void* dx
   float* ca = coef;
   float* cb = coef + C;
   float* cc = coef + 2 * C;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, workspace, G, C, M, w,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C, M, w,
                      save_mean, save_invstd, dw, db, ca, cb, cc);
   MADNN_HIP_CHECK(hipGetLastError());
   const int64_t total = M * C;
