@@ -115,6 +115,43 @@ int madnn_pipeline_schedule(int kind, int stage, int nstages, int nmicro, int* o
   return k;
 }
 
+// Full per-stage pipeline PROGRAM, communication included, as (op, a, b)
+// triples.  Ops: 0 RECV_FWD m | 1 FWD m | 2 SEND_FWD m | 3 RECV_BWD m | 4 BWD m |
+// 5 SEND_BWD m | 6 SEND_FWD_RECV_BWD (send m=a, recv m=b) |
+// 7 SEND_BWD_RECV_FWD (send m=a, recv m=b).
+// 1F1B follows the non-interleaved PipeDream-flush order with the steady-state
+// send/recv pairs batched into one group, which is what keeps two adjacent
+// stages from both blocking in a send on a shared point-to-point channel.
+// Returns the number of triples written (<= 6*M: GPipe; 1F1B <= 4*M + 1).
+int madnn_pipeline_program(int kind, int stage, int nstages, int nmicro, int* out) {
+  int k = 0;
+  auto emit = [&](int op, int a, int b) {
+    out[3 * k] = op;
+    out[3 * k + 1] = a;
+    out[3 * k + 2] = b;
+    ++k;
+  };
+  if (kind == 0) {  // GPipe
+    for (int m = 0; m < nmicro; ++m) { emit(0, m, -1); emit(1, m, -1); emit(2, m, -1); }
+    for (int m = 0; m < nmicro; ++m) { emit(3, m, -1); emit(4, m, -1); emit(5, m, -1); }
+    return k;
+  }
+  const int warm = std::min(nstages - stage - 1, nmicro);
+  const int steady = nmicro - warm;
+  for (int i = 0; i < warm; ++i) { emit(0, i, -1); emit(1, i, -1); emit(2, i, -1); }
+  if (steady > 0) emit(0, warm, -1);
+  for (int i = 0; i < steady; ++i) {
+    const int f = warm + i;
+    emit(1, f, -1);
+    emit(6, f, i);
+    emit(4, i, -1);
+    if (i == steady - 1) emit(5, i, -1);
+    else emit(7, i, f + 1);
+  }
+  for (int i = steady; i < nmicro; ++i) { emit(3, i, -1); emit(4, i, -1); emit(5, i, -1); }
+  return k;
+}
+
 // 64-bit FNV-1a over (op, group, numel, dtype) events.
 uint64_t madnn_hash_init() { return 1469598103934665603ULL; }
 

@@ -34,6 +34,8 @@ def _load():
                                            ctypes.POINTER(L)]
         lib.madnn_pipeline_schedule.restype = I
         lib.madnn_pipeline_schedule.argtypes = [I, I, I, I, ctypes.POINTER(I)]
+        lib.madnn_pipeline_program.restype = I
+        lib.madnn_pipeline_program.argtypes = [I, I, I, I, ctypes.POINTER(I)]
         lib.madnn_hash_init.restype = U
         lib.madnn_hash_init.argtypes = []
         lib.madnn_hash_event.restype = U
@@ -84,6 +86,20 @@ def pipeline_schedule(kind: str, stage: int, nstages: int, nmicro: int) -> List[
     for v in list(out)[:k]:
         res.append(("B", v - 1000000) if v >= 1000000 else ("F", v))
     return res
+
+
+PROGRAM_OPS = ("RECV_FWD", "FWD", "SEND_FWD", "RECV_BWD", "BWD", "SEND_BWD", "SEND_FWD_RECV_BWD",
+               "SEND_BWD_RECV_FWD")
+
+
+def pipeline_program(kind: str, stage: int, nstages: int, nmicro: int) -> List[Tuple[str, int, int]]:
+    """Per-stage instruction list (op, a, b) including the point-to-point steps."""
+    lib = _load()
+    cap = 6 * nmicro + 8
+    out = (ctypes.c_int * (3 * cap))()
+    k = lib.madnn_pipeline_program(0 if kind == "gpipe" else 1, stage, nstages, nmicro, out)
+    vals = list(out)[:3 * k]
+    return [(PROGRAM_OPS[vals[3 * i]], vals[3 * i + 1], vals[3 * i + 2]) for i in range(k)]
 
 
 class OrderHash:

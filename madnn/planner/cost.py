@@ -1,0 +1,225 @@
+"""Per-layer cost model: FLOPs, bytes moved, parameters, activation memory,
+and (optionally) measured forward/backward time with HIP events.
+
+Reference: the only cost signal in TorchAD-NN is a dead probe that times
+10 x (forward, backward, synchronizeGradients) (datamodule.lua:280-303,
+call commented out at :42) plus a size-only heuristic (datamodule.lua:68-78).
+Here every layer of the traced spine is costed analytically on the META
+device — no weights are materialised, so an 8B-parameter model is costed on a
+laptop — by running it under a dispatch mode that counts matmul/conv/attention
+FLOPs (``torch.utils.flop_counter``) and the bytes every op writes.  On a GPU,
+``measure()`` replaces the analytic times with HIP-event timings.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Any, List, Optional
+
+import torch
+from torch import nn
+from torch.func import functional_call
+from torch.utils._python_dispatch import TorchDispatchMode
+from torch.utils.flop_counter import FlopCounterMode
+
+from .hw import Machine, load
+from .trace import Spine
+
+
+@dataclass
+class LayerCost:
+    name: str
+    params: int                 # parameters owned by this layer (shared ones counted where first seen)
+    shared_params: int          # parameters also used by another layer (tied weights)
+    flops: float                # forward FLOPs per sample
+    act_bytes: float            # bytes written by forward ops per sample (~ saved-activation memory)
+    out_bytes: float            # boundary tensor bytes per sample (what a stage sends)
+    out_shape: tuple = ()
+    out_dtype: Any = None
+    fwd_s: float = 0.0          # per-sample forward time estimate (or measurement)
+    bwd_s: float = 0.0
+    measured: bool = False
+
+    @property
+    def time_s(self) -> float:
+        return self.fwd_s + self.bwd_s
+
+
+class _BytesMode(TorchDispatchMode):
+    """Counts bytes of every op output (excluding views)."""
+
+    def __init__(self):
+        super().__init__()
+        self.bytes = 0
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        name = getattr(func, "__name__", "")
+        if not any(v in name for v in ("view", "alias", "expand", "as_strided", "permute", "transpose", "detach",
+                                       "t.default", "unsqueeze", "squeeze", "slice", "select", "split")):
+            for t in (out if isinstance(out, (list, tuple)) else (out,)):
+                if isinstance(t, torch.Tensor):
+                    self.bytes += t.numel() * t.element_size()
+        return out
+
+
+def _meta_state(layer: nn.Module, dtype: Optional[torch.dtype]):
+    st = {}
+    for n, p in layer.named_parameters(remove_duplicate=False):
+        dt = dtype if (dtype is not None and p.is_floating_point()) else p.dtype
+        st[n] = torch.empty(p.shape, dtype=dt, device="meta")
+    for n, b in layer.named_buffers(remove_duplicate=False):
+        st[n] = torch.empty(b.shape, dtype=b.dtype, device="meta")
+    return st
+
+
+def _to_meta(x, dtype):
+    if isinstance(x, torch.Tensor):
+        dt = dtype if (dtype is not None and x.is_floating_point()) else x.dtype
+        return torch.empty(x.shape, dtype=dt, device="meta")
+    return x
+
+
+class _FlashSDPA:
+    """Cost stand-in for F.scaled_dot_product_attention during meta estimation.
+
+    On MI355X attention runs as a fused flash kernel (no S x S matrix in HBM), but
+    on the meta device SDPA would decompose into the math path and count the
+    score matrix; this replaces it with the flash cost: 4*B*H*Sq*Sk*D FLOPs
+    (halved when causal) and only the output tensor written."""
+
+    def __init__(self):
+        self.flops = 0.0
+        self._orig = None
+
+    def __call__(self, q, k, v, attn_mask=None, dropout_p=0.0, is_causal=False, scale=None, enable_gqa=False):
+        b, h, sq, d = q.shape
+        sk = k.shape[-2]
+        f = 4.0 * b * h * sq * sk * d
+        self.flops += f / 2 if is_causal else f
+        return torch.empty(b, h, sq, v.shape[-1], dtype=q.dtype, device=q.device)
+
+    def __enter__(self):
+        import torch.nn.functional as F
+
+        self._orig = F.scaled_dot_product_attention
+        F.scaled_dot_product_attention = self
+        return self
+
+    def __exit__(self, *exc):
+        import torch.nn.functional as F
+
+        F.scaled_dot_product_attention = self._orig
+        return False
+
+
+def estimate(spine: Spine, example_input: torch.Tensor, dtype: Optional[torch.dtype] = torch.bfloat16,
+             machine: Optional[Machine] = None) -> List[LayerCost]:
+    """Analytic per-sample costs of every spine layer (meta device, no allocation)."""
+    hw = machine or load()
+    batch = example_input.shape[0] if example_input.dim() > 0 else 1
+    x = _to_meta(example_input, dtype)
+    seen = {}
+    for i, layer in enumerate(spine.layers):
+        for p in layer.parameters():
+            seen.setdefault(id(p), []).append(i)
+    costs = []
+    counted = set()
+    for i, (layer, name) in enumerate(zip(spine.layers, spine.names)):
+        own = shared = 0
+        for p in layer.parameters():
+            if len(seen[id(p)]) > 1:
+                shared += p.numel()
+            if id(p) not in counted:
+                own += p.numel()
+                counted.add(id(p))
+        st = _meta_state(layer, dtype)
+        fc = FlopCounterMode(display=False)
+        bm = _BytesMode()
+        with torch.no_grad(), _FlashSDPA() as attn, fc, bm:
+            y = functional_call(layer, st, (x,))
+        flops = (fc.get_total_flops() + attn.flops) / batch
+        act = bm.bytes / batch
+        out_b = y.numel() * y.element_size() / batch
+        eff_flops = hw.bf16_tflops * 1e12 if (dtype in (torch.bfloat16, torch.float16)) else hw.fp32_tflops * 1e12
+        fwd = flops / eff_flops + 2.0 * act / (hw.hbm_tbps * 1e12)  # write + one re-read of every output
+        costs.append(LayerCost(name=name, params=own, shared_params=shared, flops=flops, act_bytes=act,
+                               out_bytes=out_b, out_shape=tuple(y.shape[1:]), out_dtype=y.dtype,
+                               fwd_s=fwd, bwd_s=2.0 * fwd))
+        x = y
+    return costs
+
+
+def measure(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], iters: int = 3) -> List[LayerCost]:
+    """Replace analytic times with HIP-event timings of each layer (fwd and fwd+bwd).
+
+    Requires the spine's parameters to live on the GPU; the example input's batch
+    is used as is (per-sample numbers are divided by it)."""
+    if not torch.cuda.is_available():
+        return costs
+    batch = example_input.shape[0]
+    x = example_input
+    for layer, c in zip(spine.layers, costs):
+        xin = x.detach().requires_grad_(x.is_floating_point())
+        for _ in range(2):
+            y = layer(xin)
+        start, mid, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        fw = bw = 0.0
+        for _ in range(iters):
+            start.record()
+            y = layer(xin)
+            mid.record()
+            if y.requires_grad:
+                y.backward(torch.ones_like(y))
+            end.record()
+            end.synchronize()
+            fw += start.elapsed_time(mid)
+            bw += mid.elapsed_time(end)
+        c.fwd_s = fw / iters / 1e3 / batch
+        c.bwd_s = bw / iters / 1e3 / batch
+        c.measured = True
+        x = y.detach()
+        for p in layer.parameters():
+            p.grad = None
+    return costs
+
+
+def param_state_bytes(params: int, optimizer: str = "adam", compute_bytes: int = 2) -> float:
+    """Bytes per parameter in madnn's layout: bf16 model + bf16 grad + fp32 master
+    + fp32 flat reduce buffer + optimizer state (SGD momentum 4 B, Adam 8 B)."""
+    opt = 8 if optimizer == "adam" else 4
+    master = 4 if compute_bytes < 4 else 0
+    return params * (compute_bytes + compute_bytes + master + 4 + opt)
+
+
+@dataclass
+class StageEstimate:
+    layers: tuple
+    time_per_sample_s: float
+    param_bytes: float
+    act_bytes_per_sample: float
+    out_bytes_per_sample: float
+    params: int = 0
+    notes: list = field(default_factory=list)
+
+
+def stage_estimate(costs: List[LayerCost], lo: int, hi: int, optimizer: str = "adam",
+                   checkpoint: bool = False) -> StageEstimate:
+    seg = costs[lo:hi]
+    t = sum(c.time_s for c in seg)
+    params = sum(c.params + (c.shared_params if lo > 0 and c.shared_params else 0) for c in seg)
+    if checkpoint:
+        t += sum(c.fwd_s for c in seg)  # recompute forward in backward
+        act = sum(c.out_bytes for c in seg) + max((c.act_bytes for c in seg), default=0.0)
+    else:
+        act = sum(c.act_bytes for c in seg)
+    return StageEstimate((lo, hi), t, param_state_bytes(params, optimizer), act, seg[-1].out_bytes if seg else 0.0,
+                         params)
+
+
+def divisors(n: int):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def ceil_div(a, b):
+    return int(math.ceil(a / b))

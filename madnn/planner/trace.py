@@ -58,9 +58,23 @@ def find_block_list(model: nn.Module) -> Optional[str]:
     return best
 
 
+class _Tracer(fx.Tracer):
+    """fx tracer that keeps madnn's fused-kernel modules (and torch.nn) as leaves."""
+
+    def is_leaf_module(self, m: nn.Module, qualname: str) -> bool:
+        if type(m).__module__.startswith("madnn.nn"):
+            return True
+        return super().is_leaf_module(m, qualname)
+
+
+def symbolic_trace(model: nn.Module) -> fx.GraphModule:
+    graph = _Tracer().trace(model)
+    return fx.GraphModule(model, graph, model.__class__.__name__)
+
+
 def _fx_split(model: nn.Module) -> Optional[Spine]:
     try:
-        gm = fx.symbolic_trace(model)
+        gm = symbolic_trace(model)
     except Exception as e:  # noqa: BLE001
         return Spine([model], ["model"], "whole", find_block_list(model), [f"fx trace failed: {type(e).__name__}"])
     nodes = list(gm.graph.nodes)
