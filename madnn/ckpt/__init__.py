@@ -1,0 +1,276 @@
+"""Strategy-agnostic checkpoints (save / load / consolidate / resume).
+
+The reference has no checkpointing at all: no torch.save of
+models or optimizer state, and the trainer's sync counter lives only on the
+object.  madnn's format::
+
+    <dir>/madnn_meta.json              plan (strategy, dp/pp/tp, stage bounds,
+                                       microbatches, sync mode/period/counter),
+                                       step, world size, versions, shard list
+    <dir>/model-<shard>.safetensors    fp32 master weights + buffers, keyed by the
+                                       UN-WRAPPED single-device parameter names
+    <dir>/optim-<shard>.pt             optimizer state per parameter name (plain
+                                       tensors only: loads with weights_only=True)
+    <dir>/rng-rank<r>.pt               per-rank RNG states
+
+One shard per pipeline stage, written by that stage's DP-rank 0.  Because keys
+are the original model's names, ``consolidate()`` merges the shards into one
+state dict that loads into plain PyTorch, and ``load()`` restores into ANY
+placement (different world size / strategy) by name — re-planning is free.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from .. import runtime as rt
+
+FORMAT = "madnn-ckpt-v1"
+
+
+def _st():
+    from safetensors.torch import load_file, save_file
+
+    return save_file, load_file
+
+
+def _named_state(engine) -> Dict[str, torch.Tensor]:
+    """name -> fp32 value of every parameter this rank owns, plus buffers."""
+    from ..parallel.dp import DataParallel
+    from ..parallel.pp import PipelineEngine
+
+    out = {}
+    if isinstance(engine, PipelineEngine):
+        space = engine.dp.space
+        for name, p in engine.state_dict().items():
+            out[name] = space.master_view(p).detach().float().cpu().contiguous() if id(p) in space.param_info \
+                else p.detach().float().cpu()
+        for name, b in engine.named_buffers():
+            out[name] = b.detach().cpu().clone()
+        return out
+    module = engine.module if isinstance(engine, DataParallel) else engine
+    space = engine.space if isinstance(engine, DataParallel) else None
+    seen = {}
+    for name, p in module.named_parameters(remove_duplicate=False):
+        if id(p) in seen:  # tied weight: store once, record the alias
+            out.setdefault("__aliases__", {})[name] = seen[id(p)]
+            continue
+        seen[id(p)] = name
+        if space is not None and id(p) in space.param_info:
+            out[name] = space.master_view(p).detach().float().cpu().contiguous()
+        else:
+            out[name] = _full_param(module, name, p).detach().float().cpu().contiguous()
+    for name, b in module.named_buffers():
+        out[name] = b.detach().cpu().clone()
+    return out
+
+
+def _full_param(module, name, p):
+    """Gather TP-sharded weights back to their full shape."""
+    from ..parallel.tp import ColumnParallelLinear, RowParallelLinear, _gather_last, _world
+
+    owner_name, _, attr = name.rpartition(".")
+    owner = module.get_submodule(owner_name) if owner_name else module
+    if isinstance(owner, RowParallelLinear) and attr == "weight" and _world(owner.group) > 1:
+        return _gather_last(p.detach(), owner.group)
+    if isinstance(owner, ColumnParallelLinear) and _world(owner.group) > 1:
+        t = p.detach()
+        return _gather_last(t.t().contiguous(), owner.group).t() if attr == "weight" else _gather_last(t, owner.group)
+    return p
+
+
+def _optim_state(engine, optimizer) -> Dict[str, Dict[str, torch.Tensor]]:
+    if optimizer is None:
+        return {}
+    sd = optimizer.state_dict()
+    idx2p = {}
+    k = 0
+    for g in optimizer.param_groups:
+        for p in g["params"]:
+            idx2p[k] = p
+            k += 1
+    names = _param_names(engine)
+    out = {}
+    for i, st in sd["state"].items():
+        p = idx2p.get(int(i))
+        if p is None or id(p) not in names:
+            continue
+        out[names[id(p)]] = {kk: (v.detach().cpu() if isinstance(v, torch.Tensor) else torch.tensor(v))
+                             for kk, v in st.items()}
+    return out
+
+
+def _param_names(engine) -> Dict[int, str]:
+    from ..parallel.dp import DataParallel
+    from ..parallel.pp import PipelineEngine
+
+    if isinstance(engine, PipelineEngine):
+        return {id(p): n for n, p in engine.state_dict().items()}
+    module = engine.module if isinstance(engine, DataParallel) else engine
+    return {id(p): n for n, p in module.named_parameters()}
+
+
+def _shard_id(engine) -> Optional[int]:
+    """Which shard this rank writes (None = this rank writes nothing)."""
+    from ..parallel.pp import PipelineEngine
+
+    if isinstance(engine, PipelineEngine):
+        return engine.stage if engine.groups.dp_idx == 0 else None
+    return 0 if rt.get_rank() == 0 else None
+
+
+def save(path: str, engine, optimizer=None, step: int = 0, extra: Optional[dict] = None) -> None:
+    """Collective: every rank calls it; DP-rank 0 of every stage writes its shard."""
+    save_file, _ = _st()
+    os.makedirs(path, exist_ok=True)
+    state = _named_state(engine)          # collective for TP gathers: all ranks
+    aliases = state.pop("__aliases__", {})
+    ostate = _optim_state(engine, optimizer)
+    shard = _shard_id(engine)
+    if shard is not None:
+        save_file(state, os.path.join(path, f"model-{shard:05d}.safetensors"))
+        flat = {}
+        for name, st in ostate.items():
+            for k, v in st.items():
+                flat[f"{name}::{k}"] = v
+        torch.save(flat, os.path.join(path, f"optim-{shard:05d}.pt"))
+    rng = {"cpu": torch.get_rng_state()}
+    if torch.cuda.is_available():
+        rng["cuda"] = torch.cuda.get_rng_state()
+    torch.save(rng, os.path.join(path, f"rng-rank{rt.get_rank()}.pt"))
+    rt.barrier()
+    if rt.get_rank() == 0:
+        meta = {"format": FORMAT, "time": time.time(), "step": int(step), "world": rt.get_world_size(),
+                "torch": torch.__version__, "plan": _plan_meta(engine), "extra": extra or {},
+                "aliases": aliases,
+                "shards": sorted(f for f in os.listdir(path) if f.startswith("model-"))}
+        with open(os.path.join(path, "madnn_meta.json"), "w") as f:
+            json.dump(meta, f, indent=2)
+    rt.barrier()
+
+
+def _plan_meta(engine) -> dict:
+    from ..parallel.dp import DataParallel
+    from ..parallel.pp import PipelineEngine
+
+    if isinstance(engine, PipelineEngine):
+        p = engine.plan
+        return {"strategy": p.strategy, "dp": p.dp, "pp": p.pp, "bounds": p.bounds, "microbatches": p.microbatches,
+                "schedule": engine.schedule}
+    if isinstance(engine, DataParallel):
+        return {"strategy": "dp", "dp": engine.world, "pp": 1, "sync": engine.sync, "sync_every": engine.sync_every,
+                "steps": engine._steps}
+    return {"strategy": "none"}
+
+
+def consolidate(path: str) -> Dict[str, torch.Tensor]:
+    """Merge every model shard into one plain state dict (loads into the un-wrapped model)."""
+    _, load_file = _st()
+    out = {}
+    for f in sorted(os.listdir(path)):
+        if f.startswith("model-") and f.endswith(".safetensors"):
+            out.update(load_file(os.path.join(path, f)))
+    meta_f = os.path.join(path, "madnn_meta.json")
+    if os.path.exists(meta_f):
+        with open(meta_f) as fh:
+            for alias, canon in json.load(fh).get("aliases", {}).items():
+                if alias not in out and canon in out:
+                    out[alias] = out[canon]
+    return out
+
+
+def _optim_all(path: str) -> Dict[str, Dict[str, torch.Tensor]]:
+    out: Dict[str, Dict[str, torch.Tensor]] = {}
+    for f in sorted(os.listdir(path)):
+        if f.startswith("optim-") and f.endswith(".pt"):
+            flat = torch.load(os.path.join(path, f), map_location="cpu", weights_only=True)
+            for key, v in flat.items():
+                name, _, k = key.partition("::")
+                out.setdefault(name, {})[k] = v
+    return out
+
+
+def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
+    """Restore weights (and optimizer state) into any placement, by parameter name."""
+    from ..parallel.dp import DataParallel
+    from ..parallel.pp import PipelineEngine
+
+    with open(os.path.join(path, "madnn_meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"not a madnn checkpoint: {path}")
+    full = consolidate(path)
+    names = _param_names(engine)
+    space = None
+    if isinstance(engine, PipelineEngine):
+        space = engine.dp.space
+        params = {n: p for n, p in engine.state_dict().items()}
+        module = engine.module
+    elif isinstance(engine, DataParallel):
+        space = engine.space
+        module = engine.module
+        params = dict(module.named_parameters())
+    else:
+        module = engine
+        params = dict(module.named_parameters())
+    missing = [n for n in params if n not in full]
+    if strict and missing:
+        raise KeyError(f"checkpoint misses parameters: {missing[:5]}")
+    with torch.no_grad():
+        for n, p in params.items():
+            if n not in full:
+                continue
+            v = full[n]
+            if space is not None and id(p) in space.param_info:
+                space.master_view(p).copy_(v.to(space.master_view(p).device))
+            else:
+                _load_param(module, n, p, v)
+        if space is not None:
+            space.sync_model_from_master()
+        bufs = dict(engine.named_buffers()) if isinstance(engine, PipelineEngine) else dict(module.named_buffers())
+        for n, b in bufs.items():
+            if n in full:
+                b.copy_(full[n].to(b.device))
+    if optimizer is not None:
+        ost = _optim_all(path)
+        sd = optimizer.state_dict()
+        k = 0
+        new_state = {}
+        for g in optimizer.param_groups:
+            for p in g["params"]:
+                n = names.get(id(p))
+                if n in ost:
+                    new_state[k] = ost[n]
+                k += 1
+        sd["state"] = new_state
+        optimizer.load_state_dict(sd)
+    if isinstance(engine, DataParallel):
+        engine._steps = int(meta.get("plan", {}).get("steps", engine._steps))
+    rng_file = os.path.join(path, f"rng-rank{rt.get_rank()}.pt")
+    if os.path.exists(rng_file):
+        rng = torch.load(rng_file, weights_only=True)
+        torch.set_rng_state(rng["cpu"])
+        if "cuda" in rng and torch.cuda.is_available():
+            torch.cuda.set_rng_state(rng["cuda"])
+    return meta
+
+
+def _load_param(module, name, p, v):
+    from ..parallel.tp import ColumnParallelLinear, RowParallelLinear
+
+    owner_name, _, attr = name.rpartition(".")
+    owner = module.get_submodule(owner_name) if owner_name else module
+    if isinstance(owner, (RowParallelLinear, ColumnParallelLinear)) and tuple(v.shape) != tuple(p.shape):
+        if attr == "weight":
+            owner.load_full(v.to(p.device), None)
+        else:
+            r = torch.distributed.get_rank(owner.group) if torch.distributed.is_initialized() else 0
+            k = p.numel()
+            p.copy_(v[r * k:(r + 1) * k].to(p.device))
+        return
+    p.copy_(v.to(p.device))

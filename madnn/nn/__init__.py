@@ -2,3 +2,8 @@
 from .norm import FusedBatchNorm2d, FusedLayerNorm, FusedRMSNorm, swap_layernorms
 
 __all__ = ["FusedBatchNorm2d", "FusedLayerNorm", "FusedRMSNorm", "swap_layernorms"]
+from ..parallel.tp import (ColumnParallelLinear, MPBaseLinear, MPBaseReshape, MPInitialLinear, MPInitialReshape,
+                           MPTanh, RowParallelLinear, set_debug_shapes)
+
+__all__ += ["ColumnParallelLinear", "RowParallelLinear", "MPInitialLinear", "MPBaseLinear", "MPTanh",
+            "MPInitialReshape", "MPBaseReshape", "set_debug_shapes"]

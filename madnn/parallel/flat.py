@@ -119,7 +119,7 @@ class FlatParamSpace:
         for p, off in zip(bk.params, bk.offsets):
             cl = self.param_info[id(p)][2]
             p.data = _phys_view(model[off:off + p.numel()], p.shape, cl)
-            p.grad = None
+            # an existing p.grad stays valid: pack_grads re-layouts it if its strides differ
         bk.model = model
         bk.master = master
 

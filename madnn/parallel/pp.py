@@ -73,6 +73,27 @@ def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None) 
     return True
 
 
+def stage_names(model: nn.Module, layers: List[nn.Module]):
+    """Original-model names of a stage's parameters and buffers, computed from module paths
+    (parameters/buffers may have been re-created by materialisation / device moves)."""
+    from ..planner.trace import FxSegment
+
+    qual = {id(m): n for n, m in model.named_modules()}
+    pnames: Dict[int, str] = {}
+    bufs = []
+    for layer in layers:
+        if isinstance(layer, FxSegment):
+            prefix, root, strip = "", layer.gm, ""
+        else:
+            q = qual.get(id(layer), "")
+            prefix, root, strip = (q + ".") if q else "", layer, ""
+        for n, p in root.named_parameters(remove_duplicate=False):
+            pnames.setdefault(id(p), prefix + n[len(strip):])
+        for n, _ in root.named_buffers(remove_duplicate=False):
+            bufs.append((prefix + n, root, n))
+    return pnames, bufs
+
+
 def restrict_optimizer(opt, params: List[nn.Parameter]):
     """A new optimizer of the same type/hyper-parameters over ``params`` only."""
     keep = {id(p) for p in params}
@@ -137,7 +158,7 @@ class PipelineEngine:
 
     def __init__(self, stage_module: StageModule, *, stage: int, nstages: int, groups: rt.ProcessGroups,
                  microbatches: int, schedule: str, loss_fn: Callable, dp_engine: DataParallel,
-                 cast_dtype, tied: List[tuple], param_names: Dict[int, str]):
+                 cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=()):
         self.module = stage_module
         self.stage, self.nstages = stage, nstages
         self.groups = groups
@@ -149,6 +170,7 @@ class PipelineEngine:
         self.cast_dtype = cast_dtype
         self.tied = tied                      # [(param, group)] on this rank
         self.param_names = param_names
+        self.buffer_refs = list(buffer_refs)   # (original name, owner module, local name)
         dev = rt.device()
         prev = groups.pp_ranks[stage - 1] if stage > 0 else None
         nxt = groups.pp_ranks[stage + 1] if stage < nstages - 1 else None
@@ -308,13 +330,17 @@ class PipelineEngine:
         return torch.cat(outs) if outs else None
 
     def state_dict(self):
-        """This stage's parameters/buffers under their ORIGINAL model names."""
+        """This stage's parameters under their ORIGINAL model names."""
         out = {}
         for p in self.module.parameters():
             name = self.param_names.get(id(p))
             if name is not None:
                 out[name] = p
         return out
+
+    def named_buffers(self):
+        for name, owner, local in self.buffer_refs:
+            yield name, owner.get_buffer(local)
 
 
 class _null:
@@ -338,7 +364,6 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     stage = groups.pp_idx
     lo, hi = plan.bounds[stage], plan.bounds[stage + 1]
     layers = plan.spine.layers[lo:hi]
-    names = {id(p): n for n, p in model.named_parameters(remove_duplicate=False)}
     stage_mod = StageModule(layers, plan.checkpoint[lo:hi])
     dev = rt.device()
     init_fn = getattr(model, "init_weights", None)
@@ -368,6 +393,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                 tied_local.append((objs[pid], grp, ranks[0]))
 
     dtype, dtype_of, cl = prepare_model(stage_mod, cfg, dev)
+    names, buffer_refs = stage_names(model, layers)
     stage_params = [p for p in stage_mod.parameters() if p.requires_grad]
     if optimizer is not None:
         optimizer = restrict_optimizer(optimizer, stage_params)
@@ -384,7 +410,8 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                              broadcast_buffers=cfg.broadcast_buffers, find_unused=True, sync_comm=cfg.sync_comm)
     engine = PipelineEngine(stage_mod, stage=stage, nstages=plan.pp, groups=groups, microbatches=plan.microbatches,
                             schedule=cfg.schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
-                            tied=[(p, g) for p, g, _ in tied_local], param_names=names)
+                            tied=[(p, g) for p, g, _ in tied_local], param_names=names,
+                            buffer_refs=buffer_refs)
     engine.plan = plan
     if optimizer is not None:
         if not _is_fused(optimizer):

@@ -1,0 +1,320 @@
+"""Tensor (model) parallelism: column/row-parallel Linear with exact conjugate
+collectives, plus the reference's ``MP*`` layer names with corrected math.
+
+Reference (nodemodule.lua): ``MPInitialLinear`` / ``MPBaseLinear`` shard the
+LAST (feature) dimension of the input across all ranks (weight ``[o, i/W]``),
+all-reduce the partial outputs, and in backward all-reduce (sum) the disjoint
+input-gradient shards; ``MPTanh`` narrows its saved output during the first
+backward pass and tiles the local gradient shard W times; the bias is added on
+every rank before the sum.  The math is exact only for W = 1 (SURVEY A-9..A-12).
+
+Here the same layers are autograd-native with the intended semantics:
+
+* row-parallel:  x_r = shard(x)  [bwd: all-gather of the input-grad shards]
+                 y   = all_reduce(x_r W_r^T) + b   [bias added once, after the sum]
+* column-parallel: x replicated [bwd: all-reduce of dx], y_r = x W_r^T + b_r,
+                 optional all-gather of the output (bwd: take the own shard)
+* ``MPTanh`` is a plain tanh: the row-parallel backward already returns the
+  full input gradient, so no narrowing/tiling is needed (the reference's
+  ``syncTanh``/``syncReshape`` flags are accepted and ignored).
+
+All TP ranks must see identical inputs (the reference's DP and MP conflict on
+this, A-15; in madnn the TP group is a sub-group of the mesh).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
+
+from .. import comm
+from .. import runtime as rt
+
+_DEBUG = {"shapes": False}
+
+
+def set_debug_shapes(on: bool = True) -> None:
+    """Print per-layer input/output/grad shapes (reference ``printDims``, nodemodule.lua:3)."""
+    _DEBUG["shapes"] = on
+
+
+def _dbg(tag, *ts):
+    if _DEBUG["shapes"]:
+        print(f"[madnn tp r{rt.get_rank()}] {tag}: " + ", ".join(str(tuple(t.shape)) for t in ts if t is not None))
+
+
+def _world(group) -> int:
+    return rt.get_world_size(group)
+
+
+def _rank(group) -> int:
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+def _gather_last(x: torch.Tensor, group) -> torch.Tensor:
+    w = _world(group)
+    if w == 1:
+        return x
+    x = x.contiguous()
+    buf = torch.empty((w,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    comm.all_gather_into(buf.view(w * x.shape[0], *x.shape[1:]) if x.dim() > 0 else buf, x, group=group)
+    return torch.cat(list(buf.unbind(0)), dim=-1)
+
+
+def _shard_last(x: torch.Tensor, group) -> torch.Tensor:
+    w = _world(group)
+    if w == 1:
+        return x
+    n = x.shape[-1]
+    if n % w:
+        raise ValueError(f"last dim {n} not divisible by TP size {w}")
+    k = n // w
+    return x.narrow(-1, _rank(group) * k, k).contiguous()
+
+
+class _Scatter(torch.autograd.Function):
+    """fwd: own shard of the last dim; bwd: all-gather of the shard grads."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return _shard_last(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather_last(g, ctx.group), None
+
+
+class _Gather(torch.autograd.Function):
+    """fwd: all-gather along the last dim; bwd: own shard."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return _gather_last(x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _shard_last(g, ctx.group), None
+
+
+class _Reduce(torch.autograd.Function):
+    """fwd: sum all-reduce; bwd: identity (the output is replicated)."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        x = x.contiguous().clone()
+        comm.all_reduce(x, "sum", group=group)
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _Copy(torch.autograd.Function):
+    """fwd: identity; bwd: sum all-reduce (a replicated input feeding sharded weights)."""
+
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().clone()
+        comm.all_reduce(g, "sum", group=ctx.group)
+        return g, None
+
+
+class RowParallelLinear(nn.Module):
+    """y = x W^T + b with W split along its INPUT dim (``[out, in/W]`` per rank)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, input_is_parallel: bool = False,
+                 group=None, device=None, dtype=None):
+        super().__init__()
+        w = _world(group)
+        if in_features % w:
+            raise ValueError(f"in_features {in_features} not divisible by TP size {w} (reference assert, "
+                             "nodemodule.lua:36,88)")
+        self.in_features, self.out_features = in_features, out_features
+        self.group, self.input_is_parallel = group, input_is_parallel
+        self.local_in = in_features // w
+        self.weight = nn.Parameter(torch.empty(out_features, self.local_in, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.empty(out_features, device=device, dtype=dtype)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # same distribution as nn.Linear over the FULL fan-in
+        bound = 1.0 / math.sqrt(self.in_features)
+        nn.init.uniform_(self.weight, -bound, bound)
+        if self.bias is not None:
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        xs = x if self.input_is_parallel else _Scatter.apply(x, self.group)
+        y = _Reduce.apply(F.linear(xs, self.weight), self.group)
+        if self.bias is not None:
+            y = y + self.bias
+        _dbg("RowParallelLinear", x, xs, y)
+        return y
+
+    @torch.no_grad()
+    def load_full(self, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
+        """Take this rank's shard from a full ``[out, in]`` weight."""
+        r = _rank(self.group)
+        self.weight.copy_(weight[:, r * self.local_in:(r + 1) * self.local_in])
+        if bias is not None and self.bias is not None:
+            self.bias.copy_(bias)
+
+    def extra_repr(self):
+        return f"in={self.in_features} (local {self.local_in}), out={self.out_features}, tp={_world(self.group)}"
+
+
+class ColumnParallelLinear(nn.Module):
+    """y = x W^T + b with W split along its OUTPUT dim (``[out/W, in]`` per rank)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, gather_output: bool = True,
+                 group=None, device=None, dtype=None):
+        super().__init__()
+        w = _world(group)
+        if out_features % w:
+            raise ValueError(f"out_features {out_features} not divisible by TP size {w}")
+        self.in_features, self.out_features = in_features, out_features
+        self.group, self.gather_output = group, gather_output
+        self.local_out = out_features // w
+        self.weight = nn.Parameter(torch.empty(self.local_out, in_features, device=device, dtype=dtype))
+        self.bias = nn.Parameter(torch.empty(self.local_out, device=device, dtype=dtype)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        bound = 1.0 / math.sqrt(self.in_features)
+        nn.init.uniform_(self.weight, -bound, bound)
+        if self.bias is not None:
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        y = F.linear(_Copy.apply(x, self.group), self.weight, self.bias)
+        out = _Gather.apply(y, self.group) if self.gather_output else y
+        _dbg("ColumnParallelLinear", x, out)
+        return out
+
+    @torch.no_grad()
+    def load_full(self, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
+        r = _rank(self.group)
+        self.weight.copy_(weight[r * self.local_out:(r + 1) * self.local_out])
+        if bias is not None and self.bias is not None:
+            self.bias.copy_(bias[r * self.local_out:(r + 1) * self.local_out])
+
+    def extra_repr(self):
+        return f"in={self.in_features}, out={self.out_features} (local {self.local_out}), tp={_world(self.group)}"
+
+
+# --------------------------------------------------------------------------
+# Reference-compatible layer names (nodemodule.lua), corrected semantics
+# --------------------------------------------------------------------------
+class MPInitialLinear(RowParallelLinear):
+    """``nn.MPInitialLinear(i, o)`` (nodemodule.lua:34-73): first FC layer, full input sharded on its last dim."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, group=None):
+        super().__init__(in_features, out_features, bias=bias, input_is_parallel=False, group=group)
+
+
+class MPBaseLinear(RowParallelLinear):
+    """``nn.MPBaseLinear(i, o)`` (nodemodule.lua:86-119): later FC layers (same math as MPInitialLinear)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, group=None):
+        super().__init__(in_features, out_features, bias=bias, input_is_parallel=False, group=group)
+
+
+class MPTanh(nn.Module):
+    """``nn.MPTanh()`` (nodemodule.lua:132-174).  ``sync`` mirrors ``syncTanh`` and is a no-op: the
+    corrected row-parallel backward already delivers the full gradient."""
+
+    def __init__(self, sync: bool = True):
+        super().__init__()
+        self.sync = sync
+
+    def forward(self, x):
+        y = torch.tanh(x)
+        _dbg("MPTanh", x, y)
+        return y
+
+
+class _Reshape(nn.Module):
+    def __init__(self, *shape):
+        super().__init__()
+        self.shape = tuple(shape[0]) if len(shape) == 1 and isinstance(shape[0], (tuple, list)) else tuple(shape)
+
+    def forward(self, x):
+        n = 1
+        for s in self.shape:
+            n *= s
+        batch = x.numel() // n
+        y = x.reshape(batch, *self.shape) if batch > 1 or x.dim() > len(self.shape) else x.reshape(self.shape)
+        _dbg(type(self).__name__, x, y)
+        return y
+
+
+class MPInitialReshape(_Reshape):
+    """``nn.MPInitialReshape(...)`` (nodemodule.lua:186-226): reshape before the first MP linear."""
+
+
+class MPBaseReshape(_Reshape):
+    """``nn.MPBaseReshape(...)`` (nodemodule.lua:238-285): reshape between MP layers (``syncReshape`` no-op)."""
+
+
+# --------------------------------------------------------------------------
+# strategy="tp": shard the large Linear layers of an arbitrary model
+# --------------------------------------------------------------------------
+def shard_linears(model: nn.Module, group=None, min_params: int = 1 << 20) -> int:
+    """Replace every ``nn.Linear`` with >= ``min_params`` weights and a TP-divisible input dim by a
+    row-parallel copy holding this rank's shard (weights taken from the original layer)."""
+    w = _world(group)
+    n = 0
+    for name, child in list(model.named_children()):
+        if type(child) is nn.Linear and child.weight.numel() >= min_params and child.in_features % w == 0:
+            new = RowParallelLinear(child.in_features, child.out_features, bias=child.bias is not None,
+                                    group=group, device=child.weight.device, dtype=child.weight.dtype)
+            new.load_full(child.weight.detach(), child.bias.detach() if child.bias is not None else None)
+            setattr(model, name, new)
+            n += 1
+        else:
+            n += shard_linears(child, group, min_params)
+    return n
+
+
+def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
+    """``distribute(model, opt, strategy="tp")``: every rank is one TP shard; replicated parameters
+    stay identical because all ranks see the same inputs, so no gradient all-reduce is needed."""
+    from ..utils.logging import get_logger
+
+    rt.init(timeout_s=cfg.timeout_s)
+    dev = rt.device()
+    model.to(dev)
+    with torch.no_grad():  # identical replicas before sharding
+        for p in model.parameters():
+            comm.broadcast(p.data, src=0)
+    old = {id(p) for p in model.parameters()}
+    n = shard_linears(model, None, int(cfg.extra.get("tp_min_params", 1 << 20)))
+    params = [p for p in model.parameters() if p.requires_grad]
+    if optimizer is not None:
+        groups = []
+        for g in optimizer.param_groups:
+            d = {k: v for k, v in g.items() if k != "params"}
+            d["params"] = [p for p in g["params"] if id(p) in {id(q) for q in params}]
+            if d["params"]:
+                groups.append(d)
+        new_params = [p for p in params if id(p) not in old]
+        if new_params:
+            if groups:
+                groups[0]["params"] = groups[0]["params"] + new_params
+            else:
+                groups = [{"params": new_params}]
+        optimizer = type(optimizer)(groups, **optimizer.defaults)
+    get_logger().info("madnn tp: sharded %d Linear layers over %d ranks", n, rt.get_world_size())
+    return model, optimizer
