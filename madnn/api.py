@@ -106,12 +106,22 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
     device = rt.device()
     strat = cfg.strategy
     plan = None
-    if strat in ("pp", "dp_pp"):
+    if strat in ("auto", "pp", "dp_pp"):
         from .planner import plan_model
 
-        plan = plan_model(model, cfg, world=rt.get_world_size(), example_input=example_input)
-        strat = plan.strategy
-        get_logger().info("madnn plan: %s", plan.describe())
+        try:
+            plan = plan_model(model, cfg, world=rt.get_world_size(), example_input=example_input,
+                              optimizer=optimizer)
+        except Exception as e:  # noqa: BLE001 - an uncostable model still trains data-parallel
+            if strat != "auto":
+                raise
+            get_logger().warning("madnn planner could not cost the model (%s); using data parallelism", e)
+            plan = None
+        if plan is not None:
+            strat = plan.strategy
+            get_logger().info("madnn plan: %s", plan.describe())
+        else:
+            strat = "dp"
     if strat in ("pp", "dp_pp"):
         from .parallel.pp import build_pipeline
 
@@ -122,10 +132,51 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
         return apply_tensor_parallel(model, optimizer, cfg)
     if strat == "none":
         return model, optimizer
-    return _distribute_dp(model, optimizer, cfg, device, loss_fn=loss_fn)
+    engine, optimizer = _distribute_dp(model, optimizer, cfg, device, loss_fn=loss_fn, plan=plan)
+    return engine, optimizer
 
 
-def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: int = 0, loss_fn=None):
+def enable_checkpointing(module: nn.Module) -> None:
+    """Activation checkpointing for one module, instance-level (state-dict keys and hooks unchanged)."""
+    if getattr(module, "_madnn_ckpt_forward", None) is not None:
+        return
+    orig = module.forward
+
+    def fwd(*args, **kwargs):
+        if module.training and torch.is_grad_enabled():
+            return torch.utils.checkpoint.checkpoint(orig, *args, use_reentrant=False, **kwargs)
+        return orig(*args, **kwargs)
+
+    module._madnn_ckpt_forward = orig
+    module.forward = fwd
+
+
+def _apply_checkpointing(model: nn.Module, cfg: Config, plan) -> int:
+    flags = None
+    layers = None
+    if plan is not None and plan.spine is not None and plan.spine.source in ("declared", "sequential"):
+        layers, flags = plan.spine.layers, plan.checkpoint
+    elif cfg.checkpointing == "all":
+        from .planner.trace import trace
+
+        sp = trace(model)
+        if sp.source in ("declared", "sequential"):
+            layers = sp.layers
+            flags = [0 < i < len(layers) - 1 or len(layers) == 1 for i in range(len(layers))]
+    if not layers or not flags:
+        return 0
+    n = 0
+    for layer, f in zip(layers, flags):
+        if f:
+            enable_checkpointing(layer)
+            n += 1
+    return n
+
+
+def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: int = 0, loss_fn=None, plan=None):
+    nck = _apply_checkpointing(model, cfg, plan) if cfg.checkpointing != "none" else 0
+    if nck:
+        get_logger().info("madnn: activation checkpointing on %d layers", nck)
     dtype, dtype_of, cl = prepare_model(model, cfg, device)
     fused = optimizer is None or _is_fused(optimizer)
     space = build_space(model, optimizer, cfg, device, dtype_of, cl)
@@ -135,7 +186,8 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
                           overlap=cfg.overlap, cast_dtype=dtype, channels_last=cl, unpack_grads=not fused,
                           broadcast_buffers=cfg.broadcast_buffers, find_unused=cfg.find_unused,
                           sync_comm=cfg.sync_comm)
-    engine.loss_fn = loss_fn
+    engine.loss_fn = loss_fn or getattr(model, "loss_fn", None)
+    engine.plan = plan
     if optimizer is not None:
         if fused:
             optimizer.bind(space)

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedLayerNorm
-from .common import SelfAttention, init_normal_, mlm_loss
+from .common import init_module_, SelfAttention, init_normal_, mlm_loss
 
 
 @dataclass
@@ -103,6 +103,10 @@ class BertForPreTraining(nn.Module):
         for layer in self.layers:
             x = layer(x)
         return self.head(x)
+
+    @staticmethod
+    def init_weights(m: nn.Module):
+        init_module_(m)
 
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]

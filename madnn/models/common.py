@@ -61,11 +61,23 @@ class RotaryEmbedding(nn.Module):
 
     def __init__(self, head_dim: int, theta: float = 10000.0, max_pos: int = 8192):
         super().__init__()
-        inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
-        t = torch.arange(max_pos, dtype=torch.float64)
+        self.head_dim, self.theta, self.max_pos = head_dim, theta, max_pos
+        cos, sin = self._tables(torch.device("cpu") if torch.empty(0).device.type == "meta" else None)
+        self.register_buffer("cos", cos, persistent=False)
+        self.register_buffer("sin", sin, persistent=False)
+
+    def _tables(self, device=None):
+        inv = 1.0 / (self.theta ** (torch.arange(0, self.head_dim, 2, dtype=torch.float64, device=device)
+                                    / self.head_dim))
+        t = torch.arange(self.max_pos, dtype=torch.float64, device=device)
         f = torch.outer(t, inv)
-        self.register_buffer("cos", torch.cat([f.cos(), f.cos()], -1).float(), persistent=False)
-        self.register_buffer("sin", torch.cat([f.sin(), f.sin()], -1).float(), persistent=False)
+        return torch.cat([f.cos(), f.cos()], -1).float(), torch.cat([f.sin(), f.sin()], -1).float()
+
+    def reset_parameters(self):
+        """Recompute the tables (after ``to_empty`` materialisation from the meta device)."""
+        cos, sin = self._tables(self.cos.device)
+        self.cos.copy_(cos)
+        self.sin.copy_(sin)
 
     @staticmethod
     def _rot(x):
@@ -77,6 +89,20 @@ class RotaryEmbedding(nn.Module):
         cos = self.cos[:s].to(q.dtype)
         sin = self.sin[:s].to(q.dtype)
         return q * cos + self._rot(q) * sin, k * cos + self._rot(k) * sin
+
+
+def init_module_(m: nn.Module, std: float = 0.02):
+    """Initialise ONE module's own tensors (used when materialising from the meta device)."""
+    with torch.no_grad():
+        if isinstance(m, nn.Linear):
+            nn.init.normal_(m.weight, 0.0, std)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, std)
+        elif hasattr(m, "reset_parameters") and not isinstance(m, (nn.Linear, nn.Embedding)):
+            if not any(True for _ in m.children()):
+                m.reset_parameters()
 
 
 def init_normal_(module: nn.Module, std: float = 0.02):

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedLayerNorm
-from .common import SelfAttention, causal_lm_loss, init_normal_, scale_residual_proj_
+from .common import init_module_, SelfAttention, causal_lm_loss, init_normal_, scale_residual_proj_
 
 
 @dataclass
@@ -109,6 +109,10 @@ class GPT2(nn.Module):
         for blk in self.h:
             x = blk(x)
         return self.head(x)
+
+    @staticmethod
+    def init_weights(m: nn.Module):
+        init_module_(m)
 
     def pipeline_layers(self):
         return [self.embed, *self.h, self.head]

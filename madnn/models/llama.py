@@ -15,7 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedRMSNorm
-from .common import RotaryEmbedding, SelfAttention, causal_lm_loss, init_normal_
+from .common import init_module_, RotaryEmbedding, SelfAttention, causal_lm_loss, init_normal_
 
 
 @dataclass
@@ -105,6 +105,10 @@ class Llama(nn.Module):
         for blk in self.layers:
             x = blk(x)
         return self.head(x)
+
+    @staticmethod
+    def init_weights(m: nn.Module):
+        init_module_(m)
 
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]

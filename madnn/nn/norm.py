@@ -30,6 +30,12 @@ class FusedLayerNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(h, device=device, dtype=dtype))
         self.bias = nn.Parameter(torch.zeros(h, device=device, dtype=dtype)) if bias else None
 
+    def reset_parameters(self):
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+            if self.bias is not None:
+                self.bias.zero_()
+
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
         """LN(x) or, with ``residual``, (LN(x + residual), x + residual) in one kernel."""
         if residual is not None and residual.dtype != x.dtype:
@@ -45,6 +51,10 @@ class FusedRMSNorm(nn.Module):
         super().__init__()
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(hidden, device=device, dtype=dtype))
+
+    def reset_parameters(self):
+        with torch.no_grad():
+            self.weight.fill_(1.0)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
         if residual is not None and residual.dtype != x.dtype:

@@ -203,6 +203,23 @@ class DataParallel(nn.Module):
             kwargs = _cast_inputs(kwargs, self.cast_dtype, self.channels_last)
         return self.module(*args, **kwargs)
 
+    def train_step(self, inputs, targets=None, loss_fn=None, microbatches: int = 1):
+        """Forward + backward of one (optionally micro-batched) step; same protocol as
+        ``PipelineEngine.train_step`` so scripts can switch strategy without changes."""
+        fn = loss_fn or getattr(self, "loss_fn", None)
+        if fn is None:
+            raise ValueError("train_step needs loss_fn= (or model.loss_fn)")
+        xs = inputs.chunk(microbatches)
+        ts = targets.chunk(microbatches) if targets is not None else [None] * len(xs)
+        total = None
+        for i, (x, t) in enumerate(zip(xs, ts)):
+            ctx = self.no_sync() if i < len(xs) - 1 else contextlib.nullcontext()
+            with ctx:
+                loss = fn(self(x), t) / len(xs)
+                loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        return total
+
     @contextlib.contextmanager
     def no_sync(self):
         """Accumulate gradients locally (microbatching) without reducing."""

@@ -115,6 +115,11 @@ class P2P:
     def __init__(self, prev: Optional[int], nxt: Optional[int], group, device):
         self.prev, self.next, self.group, self.device = prev, nxt, group, device
         self.pending = []
+        # RCCL moves device tensors directly over xGMI; a gloo group (CPU tier, or several
+        # ranks sharing one GPU in tests) stages device tensors through host memory.
+        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        self.host_staged = backend == "gloo" and torch.device(device).type == "cuda"
+        self.buf_device = torch.device("cpu") if self.host_staged else torch.device(device)
 
     def _run(self, ops):
         if not ops:
@@ -128,23 +133,27 @@ class P2P:
         out = None
         if send_t is not None and send_to is not None:
             send_t = send_t.contiguous()
+            if self.host_staged:
+                send_t = send_t.cpu()
             ops.append(dist.P2POp(dist.isend, send_t, send_to, self.group))
             self.pending.append(send_t)
         if recv_shape is not None and recv_from is not None:
-            out = torch.empty(recv_shape, dtype=recv_dtype, device=self.device)
+            out = torch.empty(recv_shape, dtype=recv_dtype, device=self.buf_device)
             ops.append(dist.P2POp(dist.irecv, out, recv_from, self.group))
         self._run(ops)
+        if out is not None and self.host_staged:
+            out = out.to(self.device)
         return out
 
     def send_meta(self, t: torch.Tensor, to: int):
-        hdr = torch.zeros(10, dtype=torch.int64, device=self.device)
+        hdr = torch.zeros(10, dtype=torch.int64, device=self.buf_device)
         hdr[0] = t.dim()
         hdr[1] = _DT_CODE[t.dtype]
         hdr[2:2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
         self._run([dist.P2POp(dist.isend, hdr, to, self.group)])
 
     def recv_meta(self, frm: int):
-        hdr = torch.empty(10, dtype=torch.int64, device=self.device)
+        hdr = torch.empty(10, dtype=torch.int64, device=self.buf_device)
         self._run([dist.P2POp(dist.irecv, hdr, frm, self.group)])
         h = hdr.tolist()
         return tuple(int(v) for v in h[2:2 + h[0]]), _CODE_DT[h[1]]

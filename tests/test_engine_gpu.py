@@ -1,0 +1,131 @@
+"""T3: engines on a real MI355X.
+
+* DP (ws=1 RCCL path: flat buckets, K4 pack on the comm stream, K1/K2 fused
+  optimizer writing the bf16 model copy, K5 fused BN, K3 LayerNorm) tracks the
+  same model trained in fp32 eager PyTorch;
+* activation checkpointing gives the same gradients as no checkpointing;
+* the pipeline engine runs on the device (2 ranks sharing the box's one GPU
+  over a gloo group — RCCL refuses two ranks per GPU) and matches the loss of
+  the unpartitioned model.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dist_utils import run_dist
+
+pytestmark = pytest.mark.gpu
+
+
+def test_resnet18_dp_bf16_tracks_fp32_eager(cuda):
+    import madnn
+    from madnn.models import resnet18
+    from madnn.optim import FusedSGD
+
+    torch.manual_seed(0)
+    model = resnet18(num_classes=10, zero_init_residual=False)
+    ref = copy.deepcopy(model).to(cuda)
+    opt = FusedSGD(model.parameters(), lr=0.02, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.02, momentum=0.9, weight_decay=1e-4)
+    dm, opt = madnn.distribute(model, opt, strategy="dp")
+    assert dm.channels_last and dm.cast_dtype == torch.bfloat16
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.randn(32, 3, 64, 64, device=cuda, generator=g)
+    y = torch.randint(0, 10, (32,), device=cuda, generator=g)
+    for step in range(4):
+        loss = F.cross_entropy(dm(x).float(), y)
+        loss.backward()
+        opt.step()
+        rl = F.cross_entropy(ref(x), y)
+        rl.backward()
+        ropt.step()
+        ropt.zero_grad()
+        assert abs(float(loss) - float(rl)) < 0.05 * max(1.0, float(rl)), (step, float(loss), float(rl))
+    # BN running stats updated by the fused kernel match eager within bf16 noise
+    for (n, b), (_, rb) in zip(dm.module.named_buffers(), ref.named_buffers()):
+        if "running_mean" in n:
+            torch.testing.assert_close(b, rb, atol=5e-2, rtol=5e-2)
+
+
+def test_gpt2_tiny_dp_bf16_tracks_fp32(cuda):
+    import madnn
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.optim import FusedAdam
+
+    torch.manual_seed(0)
+    model = GPT2(gpt2_config("gpt2-tiny"))
+    ref = copy.deepcopy(model).to(cuda)
+    opt = FusedAdam(model.parameters(), lr=3e-3, weight_decay=0.01)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=3e-3, weight_decay=0.01)
+    dm, opt = madnn.distribute(model, opt, strategy="dp")
+    ids = torch.randint(0, 512, (8, 64), device=cuda)
+    for step in range(5):
+        loss = dm.train_step(ids, ids)
+        opt.step()
+        rl = ref.loss_fn(ref(ids), ids)
+        rl.backward()
+        ropt.step()
+        ropt.zero_grad()
+        assert abs(float(loss) - float(rl)) < 3e-2 * float(rl), (step, float(loss), float(rl))
+
+
+def test_activation_checkpointing_same_grads(cuda):
+    import madnn
+    from madnn.models.bert import BertForPreTraining, bert_config
+    from madnn.optim import FusedAdam
+
+    ids = torch.randint(0, 512, (4, 64), device=cuda)
+    grads = []
+    for ck in ("none", "all"):
+        torch.manual_seed(0)
+        m = BertForPreTraining(bert_config("bert-tiny"))
+        o = FusedAdam(m.parameters(), lr=1e-3)
+        dm, o = madnn.distribute(m, o, strategy="dp", checkpointing=ck, dtype="float32")
+        loss = dm.train_step(ids, ids)
+        dm.finalize_grads()
+        grads.append([bk.grad.clone() for bk in dm.space.buckets])
+        assert torch.isfinite(loss)
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-3)
+
+
+def _w_pp_gpu(rank, world):
+    import madnn
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.optim import FusedAdam
+
+    torch.manual_seed(0)
+    model = GPT2(gpt2_config("gpt2-tiny", n_layer=4))
+    ref = copy.deepcopy(model).cuda()
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    ids = torch.randint(0, 512, (8, 64), generator=torch.Generator().manual_seed(3)).cuda()
+    eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=world, microbatches=4,
+                                example_input=ids[:1].cpu(), checkpointing="none")
+    assert next(eng.module.parameters()).is_cuda
+    loss = eng.train_step(ids, ids)
+    opt.step()
+    if eng.is_last:
+        rl = ref.loss_fn(ref(ids), ids)
+        assert abs(float(loss) - float(rl)) < 2e-2 * float(rl), (float(loss), float(rl))
+    loss2 = eng.train_step(ids, ids)
+    if eng.is_last:
+        assert float(loss2) < float(loss) + 0.5 and torch.isfinite(loss2)
+
+
+def test_pipeline_two_stages_on_device(cuda):
+    run_dist(_w_pp_gpu, 2, device="cuda", backend="gloo")
+
+
+def test_measured_costs(cuda):
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.planner import estimate, trace
+    from madnn.planner.cost import measure
+
+    m = GPT2(gpt2_config("gpt2-tiny")).to(cuda)
+    sp = trace(m)
+    x = torch.randint(0, 512, (4, 64), device=cuda)
+    costs = estimate(sp, x.cpu())
+    costs = measure(sp, x, costs)
+    assert all(c.measured and c.fwd_s > 0 for c in costs)
