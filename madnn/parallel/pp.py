@@ -185,6 +185,14 @@ class PipelineEngine:
         nxt = groups.pp_ranks[stage + 1] if stage < nstages - 1 else None
         self.p2p = P2P(prev, nxt, groups.pp_group, dev)
         self.program = native_runtime.pipeline_program(schedule, stage, nstages, microbatches)
+        # A collective over every group first: RCCL communicators exist before the first
+        # batched send/recv, which must not be a group's first operation.
+        if dist.is_initialized():
+            probe = torch.zeros(1, device=dev)
+            for g in (groups.pp_group, groups.dp_group):
+                comm.all_reduce(probe, "sum", group=g)
+            for _, g in tied:
+                comm.all_reduce(probe, "sum", group=g)
         self._sig = None
         self._in_meta = None     # (shape, dtype) of the activation this stage receives
         self._out_meta = None    # (shape, dtype) of the activation this stage sends
