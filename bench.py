@@ -63,7 +63,9 @@ def bench_resnet(args, world, rank):
     from madnn.models import resnet50
     from madnn.optim import FusedSGD
 
-    per_gpu = args.batch or 256
+    # 512 images per GPU: sized for 288 GB HBM3E (a few tens of GB of activations), and large enough
+    # that the per-step fixed costs (kernel boundaries, MIOpen workspace memsets) are amortised
+    per_gpu = args.batch or 512
     torch.manual_seed(0)
     model = resnet50()
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)

@@ -30,6 +30,12 @@ class BertConfig:
     type_vocab: int = 2
     dropout: float = 0.0
     layer_norm_eps: float = 1e-12
+    vocab_pad_multiple: int = 64
+
+    @property
+    def padded_vocab(self) -> int:
+        m = max(self.vocab_pad_multiple, 1)
+        return (self.vocab_size + m - 1) // m * m
 
 
 _SIZES = {
@@ -48,7 +54,7 @@ def bert_config(name: str = "bert-large", **over) -> BertConfig:
 class BertEmbed(nn.Module):
     def __init__(self, cfg: BertConfig):
         super().__init__()
-        self.word = nn.Embedding(cfg.vocab_size, cfg.hidden)
+        self.word = nn.Embedding(cfg.padded_vocab, cfg.hidden)
         self.position = nn.Embedding(cfg.max_position, cfg.hidden)
         self.token_type = nn.Embedding(cfg.type_vocab, cfg.hidden)
         self.norm = FusedLayerNorm(cfg.hidden, eps=cfg.layer_norm_eps)
@@ -82,7 +88,7 @@ class BertMLMHead(nn.Module):
         super().__init__()
         self.dense = nn.Linear(cfg.hidden, cfg.hidden)
         self.norm = FusedLayerNorm(cfg.hidden, eps=cfg.layer_norm_eps)
-        self.decoder = nn.Linear(cfg.hidden, cfg.vocab_size, bias=True)
+        self.decoder = nn.Linear(cfg.hidden, cfg.padded_vocab, bias=True)
         self.decoder.weight = word.weight  # tied
 
     def forward(self, x):
@@ -111,6 +117,5 @@ class BertForPreTraining(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]
 
-    @staticmethod
-    def loss_fn(logits, targets):
-        return mlm_loss(logits, targets)
+    def loss_fn(self, logits, targets):
+        return mlm_loss(logits, targets, vocab=self.config.vocab_size)

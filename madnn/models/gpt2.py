@@ -28,6 +28,12 @@ class GPT2Config:
     n_head: int = 12
     dropout: float = 0.0
     layer_norm_eps: float = 1e-5
+    vocab_pad_multiple: int = 64   # embedding/LM-head rows padded (GEMM-friendly, 16-byte rows); loss masks them
+
+    @property
+    def padded_vocab(self) -> int:
+        m = max(self.vocab_pad_multiple, 1)
+        return (self.vocab_size + m - 1) // m * m
 
 
 _SIZES = {
@@ -48,7 +54,7 @@ def gpt2_config(name: str = "gpt2-medium", **over) -> GPT2Config:
 class GPT2Embed(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+        self.wte = nn.Embedding(cfg.padded_vocab, cfg.n_embd)
         self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
         self.drop = nn.Dropout(cfg.dropout)
 
@@ -87,7 +93,7 @@ class GPT2Head(nn.Module):
     def __init__(self, cfg: GPT2Config, wte: nn.Embedding):
         super().__init__()
         self.ln_f = FusedLayerNorm(cfg.n_embd, eps=cfg.layer_norm_eps)
-        self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+        self.lm_head = nn.Linear(cfg.n_embd, cfg.padded_vocab, bias=False)
         self.lm_head.weight = wte.weight      # tied
 
     def forward(self, x):
@@ -117,9 +123,8 @@ class GPT2(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.h, self.head]
 
-    @staticmethod
-    def loss_fn(logits, targets):
-        return causal_lm_loss(logits, targets)
+    def loss_fn(self, logits, targets):
+        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size)
 
     def flops_per_token(self) -> float:
         c = self.config

@@ -113,6 +113,5 @@ class Llama(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]
 
-    @staticmethod
-    def loss_fn(logits, targets):
-        return causal_lm_loss(logits, targets)
+    def loss_fn(self, logits, targets):
+        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size)

@@ -226,13 +226,48 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
                                     training=training, momentum=momentum, eps=eps, relu=relu, residual=residual)
 
 
+# ---------------------------------------------------------------------- K6
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, shift, vocab, ignore_index):
+        lg = logits.contiguous()
+        tg = targets.contiguous()
+        loss_rows, lse = torch.ops.madnn.xent_fwd(lg, tg, bool(shift), int(vocab), int(ignore_index))
+        used = tg[:, 1:] if shift else tg
+        cnt = ((used != ignore_index) & (used >= 0) & (used < vocab)).sum().clamp(min=1).to(torch.float32)
+        ctx.save_for_backward(lg, tg, lse, cnt)
+        ctx.shift, ctx.vocab, ctx.ignore_index = shift, vocab, ignore_index
+        return loss_rows.sum() / cnt
+
+    @staticmethod
+    def backward(ctx, g):
+        lg, tg, lse, cnt = ctx.saved_tensors
+        gscale = (g.to(torch.float32) / cnt).reshape(1)
+        grad = torch.ops.madnn.xent_bwd(lg, tg, lse, ctx.shift, ctx.vocab, ctx.ignore_index, gscale)
+        return grad, None, None, None, None
+
+
+def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, *, shift: bool = False, vocab: Optional[int] = None,
+                  ignore_index: int = -100) -> torch.Tensor:
+    """Mean token cross entropy of ``logits[..., :vocab]`` (fp32 math, one fused kernel each way).
+
+    ``shift=True`` is the causal-LM form: logits[:, t] predicts targets[:, t+1] and the
+    last position carries no loss — no slicing copies of the logit matrix are made.
+    Columns >= ``vocab`` (a padded vocabulary) are excluded from the softmax."""
+    v = vocab or logits.size(-1)
+    if _is_dev(logits) and logits.dtype in (torch.bfloat16, torch.float32, torch.float16):
+        _need_native("cross_entropy")
+        return _XentFn.apply(logits, targets, shift, v, ignore_index)
+    return reference.cross_entropy(logits, targets, shift=shift, vocab=v, ignore_index=ignore_index)
+
+
 def hidden_supported(h: int) -> bool:
     return h % 8 == 0 and h <= 16384
 
 
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
-    "rms_norm", "batch_norm_act", "bn_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

@@ -33,6 +33,10 @@ int madnn_bn_supported(int);
 int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, int64_t, int, int, int, int, float, float, const float*,
                         const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*, hipStream_t);
+hipError_t madnn_xent_fwd(const void*, int, const int64_t*, int64_t, int64_t, int64_t, int, int, float*, float*,
+                          hipStream_t);
+hipError_t madnn_xent_bwd(const void*, int, const int64_t*, const float*, int64_t, int64_t, int64_t, int, int, int64_t,
+                          const float*, void*, hipStream_t);
 hipError_t madnn_bn_bwd(const void*, const void*, const void*, void*, void*, int64_t, int, int, int, const float*,
                         const float*, const float*, const float*, const float*, float*, float*, float*, float*,
                         hipStream_t);
@@ -331,12 +335,69 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
 
 bool bn_supported(int64_t C) { return madnn_bn_supported((int)C) != 0; }
 
+// ---- K6 fused softmax cross-entropy ------------------------------------------
+// logits: [N, ld] or [B, S, ld] contiguous; V <= ld valid columns.  shift: causal
+// LM (logit row (b, s) predicts target (b, s+1); the last position has no loss).
+struct XentGeom {
+  int64_t n_rows_all, n_loss_rows, seq, ld;
+};
+
+XentGeom xent_geom(const at::Tensor& logits, const at::Tensor& targets, bool shift) {
+  TORCH_CHECK(logits.is_contiguous(), "xent: logits must be contiguous");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous(), "xent: int64 contiguous targets");
+  XentGeom g;
+  g.ld = logits.size(-1);
+  g.n_rows_all = logits.numel() / g.ld;
+  TORCH_CHECK(targets.numel() == g.n_rows_all, "xent: one target per logit row");
+  if (shift) {
+    TORCH_CHECK(logits.dim() == 3, "xent shift mode needs [B, S, V] logits");
+    g.seq = logits.size(1);
+    g.n_loss_rows = logits.size(0) * (g.seq - 1);
+  } else {
+    g.seq = 0;
+    g.n_loss_rows = g.n_rows_all;
+  }
+  return g;
+}
+
+std::tuple<at::Tensor, at::Tensor> xent_fwd(const at::Tensor& logits, const at::Tensor& targets, bool shift,
+                                            int64_t V, int64_t ignore_index) {
+  check_dev(logits, "logits");
+  const XentGeom g = xent_geom(logits, targets, shift);
+  TORCH_CHECK(V > 0 && V <= g.ld, "xent: bad vocabulary size");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  auto fo = logits.options().dtype(at::kFloat);
+  at::Tensor loss = at::empty({g.n_loss_rows}, fo), lse = at::empty({g.n_loss_rows}, fo);
+  check(madnn_xent_fwd(logits.data_ptr(), dt_code(logits), targets.data_ptr<int64_t>(), g.n_loss_rows, g.seq, g.ld,
+                       (int)V, (int)ignore_index, loss.data_ptr<float>(), lse.data_ptr<float>(), cur_stream(logits)),
+        "xent_fwd");
+  return {loss, lse};
+}
+
+at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const at::Tensor& lse, bool shift, int64_t V,
+                    int64_t ignore_index, const at::Tensor& gscale) {
+  check_dev(logits, "logits");
+  const XentGeom g = xent_geom(logits, targets, shift);
+  TORCH_CHECK(gscale.scalar_type() == at::kFloat && gscale.is_cuda(), "xent: fp32 device grad scale");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  at::Tensor grad = at::empty_like(logits);
+  check(madnn_xent_bwd(logits.data_ptr(), dt_code(logits), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                       g.n_loss_rows, g.seq, g.ld, (int)V, (int)ignore_index, g.n_rows_all, gscale.data_ptr<float>(),
+                       grad.data_ptr(), cur_stream(logits)),
+        "xent_bwd");
+  return grad;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
       "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("xent_fwd(Tensor logits, Tensor targets, bool shift, int V, int ignore_index) -> (Tensor, Tensor)");
+  m.def(
+      "xent_bwd(Tensor logits, Tensor targets, Tensor lse, bool shift, int V, int ignore_index, Tensor gscale) -> "
+      "Tensor");
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? res, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, "
       "Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -368,4 +429,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("norm_bwd", norm_bwd);
   m.impl("bn_fwd", bn_fwd);
   m.impl("bn_bwd", bn_bwd);
+  m.impl("xent_fwd", xent_fwd);
+  m.impl("xent_bwd", xent_bwd);
 }

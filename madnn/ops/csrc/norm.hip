@@ -216,24 +216,35 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
 }
 
 // Column-parallel reduction of the [G][2H] partial slab: block = 32 columns x
-// 8 row-slices.
+// 32 row-slices (1024 lanes), 4 independent loads in flight per lane — the slab
+// read is latency-bound, not bandwidth-bound.
+constexpr int kWgSlices = 32;
+
 template <int WDT>
-__global__ __launch_bounds__(256) void norm_wgrad_finalize_kernel(const float* __restrict__ partial, int G, int H,
-                                                                  int has_bias, void* __restrict__ dw,
-                                                                  void* __restrict__ dbias) {
-  __shared__ float red[8][33];
+__global__ __launch_bounds__(1024) void norm_wgrad_finalize_kernel(const float* __restrict__ partial, int G, int H,
+                                                                   int has_bias, void* __restrict__ dw,
+                                                                   void* __restrict__ dbias) {
+  __shared__ float red[kWgSlices][33];
   const int lc = threadIdx.x & 31;
   const int ls = threadIdx.x >> 5;
   const int col2 = blockIdx.x * 32 + lc;  // column in [0, 2H)
   float acc = 0.f;
-  if (col2 < 2 * H)
-    for (int g = ls; g < G; g += 8) acc += partial[(int64_t)g * 2 * H + col2];
+  if (col2 < 2 * H) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int g = ls;
+    for (; g + 3 * kWgSlices < G; g += 4 * kWgSlices) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += partial[(int64_t)(g + u * kWgSlices) * 2 * H + col2];
+    }
+    for (; g < G; g += kWgSlices) a[0] += partial[(int64_t)g * 2 * H + col2];
+    acc = (a[0] + a[1]) + (a[2] + a[3]);
+  }
   red[ls][lc] = acc;
   __syncthreads();
   if (ls == 0 && col2 < 2 * H) {
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += red[k][lc];
+    for (int k = 0; k < kWgSlices; ++k) s += red[k][lc];
     if (col2 < H) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dw), col2, s);
     else if (has_bias) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dbias), col2 - H, s);
   }
@@ -317,8 +328,8 @@ hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const fl
       hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC>), dim3(G), dim3(kNormThreads), lds, stream, dy, x, w,
                          mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
       MADNN_HIP_CHECK(hipGetLastError());
-      const int fgrid = (2 * H + 31) / 32;
-      hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(256), 0, stream, workspace, G, H,
+      const int fgrid = ((has_bias ? 2 * H : H) + 31) / 32;
+      hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(32 * kWgSlices), 0, stream, workspace, G, H,
                          has_bias, dw, dbias);
     });
   });

@@ -132,3 +132,12 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
     if relu:
         y = torch.relu(y)
     return y
+
+
+def cross_entropy(logits, targets, *, shift=False, vocab=None, ignore_index=-100):
+    import torch.nn.functional as F
+
+    v = vocab or logits.size(-1)
+    if shift:
+        logits, targets = logits[:, :-1], targets[:, 1:]
+    return F.cross_entropy(logits[..., :v].reshape(-1, v).float(), targets.reshape(-1), ignore_index=ignore_index)

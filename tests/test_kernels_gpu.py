@@ -258,3 +258,26 @@ def test_fused_resnet_block_matches_eager(cuda):
     blk_cpu.load_state_dict({k: v.cpu() for k, v in blk.state_dict().items()})
     yr = blk_cpu(x.cpu())  # eager path
     torch.testing.assert_close(y.cpu(), yr, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("V,ld", [(50257, 50257), (50257, 50304), (1000, 1000), (130, 136)])
+@pytest.mark.parametrize("shift", [False, True])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fused_cross_entropy(cuda, V, ld, shift, dt):
+    """K6 vs fp32 F.cross_entropy: loss and logit gradient, padded vocab, causal shift, ignore_index."""
+    torch.manual_seed(9)
+    B, S = 3, 17
+    logits = (torch.randn(B, S, ld, device=cuda) * 3).to(dt).requires_grad_(True)
+    tg = torch.randint(0, V, (B, S), device=cuda)
+    tg[0, 3] = -100
+    loss = ops.cross_entropy(logits, tg, shift=shift, vocab=V)
+    loss.backward()
+    lr = logits.detach().float().requires_grad_(True)
+    l2, t2 = (lr[:, :-1], tg[:, 1:]) if shift else (lr, tg)
+    ref = torch.nn.functional.cross_entropy(l2[..., :V].reshape(-1, V), t2.reshape(-1), ignore_index=-100)
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref, atol=2e-3, rtol=2e-3)
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(logits.grad.float(), lr.grad, atol=tol * lr.grad.abs().max().item() + 1e-7, rtol=tol)
+    if ld > V:
+        assert logits.grad[..., V:].abs().max() == 0
