@@ -46,12 +46,18 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu (gloo; for testing the harness)")
+    ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--miopen-benchmark", type=int, default=0,
                     help="torch.backends.cudnn.benchmark (MIOpen find-mode kernel search for each conv shape)")
     return ap.parse_args()
 
 
 def _sync_all():
+    if not torch.cuda.is_available():
+        if dist.is_initialized():
+            dist.barrier()
+        return
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier(device_ids=[torch.cuda.current_device()])
@@ -75,8 +81,9 @@ def bench_resnet(args, world, rank):
     dmodel, opt = madnn.distribute(model, opt, strategy="dp", overlap=not args.no_overlap,
                                    channels_last=bool(args.channels_last), **kw)
     dev = madnn.device()
-    x, y = madnn.data.synthetic_batch("image", per_gpu, dev, dtype=torch.bfloat16,
-                                      channels_last=bool(args.channels_last), seed=1234 + rank)
+    x, y = madnn.data.synthetic_batch("image", per_gpu, dev, dtype=torch.bfloat16 if dev.type == "cuda" else
+                                      torch.float32, channels_last=bool(args.channels_last), seed=1234 + rank,
+                                      shape=(3, args.image_size, args.image_size))
 
     def step():
         out = dmodel(x)
@@ -94,7 +101,7 @@ def bench_resnet(args, world, rank):
     _sync_all()
     dt = time.perf_counter() - t0
     return dt, per_gpu * world, {"model": "resnet50", "global_batch": per_gpu * world, "per_gpu_batch": per_gpu,
-                                 "seq_len": None, "image": [3, 224, 224], "parallelism": f"dp{world}",
+                                 "seq_len": None, "image": [3, args.image_size, args.image_size], "parallelism": f"dp{world}",
                                  "optimizer": "FusedSGD(momentum=0.9)", "loss": float(loss.detach())}
 
 
@@ -142,7 +149,7 @@ def main():
     import madnn
 
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
-    madnn.init()
+    madnn.init(device=args.device)
     rank = madnn.get_rank()
     if args.model == "resnet50":
         dt, samples_per_step, config = bench_resnet(args, world, rank)
@@ -165,7 +172,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak" if args.model == "resnet50" else "strong",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "bf16" if madnn.device().type == "cuda" else "fp32",
         "data": "synthetic (random ImageNet-shaped images, random-init weights)" if args.model == "resnet50"
         else "synthetic (random tokens, random-init weights)",
         "config": config,
