@@ -154,13 +154,13 @@ def enable_checkpointing(module: nn.Module) -> None:
 def _apply_checkpointing(model: nn.Module, cfg: Config, plan) -> int:
     flags = None
     layers = None
-    if plan is not None and plan.spine is not None and plan.spine.source in ("declared", "sequential"):
+    if plan is not None and plan.spine is not None and plan.spine.source in ("declared", "sequential", "hf"):
         layers, flags = plan.spine.layers, plan.checkpoint
     elif cfg.checkpointing == "all":
         from .planner.trace import trace
 
         sp = trace(model)
-        if sp.source in ("declared", "sequential"):
+        if sp.source in ("declared", "sequential", "hf"):
             layers = sp.layers
             flags = [0 < i < len(layers) - 1 or len(layers) == 1 for i in range(len(layers))]
     if not layers or not flags:

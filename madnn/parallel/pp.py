@@ -73,24 +73,43 @@ def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None) 
     return True
 
 
-def stage_names(model: nn.Module, layers: List[nn.Module]):
-    """Original-model names of a stage's parameters and buffers, computed from module paths
-    (parameters/buffers may have been re-created by materialisation / device moves)."""
-    from ..planner.trace import FxSegment
-
+def original_names(model: nn.Module, layers: List[nn.Module]):
+    """(layer index, local name) -> original-model name for every parameter and buffer of
+    ``layers``; computed BEFORE materialisation (which may re-create the tensors)."""
+    pid = {}
+    for n, p in model.named_parameters(remove_duplicate=False):
+        pid.setdefault(id(p), n)
+    bid = {}
+    for n, b in model.named_buffers(remove_duplicate=False):
+        bid.setdefault(id(b), n)
     qual = {id(m): n for n, m in model.named_modules()}
+    pmap, bmap = {}, {}
+    for i, layer in enumerate(layers):
+        q = qual.get(id(layer))
+        for n, p in layer.named_parameters(remove_duplicate=False):
+            name = pid.get(id(p)) or ((q + "." + n) if q else None)
+            if name is not None:
+                pmap[(i, n)] = name
+        for n, b in layer.named_buffers(remove_duplicate=False):
+            name = bid.get(id(b)) or ((q + "." + n) if q else None)
+            if name is not None:
+                bmap[(i, n)] = name
+    return pmap, bmap
+
+
+def stage_names(layers: List[nn.Module], pmap, bmap):
+    """Resolve the (layer, local name) maps against the (possibly re-created) stage tensors."""
     pnames: Dict[int, str] = {}
     bufs = []
-    for layer in layers:
-        if isinstance(layer, FxSegment):
-            prefix, root, strip = "", layer.gm, ""
-        else:
-            q = qual.get(id(layer), "")
-            prefix, root, strip = (q + ".") if q else "", layer, ""
-        for n, p in root.named_parameters(remove_duplicate=False):
-            pnames.setdefault(id(p), prefix + n[len(strip):])
-        for n, _ in root.named_buffers(remove_duplicate=False):
-            bufs.append((prefix + n, root, n))
+    for i, layer in enumerate(layers):
+        for n, p in layer.named_parameters(remove_duplicate=False):
+            if (i, n) in pmap:
+                pnames.setdefault(id(p), pmap[(i, n)])
+        seen = set()
+        for n, _ in layer.named_buffers(remove_duplicate=False):
+            if (i, n) in bmap and bmap[(i, n)] not in seen:
+                seen.add(bmap[(i, n)])
+                bufs.append((bmap[(i, n)], layer, n))
     return pnames, bufs
 
 
@@ -381,12 +400,17 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     stage = groups.pp_idx
     lo, hi = plan.bounds[stage], plan.bounds[stage + 1]
     layers = plan.spine.layers[lo:hi]
+    pmap, bmap = original_names(model, layers)
     stage_mod = StageModule(layers, plan.checkpoint[lo:hi])
     dev = rt.device()
     init_fn = getattr(model, "init_weights", None)
     materialize_(stage_mod, dev, init_fn)
     stage_mod.to(dev)
     loss_fn = loss_fn or getattr(model, "loss_fn", None)
+    if loss_fn is None:
+        from ..models.hf import hf_loss_fn
+
+        loss_fn = hf_loss_fn(model)
     if loss_fn is None:
         raise ValueError("pipeline parallelism needs loss_fn= (or model.loss_fn)")
 
@@ -410,7 +434,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                 tied_local.append((objs[pid], grp, ranks[0]))
 
     dtype, dtype_of, cl = prepare_model(stage_mod, cfg, dev)
-    names, buffer_refs = stage_names(model, layers)
+    names, buffer_refs = stage_names(layers, pmap, bmap)
     stage_params = [p for p in stage_mod.parameters() if p.requires_grad]
     if optimizer is not None:
         optimizer = restrict_optimizer(optimizer, stage_params)

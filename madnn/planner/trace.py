@@ -12,7 +12,9 @@ can send over xGMI.  Three sources, tried in order:
    exactly one tensor value is live across the cut; the segments between cuts
    become ``fx.GraphModule`` layers that share the original parameters (tied
    weights stay tied).
-4. Fallback for untraceable models: the module tree's largest ``ModuleList``
+4. Hugging Face models (``madnn.models.hf``): embedding -> ``transformer.h`` /
+   ``model.layers`` / ``bert.encoder.layer`` -> head, wrapped as single-tensor layers.
+5. Fallback for untraceable models: the module tree's largest ``ModuleList``
    of identical blocks (``transformer.h``, ``model.layers``, ``encoder.layer``)
    is reported for costing, and the model is treated as one layer.
 """
@@ -142,6 +144,12 @@ def trace(model: nn.Module) -> Spine:
         return Spine(layers, names, "declared", find_block_list(model))
     if isinstance(model, nn.Sequential):
         return Spine(list(model), [n for n, _ in model.named_children()], "sequential")
+    from ..models.hf import hf_pipeline_layers
+
+    hf = hf_pipeline_layers(model)
+    if hf is not None:
+        bl = find_block_list(model)
+        return Spine(hf, [f"{type(l).__name__}{i}" for i, l in enumerate(hf)], "hf", bl)
     return _fx_split(model)
 
 
