@@ -289,32 +289,50 @@ def shard_linears(model: nn.Module, group=None, min_params: int = 1 << 20) -> in
 
 
 def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
-    """``distribute(model, opt, strategy="tp")``: every rank is one TP shard; replicated parameters
-    stay identical because all ranks see the same inputs, so no gradient all-reduce is needed."""
+    """``distribute(model, opt, strategy="tp", tp_size=T)``.
+
+    The world is laid out as ``dp x tp`` (``tp_size`` defaults to the world size).  Large
+    Linears are sharded over each TP group; replicated parameters stay identical inside a
+    TP group because its ranks see the same inputs.  With dp > 1, every parameter (shard or
+    replica) is then averaged over its DP group by the bucketed DataParallel reducer — the
+    DP group of a rank is the set of ranks holding the same TP shard index."""
+    from ..api import _distribute_dp
     from ..utils.logging import get_logger
 
     rt.init(timeout_s=cfg.timeout_s)
+    world = rt.get_world_size()
+    tp = cfg.tp_size if cfg.tp_size and cfg.tp_size > 1 else world
+    if world % tp:
+        raise ValueError(f"tp_size {tp} does not divide world size {world}")
+    groups = rt.ProcessGroups(rt.Mesh(dp=world // tp, pp=1, tp=tp))
     dev = rt.device()
     model.to(dev)
     with torch.no_grad():  # identical replicas before sharding
         for p in model.parameters():
             comm.broadcast(p.data, src=0)
     old = {id(p) for p in model.parameters()}
-    n = shard_linears(model, None, int(cfg.extra.get("tp_min_params", 1 << 20)))
+    n = shard_linears(model, groups.tp_group, int(cfg.extra.get("tp_min_params", 1 << 20)))
     params = [p for p in model.parameters() if p.requires_grad]
     if optimizer is not None:
-        groups = []
+        keep = {id(q) for q in params}
+        groups_o = []
         for g in optimizer.param_groups:
             d = {k: v for k, v in g.items() if k != "params"}
-            d["params"] = [p for p in g["params"] if id(p) in {id(q) for q in params}]
+            d["params"] = [p for p in g["params"] if id(p) in keep]
             if d["params"]:
-                groups.append(d)
+                groups_o.append(d)
         new_params = [p for p in params if id(p) not in old]
         if new_params:
-            if groups:
-                groups[0]["params"] = groups[0]["params"] + new_params
+            if groups_o:
+                groups_o[0]["params"] = groups_o[0]["params"] + new_params
             else:
-                groups = [{"params": new_params}]
-        optimizer = type(optimizer)(groups, **optimizer.defaults)
-    get_logger().info("madnn tp: sharded %d Linear layers over %d ranks", n, rt.get_world_size())
+                groups_o = [{"params": new_params}]
+        optimizer = type(optimizer)(groups_o, **optimizer.defaults)
+    get_logger().info("madnn tp: sharded %d Linear layers, mesh dp=%d x tp=%d", n, world // tp, tp)
+    if world // tp > 1:
+        engine, optimizer = _distribute_dp(model, optimizer, cfg, dev, group=groups.dp_group,
+                                           src_rank=groups.dp_ranks[0])
+        engine.groups = groups
+        return engine, optimizer
+    model.groups = groups
     return model, optimizer

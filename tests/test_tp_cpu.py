@@ -139,3 +139,34 @@ def _w_strategy_tp(rank, world):
 
 def test_distribute_strategy_tp():
     run_dist(_w_strategy_tp, 2)
+
+
+def _w_dp_tp(rank, world):
+    """dp2 x tp2: each DP replica gets half the batch; equals one process on the full batch."""
+    import madnn
+    from madnn.models import MLP
+    from madnn.optim import FusedSGD
+
+    torch.manual_seed(4)
+    m = MLP(64, 128, 10)
+    ref = MLP(64, 128, 10)
+    ref.load_state_dict(m.state_dict())
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9)
+    eng, opt = madnn.distribute(m, opt, strategy="tp", tp_size=2, tp_min_params=1000)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(5)
+    x, y = torch.randn(8, 64, generator=g), torch.randint(0, 10, (8,), generator=g)
+    d = eng.groups.dp_idx
+    for _ in range(3):
+        F.cross_entropy(eng(x[d * 4:(d + 1) * 4]), y[d * 4:(d + 1) * 4]).backward()
+        opt.step()
+        F.cross_entropy(ref(x), y).backward()
+        ropt.step()
+        ropt.zero_grad()
+    eng.eval()
+    ref.eval()
+    torch.testing.assert_close(eng(x), ref(x), atol=2e-5, rtol=2e-5)
+
+
+def test_dp2_x_tp2():
+    run_dist(_w_dp_tp, 4)
