@@ -2,7 +2,8 @@
 torchvision is not installed.  BASELINE config 2:
 "ResNet-50 auto data-parallel bf16 on 8xMI355X".
 
-Convolutions and pooling run on MIOpen through PyTorch-ROCm; every
+Convolutions run on MIOpen through PyTorch-ROCm; the stem max-pool is madnn's
+NHWC kernel (K7, byte argmax + gather backward); every
 BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
 end of each block, the residual add folded in: ``relu(bn3(conv3(h)) + idt)`` is
 one kernel forward and one backward.  The network runs channels_last (NHWC) in
@@ -17,6 +18,7 @@ import torch
 from torch import nn
 
 from ..nn.norm import FusedBatchNorm2d as BN
+from ..nn.norm import FusedMaxPool2d
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -71,7 +73,7 @@ class ResNet(nn.Module):
         self.inplanes = width
         self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
         self.bn1 = BN(width)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = FusedMaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, width, layers[0])
         self.layer2 = self._make_layer(block, width * 2, layers[1], stride=2)
         self.layer3 = self._make_layer(block, width * 4, layers[2], stride=2)

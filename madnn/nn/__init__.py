@@ -1,7 +1,7 @@
 """madnn layers: fused-kernel norms and tensor-parallel (model-parallel) layers."""
-from .norm import FusedBatchNorm2d, FusedLayerNorm, FusedRMSNorm, swap_layernorms
+from .norm import FusedBatchNorm2d, FusedLayerNorm, FusedMaxPool2d, FusedRMSNorm, swap_layernorms
 
-__all__ = ["FusedBatchNorm2d", "FusedLayerNorm", "FusedRMSNorm", "swap_layernorms"]
+__all__ = ["FusedBatchNorm2d", "FusedLayerNorm", "FusedMaxPool2d", "FusedRMSNorm", "swap_layernorms"]
 from ..parallel.tp import (ColumnParallelLinear, MPBaseLinear, MPBaseReshape, MPInitialLinear, MPInitialReshape,
                            MPTanh, RowParallelLinear, set_debug_shapes)
 

@@ -98,3 +98,14 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
                                   self.num_batches_tracked if (self.training and self.track_running_stats) else None,
                                   training=training, momentum=self.momentum, eps=self.eps, relu=relu,
                                   residual=residual)
+
+
+class FusedMaxPool2d(nn.MaxPool2d):
+    """``nn.MaxPool2d`` whose NHWC (channels_last) HIP path is the K7 kernel pair:
+    a byte-per-element argmax instead of int64 indices and a gather backward
+    (no dx memset, no scatter).  Any other input falls back to ``F.max_pool2d``."""
+
+    def forward(self, x: torch.Tensor):
+        if self.return_indices:
+            return super().forward(x)
+        return ops.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.dilation, self.ceil_mode)

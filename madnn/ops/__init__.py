@@ -171,10 +171,11 @@ def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = No
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu):
-        y, mean, invstd, scale, shift = torch.ops.madnn.bn_fwd(x, residual, weight, bias, running_mean,
-                                                                running_var, nbt, bool(training), float(momentum),
-                                                                float(eps), bool(relu))
-        ctx.save_for_backward(x, residual, weight, mean, invstd, scale, shift)
+        y, mean, invstd, scale, shift, mask = torch.ops.madnn.bn_fwd(x, residual, weight, bias, running_mean,
+                                                                      running_var, nbt, bool(training),
+                                                                      float(momentum), float(eps), bool(relu))
+        # the residual itself is not saved: with ReLU its only backward use (the mask) is the bit mask
+        ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_w = weight is not None
@@ -182,10 +183,10 @@ class _BNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, residual, weight, mean, invstd, scale, shift = ctx.saved_tensors
+        x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, residual if ctx.has_res else None, weight, mean, invstd,
-                                                  scale, shift, ctx.relu, need_w)
+        dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
+                                                  mean, invstd, scale, shift, ctx.relu, need_w)
         return (dx, dw if need_w else None, db if need_w else None, dres if ctx.has_res else None,
                 None, None, None, None, None, None, None)
 
@@ -224,6 +225,52 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
                            num_batches_tracked if training else None, training, momentum, eps, relu)
     return reference.batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked,
                                     training=training, momentum=momentum, eps=eps, relu=relu, residual=residual)
+
+
+# ---------------------------------------------------------------------- K7
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, arg = torch.ops.madnn.maxpool_fwd(x, k, s, p, True)
+        ctx.save_for_backward(arg)
+        ctx.geom = (x.size(2), x.size(3), k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        return torch.ops.madnn.maxpool_bwd(dy, arg, *ctx.geom), None, None, None
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def max_pool_supported(x: torch.Tensor, kernel_size, stride=None, padding=0, dilation=1,
+                       ceil_mode: bool = False) -> bool:
+    """Layouts/geometries the K7 NHWC max-pool kernel handles."""
+    k, s, p, d = _pair(kernel_size), _pair(stride if stride else kernel_size), _pair(padding), _pair(dilation)
+    if x.device.type != "cuda" or x.dtype not in (torch.bfloat16, torch.float32, torch.float16):
+        return False
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.size(1) % 8:
+        return False
+    if k[0] != k[1] or s[0] != s[1] or p[0] != p[1] or d != (1, 1) or ceil_mode:
+        return False
+    return k[0] * k[0] <= 255 and 2 * p[0] <= k[0] and x.numel() < 2**31
+
+
+def max_pool2d(x: torch.Tensor, kernel_size, stride=None, padding=0, dilation=1, ceil_mode: bool = False):
+    """Square max-pooling; NHWC device tensors run the K7 kernels (argmax kept as one byte per
+    output element, gather backward), everything else ``F.max_pool2d``."""
+    if max_pool_supported(x, kernel_size, stride, padding, dilation, ceil_mode):
+        _need_native("max_pool2d")
+        k = _pair(kernel_size)[0]
+        s = _pair(stride if stride else kernel_size)[0]
+        p = _pair(padding)[0]
+        if torch.is_grad_enabled() and x.requires_grad:
+            return _MaxPoolFn.apply(x, k, s, p)
+        return torch.ops.madnn.maxpool_fwd(x, k, s, p, False)[0]
+    return torch.nn.functional.max_pool2d(x, kernel_size, stride, padding, dilation, ceil_mode)
 
 
 # ---------------------------------------------------------------------- K6

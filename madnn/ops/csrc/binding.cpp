@@ -31,15 +31,20 @@ hipError_t madnn_norm_bwd(const void*, const void*, const void*, const float*, c
                           void*, float*, int64_t, int, int, int, int, hipStream_t);
 int madnn_bn_supported(int);
 int madnn_bn_partial_rows(int64_t, int);
-hipError_t madnn_bn_fwd(const void*, const void*, void*, int64_t, int, int, int, int, float, float, const float*,
-                        const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*, hipStream_t);
+hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
+                        const float*, const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*,
+                        hipStream_t);
+int madnn_maxpool_supported(int64_t, int, int);
+hipError_t madnn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+hipError_t madnn_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int,
+                             hipStream_t);
 hipError_t madnn_xent_fwd(const void*, int, const int64_t*, int64_t, int64_t, int64_t, int, int, float*, float*,
                           hipStream_t);
 hipError_t madnn_xent_bwd(const void*, int, const int64_t*, const float*, int64_t, int64_t, int64_t, int, int, int64_t,
                           const float*, void*, hipStream_t);
-hipError_t madnn_bn_bwd(const void*, const void*, const void*, void*, void*, int64_t, int, int, int, const float*,
-                        const float*, const float*, const float*, const float*, float*, float*, float*, float*,
-                        hipStream_t);
+hipError_t madnn_bn_bwd(const void*, const void*, const unsigned char*, int, void*, void*, int64_t, int, int, int,
+                        const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
+                        float*, hipStream_t);
 }
 
 namespace {
@@ -272,7 +277,7 @@ const float* optf(const c10::optional<at::Tensor>& t) {
 
 float* optf_mut(const c10::optional<at::Tensor>& t) { return const_cast<float*>(optf(t)); }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fwd(
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fwd(
     const at::Tensor& x, const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& w,
     const c10::optional<at::Tensor>& b, const c10::optional<at::Tensor>& run_mean,
     const c10::optional<at::Tensor>& run_var, const c10::optional<at::Tensor>& nbt, bool training, double momentum,
@@ -289,22 +294,26 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_fwd(
   at::Tensor save_mean = at::empty({C}, fo), save_invstd = at::empty({C}, fo);
   at::Tensor scale = at::empty({C}, fo), shift = at::empty({C}, fo);
   at::Tensor ws = at::empty({training ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C : 1}, fo);
+  // training with a fused residual + ReLU: 1-bit ReLU mask for the backward passes
+  const bool need_mask = training && relu && res.has_value();
+  at::Tensor mask = at::empty({need_mask ? x.numel() / 8 : 0}, x.options().dtype(at::kByte));
   int64_t* nb = nullptr;
   if (nbt.has_value() && nbt->defined()) {
     TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "num_batches_tracked must be an int64 device tensor");
     nb = nbt->data_ptr<int64_t>();
   }
-  check(madnn_bn_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, y.data_ptr(), M, (int)C, dt_code(x),
+  check(madnn_bn_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, y.data_ptr(),
+                     need_mask ? mask.data_ptr<uint8_t>() : nullptr, M, (int)C, dt_code(x),
                      relu ? 1 : 0, training ? 1 : 0, (float)eps, (float)momentum, optf(w), optf(b),
                      training ? optf_mut(run_mean) : const_cast<float*>(optf(run_mean)), optf_mut(run_var),
                      training ? nb : nullptr, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                      scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(x)),
         "bn_fwd");
-  return {y, save_mean, save_invstd, scale, shift};
+  return {y, save_mean, save_invstd, scale, shift, mask};
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
-    const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& res,
+    const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& mask, bool has_res,
     const c10::optional<at::Tensor>& w, const at::Tensor& save_mean, const at::Tensor& save_invstd,
     const at::Tensor& scale, const at::Tensor& shift, bool relu, bool need_wgrad) {
   check_dev(x, "x");
@@ -317,12 +326,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
     dyc.copy_(dy);
   }
   at::Tensor dx = at::empty_like(x);
-  at::Tensor dres = res.has_value() ? at::empty_like(x) : at::Tensor();
+  at::Tensor dres = has_res ? at::empty_like(x) : at::Tensor();
+  const uint8_t* mk = nullptr;
+  if (relu && has_res) {
+    TORCH_CHECK(mask.has_value() && mask->numel() == x.numel() / 8, "bn_bwd: ReLU bit mask required");
+    mk = mask->data_ptr<uint8_t>();
+  }
   auto fo = x.options().dtype(at::kFloat);
   at::Tensor dw = at::empty({C}, fo), db = at::empty({C}, fo);
   at::Tensor coef = at::empty({3 * C}, fo);
   at::Tensor ws = at::empty({(int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
-  check(madnn_bn_bwd(dyc.data_ptr(), x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr, dx.data_ptr(),
+  check(madnn_bn_bwd(dyc.data_ptr(), x.data_ptr(), mk, has_res ? 1 : 0, dx.data_ptr(),
                      dres.defined() ? dres.data_ptr() : nullptr, M, (int)C, dt_code(x), relu ? 1 : 0, optf(w),
                      save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), scale.data_ptr<float>(),
                      shift.data_ptr<float>(), need_wgrad ? dw.data_ptr<float>() : nullptr,
@@ -388,19 +402,58 @@ at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const a
   return grad;
 }
 
+// K7 NHWC max-pool.  x: [N, C, H, W] in channels_last.  Returns (y, argmax bytes);
+// argmax is empty when need_arg is false (inference).
+std::tuple<at::Tensor, at::Tensor> maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p, bool need_arg) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool: NHWC 4-D input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(madnn_maxpool_supported(x.numel(), (int)C, (int)k), "maxpool: unsupported shape");
+  TORCH_CHECK(k > 0 && s > 0 && p >= 0 && 2 * p <= k, "maxpool: bad window");
+  const int64_t Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: empty output");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor arg = at::empty({need_arg ? N * Ho * Wo * C : 0}, x.options().dtype(at::kByte));
+  check(madnn_maxpool_fwd(x.data_ptr(), y.data_ptr(), need_arg ? arg.data_ptr() : nullptr, (int)N, (int)H, (int)W,
+                          (int)C, (int)Ho, (int)Wo, (int)k, (int)s, (int)p, dt_code(x), cur_stream(x)),
+        "maxpool_fwd");
+  return {y, arg};
+}
+
+at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W, int64_t k, int64_t s,
+                       int64_t p) {
+  check_dev(dy, "dy");
+  TORCH_CHECK(dy.dim() == 4, "maxpool_bwd: 4-D grad");
+  const int64_t N = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(arg.numel() == dy.numel() && arg.scalar_type() == at::kByte, "maxpool_bwd: argmax map mismatch");
+  TORCH_CHECK(Ho == (H + 2 * p - k) / s + 1 && Wo == (W + 2 * p - k) / s + 1, "maxpool_bwd: geometry mismatch");
+  at::Tensor dyc = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  TORCH_CHECK(madnn_maxpool_supported(dx.numel(), (int)C, (int)k), "maxpool_bwd: unsupported shape");
+  check(madnn_maxpool_bwd(dyc.data_ptr(), arg.data_ptr(), dx.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)Ho,
+                          (int)Wo, (int)k, (int)s, (int)p, dt_code(dy), cur_stream(dy)),
+        "maxpool_bwd");
+  return dx;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
-      "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
+      "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor, Tensor, "
+      "Tensor)");
   m.def("xent_fwd(Tensor logits, Tensor targets, bool shift, int V, int ignore_index) -> (Tensor, Tensor)");
   m.def(
       "xent_bwd(Tensor logits, Tensor targets, Tensor lse, bool shift, int V, int ignore_index, Tensor gscale) -> "
       "Tensor");
   m.def(
-      "bn_bwd(Tensor dy, Tensor x, Tensor? res, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, "
-      "Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
+      "bn_bwd(Tensor dy, Tensor x, Tensor? mask, bool has_res, Tensor? w, Tensor save_mean, Tensor save_invstd, "
+      "Tensor scale, Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
+  m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
   m.def("bucket_unpack(Tensor(a!)[] dsts, Tensor flat, int[] offsets, float scale) -> ()");
   m.def("flat_scale_cast(Tensor src, Tensor(a!) dst, float scale) -> ()");
@@ -431,4 +484,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("bn_bwd", bn_bwd);
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
+  m.impl("maxpool_fwd", maxpool_fwd);
+  m.impl("maxpool_bwd", maxpool_bwd);
 }

@@ -174,11 +174,13 @@ __global__ void bn_eval_coef_kernel(int C, float eps, const float* __restrict__ 
 }
 
 // y = act(x*scale + shift + res)
+// RELU && RES: also write the ReLU mask as bits (1 byte per 8 elements), so the
+// backward passes need neither the residual nor the affine recompute for it.
 template <int XDT, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, void* __restrict__ y,
-                                                       int64_t total, int C) {
+                                                       unsigned char* __restrict__ mask, int64_t total, int C) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
   const int sC = (int)(stride % C);  // channel advance per grid-stride step (no 64-bit modulo in the loop)
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
@@ -190,22 +192,31 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
     load8<kF32>(shift, c0, sh);
     float r[8];
     if constexpr (RES) load8<XDT>(res, i, r);
+    unsigned bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float z = v[j] * sc[j] + sh[j];
       if constexpr (RES) z += r[j];
-      if constexpr (RELU) z = z > 0.f ? z : 0.f;
+      if constexpr (RELU) {
+        bits |= (z > 0.f ? 1u : 0u) << j;
+        z = z > 0.f ? z : 0.f;
+      }
       v[j] = z;
     }
     store8<XDT>(y, i, v);
+    if constexpr (RELU && RES) {
+      if (mask) mask[i >> 3] = (unsigned char)bits;
+    }
   }
 }
 
 // Backward reduction: g = dy * [z > 0] (ReLU mask recomputed from x),
 // partial[blk][0:C] = sum g, partial[blk][C:2C] = sum g * x
-template <int XDT, bool RELU, bool RES>
+// MASKED (RELU && residual): the ReLU mask comes from the forward's bit mask;
+// plain RELU recomputes it from x (which is read anyway).
+template <int XDT, bool RELU, bool MASKED>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
-    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ res,
+    const void* __restrict__ dy, const void* __restrict__ x, const unsigned char* __restrict__ mask,
     const float* __restrict__ scale, const float* __restrict__ shift, int64_t M, int C,
     float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float slab[];
@@ -218,42 +229,47 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
   if (active) {
-    if constexpr (RELU) {
+    if constexpr (RELU && !MASKED) {
       load8<kF32>(scale, cg * 8, sc);
       load8<kF32>(shift, cg * 8, sh);
     }
     const int64_t step = (int64_t)gridDim.x * g.rpi;
     int64_t r = (int64_t)blockIdx.x * g.rpi + rs;
-    auto body = [&](const float (&dv)[8], const float (&xv)[8], const float (&rv)[8]) {
+    auto body = [&](const float (&dv)[8], const float (&xv)[8], unsigned bits) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float gj = dv[j];
         if constexpr (RELU) {
-          float z = xv[j] * sc[j] + sh[j];
-          if constexpr (RES) z += rv[j];
-          gj = z > 0.f ? gj : 0.f;
+          if constexpr (MASKED) {
+            gj = ((bits >> j) & 1u) ? gj : 0.f;
+          } else {
+            const float z = xv[j] * sc[j] + sh[j];
+            gj = z > 0.f ? gj : 0.f;
+          }
         }
         sg[j] += gj;
         sgx[j] += gj * xv[j];
       }
     };
-    for (; r + step < M; r += 2 * step) {  // 2 rows x (dy, x[, res]) in flight per lane
-      float dv[2][8], xv[2][8], rv[2][8];
+    for (; r + step < M; r += 2 * step) {  // 2 rows x (dy, x[, mask]) in flight per lane
+      float dv[2][8], xv[2][8];
+      unsigned mb[2] = {0u, 0u};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         load8<XDT>(dy, (r + u * step) * C + cg * 8, dv[u]);
         load8<XDT>(x, (r + u * step) * C + cg * 8, xv[u]);
-        if constexpr (RELU && RES) load8<XDT>(res, (r + u * step) * C + cg * 8, rv[u]);
+        if constexpr (MASKED) mb[u] = mask[((r + u * step) * C + cg * 8) >> 3];
       }
-      body(dv[0], xv[0], rv[0]);
-      body(dv[1], xv[1], rv[1]);
+      body(dv[0], xv[0], mb[0]);
+      body(dv[1], xv[1], mb[1]);
     }
     for (; r < M; r += step) {
-      float dv[8], xv[8], rv[8];
+      float dv[8], xv[8];
       load8<XDT>(dy, r * C + cg * 8, dv);
       load8<XDT>(x, r * C + cg * 8, xv);
-      if constexpr (RELU && RES) load8<XDT>(res, r * C + cg * 8, rv);
-      body(dv, xv, rv);
+      unsigned mb = 0u;
+      if constexpr (MASKED) mb = mask[(r * C + cg * 8) >> 3];
+      body(dv, xv, mb);
     }
   }
   if (g.rpi == 1) {
@@ -336,7 +352,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
 
 template <int XDT, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ res,
+    const void* __restrict__ dy, const void* __restrict__ x, const unsigned char* __restrict__ mask,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ ca,
     const float* __restrict__ cb, const float* __restrict__ cc, void* __restrict__ dx, void* __restrict__ dres,
     int64_t total, int C) {
@@ -345,21 +361,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   int c0 = (int)(i % C);
   for (; i < total; i += stride, c0 = (c0 + sC >= C) ? c0 + sC - C : c0 + sC) {
-    float dv[8], xv[8], rv[8], a[8], b[8], c[8];
+    float dv[8], xv[8], a[8], b[8], c[8];
     load8<XDT>(dy, i, dv);
     load8<XDT>(x, i, xv);
     load8<kF32>(ca, c0, a);
     load8<kF32>(cb, c0, b);
     load8<kF32>(cc, c0, c);
-    if constexpr (RELU) {
+    if constexpr (RELU && RES) {
+      const unsigned bits = mask[i >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[j] = ((bits >> j) & 1u) ? dv[j] : 0.f;
+    } else if constexpr (RELU) {
       float sc[8], sh[8];
       load8<kF32>(scale, c0, sc);
       load8<kF32>(shift, c0, sh);
-      if constexpr (RES) load8<XDT>(res, i, rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float z = xv[j] * sc[j] + sh[j];
-        if constexpr (RES) z += rv[j];
+        const float z = xv[j] * sc[j] + sh[j];
         dv[j] = z > 0.f ? dv[j] : 0.f;
       }
     }
@@ -392,10 +410,10 @@ int madnn_bn_supported(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 :
 int madnn_bn_partial_rows(int64_t M, int C) { return madnn::bn_grid_rows(M, C); }
 
 // Forward. training: compute batch stats (+ running update); else use running stats.
-hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C, int xdt, int relu,
-                        int training, float eps, float momentum, const float* w, const float* b, float* run_mean,
-                        float* run_var, int64_t* nbt, float* save_mean, float* save_invstd, float* scale,
-                        float* shift, float* workspace, hipStream_t stream) {
+hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, unsigned char* mask, int64_t M, int C, int xdt,
+                        int relu, int training, float eps, float momentum, const float* w, const float* b,
+                        float* run_mean, float* run_var, int64_t* nbt, float* save_mean, float* save_invstd,
+                        float* scale, float* shift, float* workspace, hipStream_t stream) {
   using namespace madnn;
   if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
@@ -418,25 +436,25 @@ hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, int64_t M, int 
   const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, res != nullptr, RELU, RES, {
     hipLaunchKernelGGL((bn_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, x, res, scale, shift, y,
-                       total, C);
+                       mask, total, C);
   }));
   return hipGetLastError();
 }
 
-hipError_t madnn_bn_bwd(const void* dy, const void* x, const void* res, void* dx, void* dres, int64_t M, int C,
-                        int xdt, int relu, const float* w, const float* save_mean, const float* save_invstd,
-                        const float* scale, const float* shift, float* dw, float* db, float* coef,
-                        float* workspace, hipStream_t stream) {
+hipError_t madnn_bn_bwd(const void* dy, const void* x, const unsigned char* mask, int has_res, void* dx, void* dres,
+                        int64_t M, int C, int xdt, int relu, const float* w, const float* save_mean,
+                        const float* save_invstd, const float* scale, const float* shift, float* dw, float* db,
+                        float* coef, float* workspace, hipStream_t stream) {
   using namespace madnn;
   if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   const int G = bn_grid_rows(M, C);
   const BnGeom g = bn_geom(C);
   const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
-  const bool has_res = res != nullptr;
+  if (relu && has_res && mask == nullptr) return hipErrorInvalidValue;
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<XDT, RELU, RES>), dim3(G), dim3(kBnThreads), lds, stream, dy, x, res,
-                       scale, shift, M, C, workspace);
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<XDT, RELU, RELU && RES>), dim3(G), dim3(kBnThreads), lds, stream, dy, x,
+                       mask, scale, shift, M, C, workspace);
   }));
   MADNN_HIP_CHECK(hipGetLastError());
   float* ca = coef;
@@ -448,7 +466,7 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const void* res, void* dx
   const int64_t total = M * C;
   const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, dy, x, res, scale,
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, dy, x, mask, scale,
                        shift, ca, cb, cc, dx, dres, total, C);
   }));
   return hipGetLastError();

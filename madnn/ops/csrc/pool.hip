@@ -1,0 +1,137 @@
+// K7: NHWC max-pooling forward/backward for gfx950 (the ResNet stem pool).
+//
+// PyTorch-ROCm's channels_last max_pool2d writes an int64 index per output
+// element (4x the output bytes in bf16) and its backward scatters through
+// those indices after a full memset of dx.  Here:
+//   forward : one lane = one output pixel x 8 channels; the k*k window is read
+//             with 16-byte loads, the result written with one 16-byte store and
+//             the window position of each max as one byte (8 bytes per lane,
+//             one 64-bit store).  Eval-mode forward skips the byte map.
+//   backward: gather, not scatter: one lane = one INPUT pixel x 8 channels; it
+//             visits the (at most ceil(k/s)^2) output pixels whose windows hold
+//             it, and sums dy where the stored byte names its position.  Every
+//             dx element is written exactly once: no memset, no atomics.
+// Tie-breaking/NaN follow ATen (first max in scan order; NaN wins).
+// Index math is 32-bit: the host refuses tensors with >= 2^31 elements.
+#include "common.h"
+
+namespace madnn {
+
+template <int XDT>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                          uint64_t* __restrict__ arg, int N, int H, int W, int C,
+                                                          int Ho, int Wo, int k, int s, int p) {
+  const unsigned CG = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * Ho * Wo * CG;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned cg = idx % CG;
+    const unsigned pix = idx / CG;
+    const int ow = (int)(pix % (unsigned)Wo);
+    const unsigned t = pix / (unsigned)Wo;
+    const int oh = (int)(t % (unsigned)Ho);
+    const int n = (int)(t / (unsigned)Ho);
+    const int h0 = oh * s - p, w0 = ow * s - p;
+    const int kh0 = h0 < 0 ? -h0 : 0, kw0 = w0 < 0 ? -w0 : 0;
+    const int kh1 = min(k, H - h0), kw1 = min(k, W - w0);
+    float best[8];
+    unsigned char a[8];
+    const unsigned char first = (unsigned char)(kh0 * k + kw0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -__builtin_inff();
+      a[j] = first;
+    }
+    for (int kh = kh0; kh < kh1; ++kh) {
+      const unsigned rowbase = ((unsigned)(n * H + h0 + kh) * W) * C + cg * 8;
+      for (int kw = kw0; kw < kw1; ++kw) {
+        float v[8];
+        load8<XDT>(x, rowbase + (unsigned)(w0 + kw) * C, v);
+        const unsigned char pos = (unsigned char)(kh * k + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (v[j] > best[j] || __builtin_isnan(v[j])) {
+            best[j] = v[j];
+            a[j] = pos;
+          }
+        }
+      }
+    }
+    store8<XDT>(y, (int64_t)pix * C + cg * 8, best);
+    if (arg) {
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) packed |= (uint64_t)a[j] << (8 * j);
+      arg[idx] = packed;
+    }
+  }
+}
+
+template <int XDT>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const void* __restrict__ dy,
+                                                          const uint64_t* __restrict__ arg, void* __restrict__ dx,
+                                                          int N, int H, int W, int C, int Ho, int Wo, int k, int s,
+                                                          int p) {
+  const unsigned CG = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CG;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned cg = idx % CG;
+    const unsigned pix = idx / CG;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    // output rows/cols whose window [o*s-p, o*s-p+k) contains h / w
+    const int nh = h + p - (k - 1), nw = w + p - (k - 1);
+    const int oh_lo = nh <= 0 ? 0 : (nh + s - 1) / s;
+    const int ow_lo = nw <= 0 ? 0 : (nw + s - 1) / s;
+    const int oh_hi = min(Ho - 1, (h + p) / s);
+    const int ow_hi = min(Wo - 1, (w + p) / s);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const unsigned oidx = ((unsigned)(n * Ho + oh) * Wo + ow) * CG + cg;
+        const uint64_t packed = arg[oidx];
+        const unsigned pos = (unsigned)((h - (oh * s - p)) * k + (w - (ow * s - p)));
+        float g[8];
+        load8<XDT>(dy, (int64_t)oidx * 8, g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += (((packed >> (8 * j)) & 0xffu) == pos) ? g[j] : 0.f;
+      }
+    }
+    store8<XDT>(dx, (int64_t)idx * 8, acc);
+  }
+}
+
+}  // namespace madnn
+
+using namespace madnn;
+
+extern "C" {
+
+int madnn_maxpool_supported(int64_t numel, int C, int k) { return numel < (1ll << 31) && C % 8 == 0 && k * k <= 255; }
+
+hipError_t madnn_maxpool_fwd(const void* x, void* y, void* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
+                             int s, int p, int xdt, hipStream_t stream) {
+  const int64_t work = (int64_t)N * Ho * Wo * (C / 8);
+  const int grid = stream_grid(work, 256, 16 * kNumCU);
+  MADNN_DISPATCH_DT(xdt, XDT, {
+    hipLaunchKernelGGL((maxpool_fwd_kernel<XDT>), dim3(grid), dim3(256), 0, stream, x, y,
+                       static_cast<uint64_t*>(arg), N, H, W, C, Ho, Wo, k, s, p);
+  });
+  return hipGetLastError();
+}
+
+hipError_t madnn_maxpool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int Ho, int Wo,
+                             int k, int s, int p, int xdt, hipStream_t stream) {
+  const int64_t work = (int64_t)N * H * W * (C / 8);
+  const int grid = stream_grid(work, 256, 16 * kNumCU);
+  MADNN_DISPATCH_DT(xdt, XDT, {
+    hipLaunchKernelGGL((maxpool_bwd_kernel<XDT>), dim3(grid), dim3(256), 0, stream, dy,
+                       static_cast<const uint64_t*>(arg), dx, N, H, W, C, Ho, Wo, k, s, p);
+  });
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -281,3 +281,40 @@ def test_fused_cross_entropy(cuda, V, ld, shift, dt):
     torch.testing.assert_close(logits.grad.float(), lr.grad, atol=tol * lr.grad.abs().max().item() + 1e-7, rtol=tol)
     if ld > V:
         assert logits.grad[..., V:].abs().max() == 0
+
+
+@pytest.mark.parametrize("geom", [(3, 2, 1, 16, 16), (3, 2, 1, 15, 13), (2, 2, 0, 8, 10), (3, 1, 1, 9, 7),
+                                  (5, 3, 2, 17, 11)])
+@pytest.mark.parametrize("C", [8, 64, 200])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_maxpool_nhwc(cuda, geom, C, dt):
+    """K7 NHWC max-pool fwd/bwd vs F.max_pool2d on the same (fp32-upcast) values: exact."""
+    k, s, p, H, W = geom
+    torch.manual_seed(11)
+    x = torch.randn(3, C, H, W, device=cuda).to(dt).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    assert ops.max_pool_supported(x, k, s, p)
+    y = ops.max_pool2d(x, k, s, p)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, k, s, p)
+    yr.backward(dy.float())
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, atol=0, rtol=0)
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-6  # overlapping windows sum in fp32, round once to bf16
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol, rtol=tol)
+    with torch.no_grad():
+        torch.testing.assert_close(ops.max_pool2d(x, k, s, p), y.detach(), atol=0, rtol=0)
+
+
+def test_maxpool_module_fallback_and_resnet_stem(cuda):
+    """FusedMaxPool2d: NCHW input falls back to ATen; the ResNet stem shape runs K7."""
+    from madnn.nn import FusedMaxPool2d
+
+    m = FusedMaxPool2d(3, 2, 1)
+    x = torch.randn(2, 64, 112, 112, device=cuda).bfloat16()
+    torch.testing.assert_close(m(x), torch.nn.functional.max_pool2d(x, 3, 2, 1))
+    xc = x.contiguous(memory_format=torch.channels_last)
+    assert ops.max_pool_supported(xc, 3, 2, 1)
+    torch.testing.assert_close(m(xc), torch.nn.functional.max_pool2d(x, 3, 2, 1), atol=0, rtol=0)
