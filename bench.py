@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu (gloo; for testing the harness)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--miopen-benchmark", type=int, default=0,
-                    help="torch.backends.cudnn.benchmark (MIOpen find-mode kernel search for each conv shape)")
+                    help="torch.backends.cudnn.benchmark (MIOpen find).  Both modes read the shipped MI355X "
+                         "find-db (madnn/tuning/miopen, seeded by madnn.init), so 0 already runs the tuned solvers")
     return ap.parse_args()
 
 
@@ -92,6 +93,7 @@ def bench_resnet(args, world, rank):
         opt.step()
         return loss
 
+    tw = time.perf_counter()
     for _ in range(args.warmup):
         step()
     _sync_all()
@@ -100,7 +102,7 @@ def bench_resnet(args, world, rank):
         loss = step()
     _sync_all()
     dt = time.perf_counter() - t0
-    return dt, per_gpu * world, {"model": "resnet50", "global_batch": per_gpu * world, "per_gpu_batch": per_gpu,
+    return dt, per_gpu * world, {"warmup_s": round(t0 - tw, 1), "model": "resnet50", "global_batch": per_gpu * world, "per_gpu_batch": per_gpu,
                                  "seq_len": None, "image": [3, args.image_size, args.image_size], "parallelism": f"dp{world}",
                                  "optimizer": "FusedSGD(momentum=0.9)", "loss": float(loss.detach())}
 

@@ -43,6 +43,9 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0, device: Option
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and device != "cpu"
     if use_gpu:
+        from ..utils.miopen import setup_find_db
+
+        setup_find_db()  # shipped MI355X MIOpen find-db: tuned conv solvers without a search
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
         dev = torch.device("cuda", torch.cuda.current_device())
     else:

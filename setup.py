@@ -24,7 +24,7 @@ setup(
     version="0.1.0",
     description="MI355X-native automatic distributed training (data/pipeline/tensor parallel, gfx950 HIP kernels)",
     packages=find_packages(include=["madnn", "madnn.*"]),
-    package_data={"madnn.ops": ["csrc/*", "*.so"]},
+    package_data={"madnn.ops": ["csrc/*", "*.so"], "madnn": ["tuning/miopen/*.txt"]},
     python_requires=">=3.9",
     install_requires=["torch>=2.4", "safetensors"],
     cmdclass={"build_py": BuildNative},

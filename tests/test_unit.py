@@ -316,3 +316,17 @@ def test_kernel_library_built_for_gfx950():
     for f in os.listdir("/tmp"):
         if f.startswith(so.name + "."):
             os.remove(os.path.join("/tmp", f))
+
+
+def test_miopen_find_db_seeding(tmp_path, monkeypatch):
+    """setup_find_db copies the shipped MI355X find/perf dbs into a writable dir and exports
+    MIOPEN_USER_DB_PATH, but never overrides a path the user already set."""
+    from madnn.utils import miopen
+
+    shipped = sorted(p.name for p in miopen.SHIPPED_DB.iterdir() if p.name.endswith(".txt"))
+    assert any(n.endswith(".ufdb.txt") for n in shipped) and any(n.endswith(".udb.txt") for n in shipped)
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH", raising=False)
+    got = miopen.setup_find_db(workdir=tmp_path / "db")
+    assert got == str(tmp_path / "db") and sorted(p.name for p in (tmp_path / "db").iterdir()) == shipped
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", "/somewhere/else")
+    assert miopen.setup_find_db() == "/somewhere/else"
