@@ -81,7 +81,7 @@ def main():
     if meta and a.strategy in ("dp", "auto") and world == 1:
         from madnn.parallel.pp import materialize_
 
-        materialize_(model, dev, getattr(model, "init_weights", None))
+        materialize_(model, dev, getattr(model, "init_weights", None), opt)
     eng, opt = madnn.distribute(model, opt, strategy=a.strategy, pp_stages=a.pp, microbatches=a.microbatches,
                                 checkpointing=a.checkpointing, example_input=example, loss_fn=loss_fn,
                                 global_batch=a.batch)

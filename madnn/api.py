@@ -174,6 +174,12 @@ def _apply_checkpointing(model: nn.Module, cfg: Config, plan) -> int:
 
 
 def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: int = 0, loss_fn=None, plan=None):
+    from .parallel.pp import materialize_
+
+    # a model built on the meta device (e.g. 8B weights never held on the host) is allocated
+    # straight on this rank's GPU; the optimizer is re-pointed at the real parameters
+    if materialize_(model, device, getattr(model, "init_weights", None), optimizer):
+        get_logger().info("madnn: materialised meta-device model on %s", device)
     nck = _apply_checkpointing(model, cfg, plan) if cfg.checkpointing != "none" else 0
     if nck:
         get_logger().info("madnn: activation checkpointing on %d layers", nck)

@@ -59,10 +59,14 @@ class StageModule(nn.Module):
         return x
 
 
-def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None) -> bool:
-    """Allocate META parameters/buffers of ``module`` on ``device`` and initialise them."""
+def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None, optimizer=None) -> bool:
+    """Allocate META parameters/buffers of ``module`` on ``device`` and initialise them.
+
+    ``to_empty`` creates new Parameter objects; an ``optimizer`` built over the meta
+    parameters is re-pointed at them (matched by parameter name)."""
     if not any(t.is_meta for t in list(module.parameters()) + list(module.buffers())):
         return False
+    old = {id(p): n for n, p in module.named_parameters(remove_duplicate=False)}
     module.to_empty(device=device)
     with torch.no_grad():
         for m in module.modules():
@@ -70,6 +74,10 @@ def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None) 
                 init_fn(m)
             elif hasattr(m, "reset_parameters"):
                 m.reset_parameters()
+    if optimizer is not None:
+        new = dict(module.named_parameters(remove_duplicate=False))
+        for g in optimizer.param_groups:
+            g["params"] = [new[old[id(p)]] if id(p) in old else p for p in g["params"]]
     return True
 
 

@@ -330,3 +330,24 @@ def test_miopen_find_db_seeding(tmp_path, monkeypatch):
     assert got == str(tmp_path / "db") and sorted(p.name for p in (tmp_path / "db").iterdir()) == shipped
     monkeypatch.setenv("MIOPEN_USER_DB_PATH", "/somewhere/else")
     assert miopen.setup_find_db() == "/somewhere/else"
+
+
+def test_distribute_meta_model_remaps_optimizer():
+    """A model built on the meta device (with its optimizer) is materialised by distribute(dp)
+    and the optimizer steps the real parameters."""
+    import madnn
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.optim import FusedAdam
+
+    torch.manual_seed(0)
+    with torch.device("meta"):
+        model = GPT2(gpt2_config("gpt2-tiny"))
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    eng, opt = madnn.distribute(model, opt, strategy="dp")
+    assert not any(p.is_meta for g in opt.param_groups for p in g["params"])
+    ids = torch.randint(0, model.config.vocab_size, (2, 16))
+    before = [p.detach().clone() for p in model.parameters()]
+    loss = eng.train_step(ids, ids)
+    opt.step()
+    assert torch.isfinite(loss)
+    assert any(not torch.equal(b, p.detach()) for b, p in zip(before, model.parameters()))
