@@ -1,8 +1,9 @@
 """Shared transformer pieces.
 
-Attention goes through ``F.scaled_dot_product_attention`` (PyTorch-ROCm's
-flash/AOTriton kernels on MI355X); QKV is one fused projection GEMM
-(hipBLASLt); norms are the madnn K3 kernel with the residual add fused in.
+Attention on the GPU is madnn's K8 MFMA flash-attention kernel, reading the packed
+QKV projection in place ([B, S, heads, D], no transposes); elsewhere (CPU, dropout,
+other head dims) ``F.scaled_dot_product_attention``.  QKV is one fused projection
+GEMM (hipBLASLt); norms are the madnn K3 kernel with the residual add fused in.
 
 Every transformer in the zoo exposes ``pipeline_layers()``: a list of modules
 whose sequential composition equals ``forward`` (embedding -> blocks -> head),
@@ -16,6 +17,8 @@ import math
 import torch
 import torch.nn.functional as F
 from torch import nn
+
+from .. import ops
 
 
 def causal_lm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None) -> torch.Tensor:
@@ -48,6 +51,17 @@ class SelfAttention(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         b, s, _ = x.shape
         qkv = self.qkv(x).view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
+        drop = self.dropout if self.training else 0.0
+        if ops.attention_supported(qkv, self.head_dim, drop):
+            # K8 HIP attention on the [B, S, heads, D] layout the projection produced: no
+            # transposes; without RoPE it reads q/k/v and writes dQKV in place
+            if self.rope is None:
+                o = ops.attention_qkvpacked(qkv, self.heads, self.kv_heads, causal=self.causal)
+            else:
+                q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
+                q, k = self.rope(q, k, seq_dim=1)
+                o = ops.attention(q, k, v, causal=self.causal)
+            return self.proj(o.view(b, s, self.heads * self.head_dim))
         q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         if self.rope is not None:
@@ -87,10 +101,13 @@ class RotaryEmbedding(nn.Module):
         x1, x2 = x.chunk(2, dim=-1)
         return torch.cat([-x2, x1], dim=-1)
 
-    def forward(self, q, k):
-        s = q.size(-2)
+    def forward(self, q, k, seq_dim: int = -2):
+        """q/k as [B, heads, S, D] (``seq_dim=-2``) or [B, S, heads, D] (``seq_dim=1``)."""
+        s = q.size(seq_dim)
         cos = self.cos[:s].to(q.dtype)
         sin = self.sin[:s].to(q.dtype)
+        if seq_dim == 1:
+            cos, sin = cos[:, None, :], sin[:, None, :]
         return q * cos + self._rot(q) * sin, k * cos + self._rot(k) * sin
 
 

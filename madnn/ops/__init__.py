@@ -308,13 +308,83 @@ def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, *, shift: bool = 
     return reference.cross_entropy(logits, targets, shift=shift, vocab=v, ignore_index=ignore_index)
 
 
+# ---------------------------------------------------------------------- K8
+class _AttnFn(torch.autograd.Function):
+    """q [B,S,H,D], k/v [B,S,Hkv,D] (strided views) -> o [B,S,H,D] contiguous."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = torch.ops.madnn.attn_fwd(q, k, v, bool(causal), float(scale))
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, ctx.causal, float(ctx.scale))
+        return dq, dk, dv, None, None
+
+
+class _AttnPackedFn(torch.autograd.Function):
+    """qkv [B,S,H+2*Hkv,D] (one projection's output) -> o [B,S,H,D]; dQKV is written in place
+    into one buffer (no split/cat copies in either direction)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads, kv_heads, causal, scale):
+        q, k, v = qkv.split([heads, kv_heads, kv_heads], dim=2)
+        o, lse = torch.ops.madnn.attn_fwd(q, k, v, bool(causal), float(scale))
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.meta = (heads, kv_heads, bool(causal), float(scale))
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        heads, kv_heads, causal, scale = ctx.meta
+        q, k, v = qkv.split([heads, kv_heads, kv_heads], dim=2)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv.split([heads, kv_heads, kv_heads], dim=2)
+        torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale)
+        return dqkv, None, None, None, None
+
+
+def attention_supported(t: torch.Tensor, head_dim: int, dropout: float = 0.0) -> bool:
+    """Inputs the K8 attention kernels take: bf16 HIP tensors, head dim 64/128, no dropout."""
+    return (t.device.type == "cuda" and t.dtype == torch.bfloat16 and head_dim in (64, 128)
+            and dropout == 0.0 and t.stride(-1) == 1)
+
+
+def attention(q, k, v, *, causal: bool = True, scale: Optional[float] = None):
+    """Scaled-dot-product attention on [B, S, heads, D] tensors (GQA when k/v have fewer heads).
+    Returns [B, S, H, D].  HIP bf16 inputs run K8; anything else runs SDPA."""
+    scale = scale if scale is not None else q.size(-1) ** -0.5
+    if attention_supported(q, q.size(-1)):
+        _need_native("attention")
+        return _AttnFn.apply(q, k, v, causal, scale)
+    return reference.attention(q, k, v, causal=causal, scale=scale)
+
+
+def attention_qkvpacked(qkv, heads: int, kv_heads: int, *, causal: bool = True, scale: Optional[float] = None):
+    """Attention straight from a packed projection ``qkv`` [B, S, heads + 2*kv_heads, D]."""
+    d = qkv.size(-1)
+    scale = scale if scale is not None else d ** -0.5
+    if attention_supported(qkv, d) and qkv.is_contiguous():
+        _need_native("attention")
+        return _AttnPackedFn.apply(qkv, heads, kv_heads, causal, scale)
+    q, k, v = qkv.split([heads, kv_heads, kv_heads], dim=2)
+    return reference.attention(q, k, v, causal=causal, scale=scale)
+
+
 def hidden_supported(h: int) -> bool:
     return h % 8 == 0 and h <= 16384
 
 
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
-    "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
+    "max_pool2d", "max_pool_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

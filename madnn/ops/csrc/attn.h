@@ -1,0 +1,34 @@
+// Shared (host <-> device) argument block of the K8 attention kernels.
+#pragma once
+#include <stdint.h>
+
+extern "C" {
+
+// All tensors bf16 except lse/delta (fp32).  q/k/v (and dq/dk/dv) are [B, S, heads, D]
+// views with the last dim contiguous; any batch/seq/head strides (in elements) -- e.g.
+// slices of one packed [B, S, H + 2*Hkv, D] QKV projection.  o/dout are [B, S, H, D]
+// with strides o_*.  lse/delta are [B, H, S] fp32 (lse in log2 units of the scaled score).
+struct MadnnAttnArgs {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  uint16_t* o;
+  float* lse;
+  const uint16_t* dout;
+  uint16_t* dq;
+  uint16_t* dk;
+  uint16_t* dv;
+  float* delta;
+  int64_t q_sb, q_ss, q_sh;
+  int64_t k_sb, k_ss, k_sh;
+  int64_t v_sb, v_ss, v_sh;
+  int64_t o_sb, o_ss, o_sh;
+  int64_t dq_sb, dq_ss, dq_sh;
+  int64_t dk_sb, dk_ss, dk_sh;
+  int64_t dv_sb, dv_ss, dv_sh;
+  int B, S, H, Hkv;
+  float scale;       // softmax scale (1/sqrt(D) by default)
+  float scale_log2;  // scale * log2(e)
+};
+
+}

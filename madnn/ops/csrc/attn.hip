@@ -1,0 +1,591 @@
+// K8: fused (flash-style) multi-head attention forward/backward for gfx950.
+//
+// Replaces PyTorch-ROCm's SDPA kernels for the transformer models (GPT-2, BERT,
+// Llama; SURVEY §7 "MFMA for GEMM-shaped work").  bf16 I/O, fp32 accumulation,
+// head dim 64 or 128, causal or full, grouped-query (Hkv | H), any sequence length.
+// Inputs are strided [B, S, heads, D] views, so the packed QKV projection output is
+// consumed in place and dQKV is written in place: no transposes, no split/cat copies.
+//
+// CDNA4 mapping (cdna_hip_programming.md §3, T2, T10; Appendix B "Fused attention"):
+//  * every product is v_mfma_f32_32x32x16_bf16 on 64-lane waves; a workgroup is
+//    4 waves (one per SIMD);
+//  * "query on the lane" (forward, dQ): S^T = K.Q^T puts one query row per lane
+//    (and its partner lane l^32), so the online-softmax max/sum is lane-local plus
+//    one cross-half exchange, and the S^T accumulator is -- unmoved -- the B
+//    operand of O^T += V^T.P^T / dQ^T += K^T.dS^T (accumulator-as-operand idiom);
+//  * "key on the lane" (dK/dV): S = Q.K^T, dP = dO.V^T give P and dS with the
+//    key on the lane; they are the A operands of dV += P^T.dO and dK += dS^T.Q;
+//  * K/V (or Q/dO) tiles are staged global -> registers -> LDS, double-buffered
+//    with one barrier per tile; the LDS image is XOR-swizzled so that BOTH the
+//    row reads (ds_read_b128, MFMA operand with the head dim as k) and the
+//    transposed reads (ds_read_b64_tr_b16, operand with the sequence as k) are
+//    bank-conflict-free (the swizzle proofs are in the comments of swz());
+//  * the backward is three kernels: delta = rowsum(dO*O); dQ (query blocks);
+//    dK/dV (key blocks, looping over the query heads of a grouped KV head) --
+//    no atomics, deterministic;
+//  * block -> (sequence block, batch*head) mapping is XCD-aware: the workgroups
+//    dispatched to one XCD work on the same heads, so K/V tiles hit in its L2.
+// Reference: the reference has no attention; this serves the
+// transformer configs of BASELINE.json (GPT-2 medium, BERT-large, Llama-3 8B).
+#include "attn.h"
+#include "common.h"
+
+namespace madnn {
+namespace attn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kRowsWG = 128;   // query rows per workgroup (fwd, dQ) / key rows (dK/dV)
+constexpr int kTile = 64;      // keys per tile (fwd, dQ) / queries per tile (dK/dV)
+constexpr float kNegBig = -1.0e30f;
+
+__device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// Byte offset of 16-B chunk `ch` of row `row` in a [64][D] bf16 LDS tile.
+// D = 64 (128-B rows, 2 rows per 256-B bank row): ch ^ f(row), f = ((row>>1)&1)<<2 | (row>>2)&3.
+//   ds_read_b128 groups {0-3,12-15,20-27} / {4-11,16-19,28-31} (row = lane): the 8 even and the 8
+//   odd rows of each group get 8 distinct f -> 16 distinct 16-B slots.  Transposed read (rows
+//   4n..4n+3, an aligned 4-chunk group per 32-lane half): rows 4n, 4n+2 differ in f bit 2, rows
+//   4n+1, 4n+3 sit in the other half of the bank row -> 16 distinct slots.
+// D = 128 (256-B rows): the dual-use image (b) of cdna_hip_programming.md T10.
+template <int D>
+__device__ __forceinline__ int swz(int row, int ch) {
+  if constexpr (D == 64) {
+    return row * 128 + 16 * (ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3)));
+  } else {
+    return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  }
+}
+
+// MFMA operand with the head dim as k: 8 bf16 of row `row`, chunk `ch` (ds_read_b128).
+template <int D>
+__device__ __forceinline__ bf16x8 lds_row(const uint16_t* tile, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(tile) + swz<D>(row, ch));
+}
+
+// MFMA operand with the tile's ROW index as k (two ds_read_b64_tr_b16): element j of lane half h
+// is tile[r0 + 8*(j>>2) + 4h + (j&3)][c0 + (lane&31)] -- the k order in which an f32x16
+// accumulator's registers 8s..8s+7 serve as the other operand (pack_acc).
+template <int D>
+__device__ __forceinline__ bf16x8 lds_tr(const uint16_t* tile, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const int row = r0 + 4 * (g >> 1) + (i >> 2);
+  const char* base = reinterpret_cast<const char*>(tile);
+  const int sub = 8 * ((col >> 2) & 1);
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + swz<D>(row, col >> 3) + sub));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + swz<D>(row + 8, col >> 3) + sub));
+  const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// registers 8s..8s+7 of an accumulator -> bf16 operand fragment (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ bf16x8 pack_acc(const f32x16& x, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(x[8 * s + j]);
+  return r;
+}
+
+// accumulator register r of lane half h -> row within the 32-row block
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// [64][D] tile: global (row stride `ld` elements, rows >= nvalid read as zeros) -> regs -> LDS.
+template <int D>
+struct TileStage {
+  static constexpr int CH = D / 8;
+  static constexpr int PER = kTile * CH / kThreads;
+  u32x4 r[PER];
+  __device__ __forceinline__ void load(const uint16_t* base, int64_t ld, int row0, int nvalid, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + kThreads * i;
+      const int row = c / CH, ch = c % CH;
+      if (row0 + row < nvalid) {
+        r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * ld + ch * 8);
+      } else {
+        r[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* tile, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + kThreads * i;
+      const int row = c / CH, ch = c % CH;
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(tile) + swz<D>(row, ch)) = r[i];
+    }
+  }
+};
+
+// Workgroup -> (sequence block, batch, head): consecutive logical ids on one XCD
+// (bijective remap, cdna_hip_programming.md "XCD swizzle must be bijective").
+__device__ __forceinline__ void map_block(int nblk, int heads, bool heavy_last, int& blk, int& b, int& h) {
+  const int nwg = gridDim.x;
+  const int id = blockIdx.x;
+  const int xcd = id % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + id / 8;
+  const int bh = wg / nblk;
+  blk = wg % nblk;
+  if (heavy_last) blk = nblk - 1 - blk;  // causal: the longest query blocks start first
+  b = bh / heads;
+  h = bh % heads;
+}
+
+__device__ __forceinline__ void store4_bf16(uint16_t* p, float a, float b, float c, float d) {
+  const unsigned lo = (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+  const unsigned hi = (unsigned)f32_to_bf16(c) | ((unsigned)f32_to_bf16(d) << 16);
+  *reinterpret_cast<u32x2*>(p) = u32x2{lo, hi};
+}
+
+// ------------------------------------------------------------------ forward
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs a) {
+  constexpr int DS = D / 16, DB = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[2][kTile * D];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
+  int qblk, b, h;
+  map_block(nqb, a.H, CAUSAL, qblk, b, h);
+  const int hk = h / (a.H / a.Hkv);
+  const int q0w = qblk * kRowsWG + wave * 32;
+  const int qrow = q0w + l32;
+
+  // Q^T as the B operand of S^T = K.Q^T: lane holds Q[qrow][16s + 8hh + j]
+  bf16x8 qf[DS];
+  {
+    const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)min(qrow, a.S - 1) * a.q_ss;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+  }
+  const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
+  f32x16 o[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) o[d] = zero16();
+  float m = kNegBig, l = 0.f;
+  const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
+  const int ntiles = (kv_end + kTile - 1) / kTile;
+
+  TileStage<D> stk, stv;
+  stk.load(kb_, a.k_ss, 0, a.S, tid);
+  stv.load(vb_, a.v_ss, 0, a.S, tid);
+  stk.store(sK[0], tid);
+  stv.store(sV[0], tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stk.load(kb_, a.k_ss, (t + 1) * kTile, a.S, tid);
+      stv.load(vb_, a.v_ss, (t + 1) * kTile, a.S, tid);
+    }
+    const int k0 = t * kTile;
+    if (!CAUSAL || k0 <= q0w + 31) {
+      f32x16 sc[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        sc[kb] = zero16();
+#pragma unroll
+        for (int s = 0; s < DS; ++s) sc[kb] = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
+      }
+      const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
+      float mx = kNegBig;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float x = sc[kb][r] * a.scale_log2;
+          if (edge) {
+            const int key = k0 + kb * 32 + acc_row(r, hh);
+            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+            x = ok ? x : -__builtin_inff();
+          }
+          sc[kb][r] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = exp2f(m - mnew);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = exp2f(sc[kb][r] - mnew);
+          sc[kb][r] = p;
+          rs += p;
+        }
+      }
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      }
+      // O^T[d][q] += sum_key V[key][d] P^T[key][q]
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = pack_acc(sc[kb], s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) o[d] = mfma(lds_tr<D>(sV[cur], kb * 32 + 16 * s, d * 32, lane), pf, o[d]);
+        }
+      }
+    }
+    if (more) {
+      stk.store(sK[cur ^ 1], tid);
+      stv.store(sV[cur ^ 1], tid);
+    }
+    __syncthreads();
+  }
+  const float lt = l + __shfl_xor(l, 32);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < a.S) {
+    uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        store4_bf16(op + d * 32 + 8 * g + 4 * hh, o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv,
+                    o[d][4 * g + 3] * inv);
+      }
+    }
+    if (hh == 0) a.lse[((int64_t)b * a.H + h) * a.S + qrow] = m + log2f(lt);
+  }
+}
+
+// ------------------------------------------------------- backward: delta = rowsum(dO * O)
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const MadnnAttnArgs a) {
+  constexpr int LPR = D / 8;  // lanes per (b, s, h) row
+  const int64_t rows = (int64_t)a.B * a.S * a.H;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid / LPR;
+  const int part = (int)(gid % LPR);
+  float acc = 0.f;
+  int b = 0, s = 0, h = 0;
+  if (row < rows) {
+    h = (int)(row % a.H);
+    s = (int)((row / a.H) % a.S);
+    b = (int)(row / ((int64_t)a.H * a.S));
+    const int64_t off = b * a.o_sb + (int64_t)s * a.o_ss + h * a.o_sh + part * 8;
+    float x[8], y[8];
+    load8<kBF16>(a.dout, off, x);
+    load8<kBF16>(a.o, off, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+  }
+#pragma unroll
+  for (int w = LPR / 2; w > 0; w >>= 1) acc += __shfl_xor(acc, w, LPR);
+  if (row < rows && part == 0) a.delta[((int64_t)b * a.H + h) * a.S + s] = acc;
+}
+
+// ------------------------------------------------------------------ backward: dQ
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
+  constexpr int DS = D / 16, DB = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[2][kTile * D];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
+  int qblk, b, h;
+  map_block(nqb, a.H, CAUSAL, qblk, b, h);
+  const int hk = h / (a.H / a.Hkv);
+  const int q0w = qblk * kRowsWG + wave * 32;
+  const int qrow = q0w + l32;
+  const int qc = min(qrow, a.S - 1);
+  bf16x8 qf[DS], df[DS];
+  {
+    const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)qc * a.q_ss;
+    const uint16_t* dp = a.dout + b * a.o_sb + h * a.o_sh + (int64_t)qc * a.o_ss;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+      df[s] = *reinterpret_cast<const bf16x8*>(dp + 16 * s + 8 * hh);
+    }
+  }
+  const int64_t srow = ((int64_t)b * a.H + h) * a.S + qc;
+  const float lse = a.lse[srow];
+  const float dl = a.delta[srow];
+  const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
+  const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
+  f32x16 dq[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) dq[d] = zero16();
+  const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
+  const int ntiles = (kv_end + kTile - 1) / kTile;
+  TileStage<D> stk, stv;
+  stk.load(kb_, a.k_ss, 0, a.S, tid);
+  stv.load(vb_, a.v_ss, 0, a.S, tid);
+  stk.store(sK[0], tid);
+  stv.store(sV[0], tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < ntiles;
+    if (more) {
+      stk.load(kb_, a.k_ss, (t + 1) * kTile, a.S, tid);
+      stv.load(vb_, a.v_ss, (t + 1) * kTile, a.S, tid);
+    }
+    const int k0 = t * kTile;
+    if (!CAUSAL || k0 <= q0w + 31) {
+      f32x16 sc[2], dp[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        sc[kb] = zero16();
+        dp[kb] = zero16();
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+          sc[kb] = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
+          dp[kb] = mfma(lds_row<D>(sV[cur], kb * 32 + l32, 2 * s + hh), df[s], dp[kb]);
+        }
+      }
+      const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = exp2f(sc[kb][r] * a.scale_log2 - lse);
+          if (edge) {
+            const int key = k0 + kb * 32 + acc_row(r, hh);
+            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+            p = ok ? p : 0.f;
+          }
+          sc[kb][r] = p * (dp[kb][r] - dl);
+        }
+      }
+      // dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 sf = pack_acc(sc[kb], s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) dq[d] = mfma(lds_tr<D>(sK[cur], kb * 32 + 16 * s, d * 32, lane), sf, dq[d]);
+        }
+      }
+    }
+    if (more) {
+      stk.store(sK[cur ^ 1], tid);
+      stv.store(sV[cur ^ 1], tid);
+    }
+    __syncthreads();
+  }
+  if (qrow < a.S) {
+    uint16_t* qp = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow * a.dq_ss;
+    const float sc = a.scale;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        store4_bf16(qp + d * 32 + 8 * g + 4 * hh, dq[d][4 * g] * sc, dq[d][4 * g + 1] * sc, dq[d][4 * g + 2] * sc,
+                    dq[d][4 * g + 3] * sc);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------- backward: dK, dV
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttnArgs a) {
+  constexpr int DS = D / 16, DB = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[2][kTile * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sO[2][kTile * D];  // dO
+  __shared__ float sL[2][kTile], sD[2][kTile];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int nkb = (a.S + kRowsWG - 1) / kRowsWG;
+  int kblk, b, hk;
+  map_block(nkb, a.Hkv, false, kblk, b, hk);  // causal: block 0 (longest) first already
+  const int G = a.H / a.Hkv;
+  const int k0w = kblk * kRowsWG + wave * 32;
+  const int krow = k0w + l32;
+  const int kc = min(krow, a.S - 1);
+  // K^T / V^T as the B operand of S = Q.K^T / dP = dO.V^T: lane holds K[krow][16s + 8hh + j]
+  bf16x8 kf[DS], vf[DS];
+  {
+    const uint16_t* kp = a.k + b * a.k_sb + hk * a.k_sh + (int64_t)kc * a.k_ss;
+    const uint16_t* vp = a.v + b * a.v_sb + hk * a.v_sh + (int64_t)kc * a.v_ss;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const bf16x8*>(vp + 16 * s + 8 * hh);
+    }
+  }
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) {
+    dk[d] = zero16();
+    dv[d] = zero16();
+  }
+  const int t0 = CAUSAL ? (kblk * kRowsWG) / kTile : 0;
+  const int nt = (a.S + kTile - 1) / kTile - t0;
+  const int total = G * nt;
+  auto src = [&](int it, const uint16_t*& qp, const uint16_t*& dp, int& q0, int& hq) {
+    hq = hk * G + it / nt;
+    q0 = (t0 + it % nt) * kTile;
+    qp = a.q + b * a.q_sb + hq * a.q_sh;
+    dp = a.dout + b * a.o_sb + hq * a.o_sh;
+  };
+  auto load_stats = [&](int it, int buf) {
+    const uint16_t *qp, *dp;
+    int q0, hq;
+    src(it, qp, dp, q0, hq);
+    if (tid < kTile) {
+      const int q = q0 + tid;
+      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + q;
+      sL[buf][tid] = q < a.S ? a.lse[sr] : __builtin_inff();
+    } else if (tid < 2 * kTile) {
+      const int q = q0 + tid - kTile;
+      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + q;
+      sD[buf][tid - kTile] = q < a.S ? a.delta[sr] : 0.f;
+    }
+  };
+  TileStage<D> stq, sto;
+  if (total > 0) {
+    const uint16_t *qp, *dp;
+    int q0, hq;
+    src(0, qp, dp, q0, hq);
+    stq.load(qp, a.q_ss, q0, a.S, tid);
+    sto.load(dp, a.o_ss, q0, a.S, tid);
+    stq.store(sQ[0], tid);
+    sto.store(sO[0], tid);
+    load_stats(0, 0);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < total;
+    if (more) {
+      const uint16_t *qp, *dp;
+      int q0n, hqn;
+      src(it + 1, qp, dp, q0n, hqn);
+      stq.load(qp, a.q_ss, q0n, a.S, tid);
+      sto.load(dp, a.o_ss, q0n, a.S, tid);
+    }
+    const int q0 = (t0 + it % nt) * kTile;
+    if (!CAUSAL || q0 + kTile - 1 >= k0w) {
+      f32x16 sc[2], dp[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        sc[qb] = zero16();
+        dp[qb] = zero16();
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+          sc[qb] = mfma(lds_row<D>(sQ[cur], qb * 32 + l32, 2 * s + hh), kf[s], sc[qb]);
+          dp[qb] = mfma(lds_row<D>(sO[cur], qb * 32 + l32, 2 * s + hh), vf[s], dp[qb]);
+        }
+      }
+      const bool edge = CAUSAL && q0 < k0w + 31;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = qb * 32 + acc_row(r, hh);
+          float p = exp2f(sc[qb][r] * a.scale_log2 - sL[cur][qi]);
+          if (edge) p = (krow <= q0 + qi) ? p : 0.f;
+          sc[qb][r] = p;
+          dp[qb][r] = p * (dp[qb][r] - sD[cur][qi]);
+        }
+      }
+      // dV[key][d] += sum_q P[q][key] dO[q][d];  dK[key][d] += sum_q dS[q][key] Q[q][d]
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = pack_acc(sc[qb], s);
+          const bf16x8 sf = pack_acc(dp[qb], s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) {
+            dv[d] = mfma(pf, lds_tr<D>(sO[cur], qb * 32 + 16 * s, d * 32, lane), dv[d]);
+            dk[d] = mfma(sf, lds_tr<D>(sQ[cur], qb * 32 + 16 * s, d * 32, lane), dk[d]);
+          }
+        }
+      }
+    }
+    if (more) {
+      stq.store(sQ[cur ^ 1], tid);
+      sto.store(sO[cur ^ 1], tid);
+      load_stats(it + 1, cur ^ 1);
+    }
+    __syncthreads();
+  }
+  // lane holds dK/dV[key = k0w + acc_row(r, hh)][d = 32*db + l32]
+  uint16_t* kp = a.dk + b * a.dk_sb + hk * a.dk_sh;
+  uint16_t* vp = a.dv + b * a.dv_sb + hk * a.dv_sh;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = k0w + acc_row(r, hh);
+    if (key < a.S) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        kp[(int64_t)key * a.dk_ss + d * 32 + l32] = f32_to_bf16(dk[d][r] * a.scale);
+        vp[(int64_t)key * a.dv_ss + d * 32 + l32] = f32_to_bf16(dv[d][r]);
+      }
+    }
+  }
+}
+
+template <int D, bool CAUSAL>
+hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
+  const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int D, bool CAUSAL>
+hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
+  const int64_t lanes = (int64_t)a.B * a.S * a.H * (D / 8);
+  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((lanes + 255) / 256), dim3(256), 0, st, a);
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int nb = (a.S + kRowsWG - 1) / kRowsWG;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+  MADNN_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace attn
+}  // namespace madnn
+
+using namespace madnn::attn;
+
+extern "C" {
+
+int madnn_attn_supported(int D) { return D == 64 || D == 128; }
+
+hipError_t madnn_attn_fwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t st) {
+  if (a->S <= 0 || a->B <= 0) return hipSuccess;
+  if (D == 64) return causal ? launch_fwd<64, true>(*a, st) : launch_fwd<64, false>(*a, st);
+  if (D == 128) return causal ? launch_fwd<128, true>(*a, st) : launch_fwd<128, false>(*a, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t madnn_attn_bwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t st) {
+  if (a->S <= 0 || a->B <= 0) return hipSuccess;
+  if (D == 64) return causal ? launch_bwd<64, true>(*a, st) : launch_bwd<64, false>(*a, st);
+  if (D == 128) return causal ? launch_bwd<128, true>(*a, st) : launch_bwd<128, false>(*a, st);
+  return hipErrorInvalidValue;
+}
+
+}  // extern "C"

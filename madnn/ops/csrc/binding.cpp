@@ -13,6 +13,8 @@
 
 #include <vector>
 
+#include "attn.h"
+
 extern "C" {
 hipError_t madnn_bucket_pack(void* const*, const int64_t*, const int64_t*, int, void*, int, int, float, hipStream_t);
 hipError_t madnn_bucket_unpack(void* const*, const int64_t*, const int64_t*, int, void*, int, int, float, hipStream_t);
@@ -34,6 +36,9 @@ int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
                         const float*, const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*,
                         hipStream_t);
+int madnn_attn_supported(int);
+hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
+hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
 int madnn_maxpool_supported(int64_t, int, int);
 hipError_t madnn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 hipError_t madnn_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int,
@@ -438,6 +443,81 @@ at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, i
   return dx;
 }
 
+// K8 attention.  q: [B, S, H, D], k/v: [B, S, Hkv, D] bf16 views with a contiguous last dim
+// (any other strides, e.g. slices of one packed QKV projection).
+void attn_check(const at::Tensor& t, const char* name, int64_t D) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "attention: ", name, " must be bf16");
+  TORCH_CHECK(t.dim() == 4 && t.size(3) == D && t.stride(3) == 1, "attention: ", name, " must be [B, S, heads, D]");
+  for (int i = 0; i < 3; ++i) TORCH_CHECK(t.stride(i) % 8 == 0, "attention: ", name, " strides must be multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "attention: ", name, " must be 16-byte aligned");
+}
+
+MadnnAttnArgs attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(madnn_attn_supported((int)D), "attention: head dim must be 64 or 128");
+  attn_check(q, "q", D);
+  attn_check(k, "k", D);
+  attn_check(v, "v", D);
+  TORCH_CHECK(k.sizes() == v.sizes() && k.size(0) == q.size(0) && k.size(1) == q.size(1), "attention: k/v shape");
+  TORCH_CHECK(q.size(2) % k.size(2) == 0, "attention: query heads must be a multiple of kv heads");
+  TORCH_CHECK(q.size(1) < (1ll << 30) && q.size(0) * q.size(2) < (1ll << 30), "attention: problem too large");
+  MadnnAttnArgs a{};
+  a.q = reinterpret_cast<const uint16_t*>(q.data_ptr());
+  a.k = reinterpret_cast<const uint16_t*>(k.data_ptr());
+  a.v = reinterpret_cast<const uint16_t*>(v.data_ptr());
+  a.q_sb = q.stride(0); a.q_ss = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_ss = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_ss = v.stride(1); a.v_sh = v.stride(2);
+  a.B = (int)q.size(0); a.S = (int)q.size(1); a.H = (int)q.size(2); a.Hkv = (int)k.size(2);
+  a.scale = (float)scale;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  return a;
+}
+
+std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                            bool causal, double scale) {
+  MadnnAttnArgs a = attn_args(q, k, v, scale);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  at::Tensor o = at::empty({q.size(0), q.size(1), q.size(2), q.size(3)}, q.options());
+  at::Tensor lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
+  a.lse = lse.data_ptr<float>();
+  a.o_sb = o.stride(0); a.o_ss = o.stride(1); a.o_sh = o.stride(2);
+  check(madnn_attn_fwd(&a, (int)q.size(3), causal ? 1 : 0, cur_stream(q)), "attn_fwd");
+  return {o, lse};
+}
+
+// Writes dq/dk/dv into the given (possibly strided, e.g. one packed dQKV buffer) outputs.
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+              const at::Tensor& o, const at::Tensor& lse, const at::Tensor& dq, const at::Tensor& dk,
+              const at::Tensor& dv, bool causal, double scale) {
+  MadnnAttnArgs a = attn_args(q, k, v, scale);
+  const int64_t D = q.size(3);
+  TORCH_CHECK(o.is_contiguous() && o.sizes() == q.sizes(), "attn_bwd: o must be contiguous [B, S, H, D]");
+  at::Tensor doc = dout.contiguous();
+  TORCH_CHECK(doc.sizes() == o.sizes() && doc.scalar_type() == at::kBFloat16, "attn_bwd: grad shape/dtype");
+  attn_check(dq, "dq", D);
+  attn_check(dk, "dk", D);
+  attn_check(dv, "dv", D);
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "attn_bwd: grad shapes");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == q.size(0) * q.size(1) * q.size(2), "attn_bwd: lse");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  at::Tensor delta = at::empty_like(lse);
+  a.o = reinterpret_cast<uint16_t*>(o.data_ptr());
+  a.lse = lse.data_ptr<float>();
+  a.dout = reinterpret_cast<const uint16_t*>(doc.data_ptr());
+  a.delta = delta.data_ptr<float>();
+  a.o_sb = o.stride(0); a.o_ss = o.stride(1); a.o_sh = o.stride(2);
+  a.dq = reinterpret_cast<uint16_t*>(dq.data_ptr());
+  a.dk = reinterpret_cast<uint16_t*>(dk.data_ptr());
+  a.dv = reinterpret_cast<uint16_t*>(dv.data_ptr());
+  a.dq_sb = dq.stride(0); a.dq_ss = dq.stride(1); a.dq_sh = dq.stride(2);
+  a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dk_sh = dk.stride(2);
+  a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1); a.dv_sh = dv.stride(2);
+  check(madnn_attn_bwd(&a, (int)D, causal ? 1 : 0, cur_stream(q)), "attn_bwd");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
@@ -452,6 +532,10 @@ TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? mask, bool has_res, Tensor? w, Tensor save_mean, Tensor save_invstd, "
       "Tensor scale, Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
+  m.def(
+      "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
+      "Tensor(c!) dv, bool causal, float scale) -> ()");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
@@ -485,5 +569,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
   m.impl("maxpool_fwd", maxpool_fwd);
+  m.impl("attn_fwd", attn_fwd);
+  m.impl("attn_bwd", attn_bwd);
   m.impl("maxpool_bwd", maxpool_bwd);
 }

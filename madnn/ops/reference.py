@@ -141,3 +141,13 @@ def cross_entropy(logits, targets, *, shift=False, vocab=None, ignore_index=-100
     if shift:
         logits, targets = logits[:, :-1], targets[:, 1:]
     return F.cross_entropy(logits[..., :v].reshape(-1, v).float(), targets.reshape(-1), ignore_index=ignore_index)
+
+
+def attention(q, k, v, *, causal=True, scale=None):
+    """[B, S, H, D] / [B, S, Hkv, D] -> [B, S, H, D] via SDPA (fp32 oracle when given fp32)."""
+    import torch.nn.functional as F
+
+    h, hkv = q.size(2), k.size(2)
+    o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
+                                       is_causal=causal, scale=scale, enable_gqa=h != hkv)
+    return o.transpose(1, 2).contiguous()
