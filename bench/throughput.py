@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--meta-init", action="store_true", help="build on the meta device (8B models)")
+    ap.add_argument("--metrics", default=None, help="after timing, run 3 metered steps (JSONL to this path)")
     a = ap.parse_args()
 
     import madnn
@@ -119,12 +120,24 @@ def main():
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t)
+    metered = None
+    if a.metrics:
+        from madnn.utils.metrics import StepMeter
+
+        meter = StepMeter(eng, samples_per_step=a.batch, path=a.metrics)
+        for _ in range(3):
+            meter.start()
+            loss = step()
+            metered = meter.stop(loss)
+        meter.close()
     sps = a.batch * a.steps / dt
     out = {"model": a.model, "n_gpus": world, "global_batch": a.batch, "seq_len": None if image else a.seq,
            "samples_per_s": round(sps, 2), "tokens_per_s": None if image else round(sps * a.seq, 1),
            "ms_per_step": round(dt / a.steps * 1e3, 2), "plan": plan.describe() if plan is not None else "dp",
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2), "dtype": "bf16",
            "data": "synthetic", "loss": float(loss) if loss is not None else None}
+    if metered is not None:
+        out["metrics"] = {k: round(v, 3) if isinstance(v, float) else v for k, v in metered.items()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     madnn.shutdown()

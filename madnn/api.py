@@ -340,7 +340,8 @@ class Trainer:
     def __init__(self, model: nn.Module, criterion: Callable, optimizer=None, *, learning_rate: float = 0.01,
                  learning_rate_decay: float = 0.0, max_iteration: int = 25, shuffle: bool = True,
                  batch_size: int = 32, on_example: Optional[Callable] = None,
-                 on_iteration: Optional[Callable] = None, verbose: bool = True, device=None):
+                 on_iteration: Optional[Callable] = None, verbose: bool = True, device=None,
+                 metrics_path: Optional[str] = None):
         self.model, self.criterion = model, criterion
         self.learning_rate, self.learning_rate_decay = learning_rate, learning_rate_decay
         self.max_iteration, self.shuffle, self.batch_size = max_iteration, shuffle, batch_size
@@ -350,6 +351,12 @@ class Trainer:
             optimizer = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=learning_rate)
         self.optimizer = optimizer
         self.history = []
+        self.meter = None
+        if metrics_path:  # per-step JSONL metrics
+            from .utils.metrics import StepMeter
+
+            self.meter = StepMeter(model if hasattr(model, "comm_metrics") else None,
+                                   samples_per_step=batch_size, path=metrics_path)
 
     def _lr(self, epoch: int) -> float:
         return self.learning_rate / (1.0 + epoch * self.learning_rate_decay)
@@ -368,11 +375,15 @@ class Trainer:
                 x, y = data[idx], targets[idx]
                 if self.device is not None:
                     x, y = x.to(self.device), y.to(self.device)
+                if self.meter is not None:
+                    self.meter.start()
                 self.optimizer.zero_grad(set_to_none=True)
                 out = self.model(x)
                 loss = self.criterion(out, y)
                 loss.backward()
                 self.optimizer.step()
+                if self.meter is not None:
+                    self.meter.stop(loss, epoch=epoch + 1, lr=lr)
                 tot += float(loss.detach()) * len(idx)
                 cnt += len(idx)
                 if self.on_example is not None:

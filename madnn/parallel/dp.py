@@ -91,6 +91,11 @@ class DataParallel(nn.Module):
         self._backwards = 0
         self._hooks = []
         self.stats = {"buckets_launched": 0, "bytes_reduced": 0}
+        # per-step comm observability (HIP events; read one step later, never synchronising):
+        # exposed = compute-stream time from the end of backward to the reduced gradients
+        self._ev = {}
+        self._last_ev = None
+        self._step_bytes = 0
         self.broadcast_state(broadcast_buffers)
         if sync == "grads":
             self._install_hooks()
@@ -136,6 +141,9 @@ class DataParallel(nn.Module):
             ev.record(torch.cuda.current_stream(bk.model.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if "comm_start" not in self._ev:
+                    self._ev["comm_start"] = torch.cuda.Event(enable_timing=True)
+                    self._ev["comm_start"].record(self.comm_stream)
                 for p in bk.params:
                     if p.grad is not None:
                         p.grad.record_stream(self.comm_stream)
@@ -147,10 +155,14 @@ class DataParallel(nn.Module):
         bk.launched = True
         self.stats["buckets_launched"] += 1
         self.stats["bytes_reduced"] += buf.numel() * buf.element_size()
+        self._step_bytes += buf.numel() * buf.element_size()
 
     def _on_backward_end(self):
         self._in_backward = False
         self._backwards += 1
+        if self.is_cuda:
+            self._ev["bwd_end"] = torch.cuda.Event(enable_timing=True)
+            self._ev["bwd_end"].record()
         for bk in self.space.buckets:
             if not bk.launched:
                 if not self.find_unused:
@@ -164,14 +176,27 @@ class DataParallel(nn.Module):
         if not self._needs_finalize:
             return
         cur = torch.cuda.current_stream() if self.is_cuda else None
+        if self.comm_stream is not None:
+            with torch.cuda.stream(self.comm_stream):
+                for bk in self.space.buckets:
+                    if bk.work is not None:
+                        bk.work.wait()  # comm stream waits for the collective
+                        bk.work = None
+                if "comm_start" in self._ev:
+                    self._ev["comm_end"] = torch.cuda.Event(enable_timing=True)
+                    self._ev["comm_end"].record(self.comm_stream)
+            cur.wait_stream(self.comm_stream)
         for bk in self.space.buckets:
             if bk.work is not None:
                 bk.work.wait()
                 bk.work = None
             bk.launched = False
             bk.pending = len(bk.params)
-        if self.comm_stream is not None:
-            cur.wait_stream(self.comm_stream)
+        if self.is_cuda and "bwd_end" in self._ev:
+            self._ev["final"] = torch.cuda.Event(enable_timing=True)
+            self._ev["final"].record(cur)
+        self._last_ev, self._ev = (self._ev, self._step_bytes), {}
+        self._step_bytes = 0
         for bk in self.space.buckets:
             if self.unpack_grads:
                 self.space.unpack_grads_to_params(bk)
@@ -179,6 +204,26 @@ class DataParallel(nn.Module):
                 for p in bk.params:
                     p.grad = None
         self._needs_finalize = False
+
+    def comm_metrics(self) -> dict:
+        """Comm numbers of the last finalized step (blocks on that step's events only):
+        ``comm_exposed_ms`` (compute stream stalled after backward waiting for reduced grads),
+        ``comm_ms`` (first bucket launch -> last reduction done, overlapped with backward),
+        ``allreduce_bytes`` and ``busbw_gbps`` (ring bus bandwidth over ``comm_ms``)."""
+        if self._last_ev is None:
+            return {}
+        ev, nbytes = self._last_ev
+        out = {"allreduce_bytes": nbytes}
+        if "bwd_end" in ev and "final" in ev:
+            ev["final"].synchronize()
+            out["comm_exposed_ms"] = max(ev["bwd_end"].elapsed_time(ev["final"]), 0.0)
+        if "comm_start" in ev and "comm_end" in ev:
+            ev["comm_end"].synchronize()
+            ms = ev["comm_start"].elapsed_time(ev["comm_end"])
+            out["comm_ms"] = ms
+            if ms > 0 and self.world > 1:
+                out["busbw_gbps"] = 2.0 * (self.world - 1) / self.world * nbytes / (ms * 1e-3) / 1e9
+        return out
 
     def after_step(self):
         """Called by the fused optimizer after each step (sync="params" period)."""

@@ -349,6 +349,13 @@ class PipelineEngine:
     def after_step(self):
         self.dp.after_step()
 
+    def comm_metrics(self) -> dict:
+        """DP all-reduce numbers of this stage plus the schedule's analytic bubble fraction
+        ((S-1)/(M+S-1) for GPipe and 1F1B with S stages and M microbatches)."""
+        out = self.dp.comm_metrics()
+        out["bubble_fraction"] = (self.nstages - 1) / (self.M + self.nstages - 1)
+        return out
+
     # ------------------------------------------------------------ inference
     @torch.no_grad()
     def forward_step(self, inputs: torch.Tensor) -> Optional[torch.Tensor]:

@@ -223,3 +223,34 @@ def _w_ws4(rank, world):
 
 def test_dp_parity_ws4():
     run_dist(_w_ws4, 4)
+
+
+def _metrics_worker(rank, world, path):
+    import json
+
+    import madnn
+    from madnn.models import MLP
+    from madnn.optim import FusedSGD
+    from madnn.utils.metrics import StepMeter
+
+    torch.manual_seed(0)
+    model = MLP(16, 32, 4)
+    opt = FusedSGD(model.parameters(), lr=0.1)
+    eng, opt = madnn.distribute(model, opt, strategy="dp")
+    meter = StepMeter(eng, samples_per_step=8 * world, path=path if rank == 0 else None)
+    x, y = torch.randn(8, 16), torch.randint(0, 4, (8,))
+    for _ in range(3):
+        meter.start()
+        loss = torch.nn.functional.cross_entropy(eng(x), y)
+        loss.backward()
+        opt.step()
+        m = meter.stop(loss)
+    meter.close()
+    assert m["allreduce_bytes"] > 0 and m["samples_per_s"] > 0 and m["step"] == 3
+    if rank == 0:
+        rows = [json.loads(l) for l in open(path)]
+        assert len(rows) == 3 and all("loss" in r and "step_ms" in r for r in rows)
+
+
+def test_step_metrics_jsonl(tmp_path):
+    run_dist(_metrics_worker, 2, str(tmp_path / "metrics.jsonl"))
