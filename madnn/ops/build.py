@@ -33,6 +33,9 @@ RUNTIME_SO = HERE / "_madnn_runtime.so"
 ARCH = os.environ.get("MADNN_OFFLOAD_ARCH", "gfx950")
 KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "pool.hip", "attn.hip", "binding.cpp"]
 RUNTIME_SOURCES = ["runtime.cpp"]
+# per-source extra flags: MFMA kernels keep their accumulators in the (unified) VGPR file
+# instead of AGPRs, which removes a v_accvgpr_read/write around every softmax element
+EXTRA_FLAGS = {"attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _hipcc() -> str:
@@ -102,7 +105,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = []
         for s in KERNEL_SOURCES:
-            futs.append(ex.submit(_compile, CSRC / s, BUILD / (s + ".o"), [hipcc], kflags, verbose))
+            futs.append(ex.submit(_compile, CSRC / s, BUILD / (s + ".o"), [hipcc],
+                                  kflags + EXTRA_FLAGS.get(s, []), verbose))
         for s in RUNTIME_SOURCES:
             futs.append(ex.submit(_compile, CSRC / s, BUILD / (s + ".o"), ["g++"], rflags, verbose))
         for f in futs:

@@ -49,6 +49,10 @@ __device__ __forceinline__ f32x16 mfma(const bf16x8& a, const bf16x8& b, const f
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// v_exp_f32 directly (exp2f adds denormal range reduction: 4 more VALU per element; a
+// softmax weight below 2^-126 is 0 either way)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -207,41 +211,48 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
         for (int s = 0; s < DS; ++s) sc[kb] = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
       }
       const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
-      float mx = kNegBig;
+      if (edge) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + acc_row(r, hh);
+            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+            sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
+          }
+        }
+      }
+      // running max in log2 units of the scaled score: max(s) * c, c > 0
+      float mx = sc[0][0];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = sc[kb][r] * a.scale_log2;
-          if (edge) {
-            const int key = k0 + kb * 32 + acc_row(r, hh);
-            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
-            x = ok ? x : -__builtin_inff();
-          }
-          sc[kb][r] = x;
-          mx = fmaxf(mx, x);
-        }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);
+      const float mnew = fmaxf(m, mx * a.scale_log2);
       float rs = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(sc[kb][r] - mnew);
+          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -mnew));
           sc[kb][r] = p;
           rs += p;
         }
       }
-      l = l * alpha + rs;
-      m = mnew;
+      // rescale O only when some row's max moved (exact: alpha == 1 otherwise)
+      if (__any(mnew > m)) {
+        const float alpha = ex2(m - mnew);
+        l *= alpha;
 #pragma unroll
-      for (int d = 0; d < DB; ++d) {
+        for (int d = 0; d < DB; ++d) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        }
       }
+      l += rs;
+      m = mnew;
       // O^T[d][q] += sum_key V[key][d] P^T[key][q]
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(sc[kb][r] * a.scale_log2 - lse);
+          float p = ex2(fmaf(sc[kb][r], a.scale_log2, -lse));
           if (edge) {
             const int key = k0 + kb * 32 + acc_row(r, hh);
             const bool ok = key < a.S && (!CAUSAL || key <= qrow);
@@ -502,7 +513,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qi = qb * 32 + acc_row(r, hh);
-          float p = exp2f(sc[qb][r] * a.scale_log2 - sL[cur][qi]);
+          float p = ex2(fmaf(sc[qb][r], a.scale_log2, -sL[cur][qi]));
           if (edge) p = (krow <= q0 + qi) ? p : 0.f;
           sc[qb][r] = p;
           dp[qb][r] = p * (dp[qb][r] - sD[cur][qi]);
