@@ -2,7 +2,9 @@
 torchvision is not installed.  BASELINE config 2:
 "ResNet-50 auto data-parallel bf16 on 8xMI355X".
 
-Convolutions run on MIOpen through PyTorch-ROCm; the stem max-pool is madnn's
+The bottleneck 1x1 convolutions (stride 1) run on madnn's K9 MFMA GEMM kernels,
+which also compute the following BatchNorm's batch statistics in their epilogue; the
+3x3 / stride-2 / stem convolutions run on MIOpen through PyTorch-ROCm; the stem max-pool is madnn's
 NHWC kernel (K7, byte argmax + gather backward); every
 BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
 end of each block, the residual add folded in: ``relu(bn3(conv3(h)) + idt)`` is
@@ -17,6 +19,7 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
+from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedMaxPool2d
 
@@ -26,7 +29,7 @@ def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
 
 
 def conv1x1(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    return FusedConv2d(cin, cout, 1, stride=stride, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -60,10 +63,17 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), relu=True)
+        if self.downsample is None:
+            # K9: BN statistics from the GEMM epilogue; the identity path's gradient is added
+            # inside conv1's data-grad kernel (no separate residual-gradient add)
+            y, st, idt = self.conv1(x, stats=True, fork=True)
+        else:
+            idt = self.downsample(x)
+            y, st = self.conv1(x, stats=True)
+        out = self.bn1(y, relu=True, stats=st)
         out = self.bn2(self.conv2(out), relu=True)
-        return self.bn3(self.conv3(out), residual=idt, relu=True)   # relu(bn3 + idt): one kernel
+        y, st = self.conv3(out, stats=True)
+        return self.bn3(y, residual=idt, relu=True, stats=st)   # relu(bn3 + idt): one kernel
 
 
 class ResNet(nn.Module):

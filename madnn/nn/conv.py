@@ -1,0 +1,44 @@
+"""Convolution module backed by madnn's gfx950 K9 kernels.
+
+``FusedConv2d`` is a drop-in ``nn.Conv2d`` (same parameters, state dict and
+``isinstance``).  A stride-1, unpadded, ungrouped, bias-free 1x1 convolution of an
+NHWC (channels_last) bf16 HIP tensor runs as three MFMA GEMMs (``madnn.ops.conv1x1``:
+forward, data grad, weight grad) and can hand the following
+:class:`~madnn.nn.FusedBatchNorm2d` its batch statistics, computed in the GEMM
+epilogue, so the BatchNorm skips its statistics pass.  Every other configuration runs
+``nn.Conv2d`` (MIOpen on the GPU).  ``MADNN_CONV1X1=0`` disables the K9 path (A/B runs).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+from torch import nn
+
+from .. import ops
+
+_K9 = os.environ.get("MADNN_CONV1X1", "1") != "0"
+
+
+class FusedConv2d(nn.Conv2d):
+    def _k9(self, x: torch.Tensor) -> bool:
+        return (_K9 and self.kernel_size == (1, 1) and self.stride == (1, 1) and self.dilation == (1, 1)
+                and self.groups == 1 and self.bias is None and self.padding in ((0, 0), "valid")
+                and ops.conv1x1_supported(x, self.weight))
+
+    def forward(self, x: torch.Tensor, stats: bool = False, fork: bool = False):
+        """``conv(x)``.  ``stats=True`` also returns ``partial``, the batch statistics of ``y`` for
+        :class:`~madnn.nn.FusedBatchNorm2d` (None when not computed by the kernel); ``fork=True``
+        also returns ``x`` for use as a residual path -- on the K9 path its gradient is summed
+        inside this convolution's data-grad kernel instead of by a separate add."""
+        if self._k9(x):
+            return ops.conv1x1(x, self.weight, stats=stats, fork=fork)
+        out = [super().forward(x)]
+        if stats:
+            out.append(None)
+        if fork:
+            out.append(x)
+        return out[0] if len(out) == 1 else tuple(out)
+
+    def extra_repr(self):
+        return super().extra_repr() + (", kernel=madnn.K9" if self.kernel_size == (1, 1) else "")

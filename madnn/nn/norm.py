@@ -90,14 +90,17 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     everything else the eager composition.  Same parameters/buffers as
     ``nn.BatchNorm2d`` (state dicts interchange; ``isinstance`` holds)."""
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, relu: bool = False,
+                stats: Optional[torch.Tensor] = None):
+        """``stats``: partial batch statistics of ``x`` from the producing kernel
+        (:class:`~madnn.nn.FusedConv2d` with ``stats=True``), or None."""
         training = self.training or not self.track_running_stats
         return ops.batch_norm_act(x, self.weight, self.bias,
                                   self.running_mean if (not self.training or self.track_running_stats) else None,
                                   self.running_var if (not self.training or self.track_running_stats) else None,
                                   self.num_batches_tracked if (self.training and self.track_running_stats) else None,
                                   training=training, momentum=self.momentum, eps=self.eps, relu=relu,
-                                  residual=residual)
+                                  residual=residual, stats=stats)
 
 
 class FusedMaxPool2d(nn.MaxPool2d):

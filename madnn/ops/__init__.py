@@ -170,10 +170,11 @@ def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = No
 # ---------------------------------------------------------------------- K5
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training, momentum, eps, relu, stats):
         y, mean, invstd, scale, shift, mask = torch.ops.madnn.bn_fwd(x, residual, weight, bias, running_mean,
                                                                       running_var, nbt, bool(training),
-                                                                      float(momentum), float(eps), bool(relu))
+                                                                      float(momentum), float(eps), bool(relu),
+                                                                      stats if training else None)
         # the residual itself is not saved: with ReLU its only backward use (the mask) is the bit mask
         ctx.save_for_backward(x, mask, weight, mean, invstd, scale, shift)
         ctx.relu = relu
@@ -188,7 +189,7 @@ class _BNFn(torch.autograd.Function):
         dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
                                                   mean, invstd, scale, shift, ctx.relu, need_w)
         return (dx, dw if need_w else None, db if need_w else None, dres if ctx.has_res else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def bn_supported(x: torch.Tensor, weight: Optional[torch.Tensor]) -> bool:
@@ -207,12 +208,14 @@ def bn_supported(x: torch.Tensor, weight: Optional[torch.Tensor]) -> bool:
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked=None, *, training: bool,
                    momentum: float = 0.1, eps: float = 1e-5, relu: bool = False,
-                   residual: Optional[torch.Tensor] = None):
+                   residual: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None):
     """act(BN(x) + residual) for NHWC activations in one fused kernel per direction.
 
     Device tensors of a supported layout use the K5 HIP kernels (batch statistics,
     running-stat update and num_batches_tracked increment included); anything else
     (CPU, NCHW, unsupported C, eval-mode backward) uses the eager composition.
+    ``stats``: per-channel partial (sum, sum of squares) of ``x`` already computed by the
+    kernel that produced it (``conv1x1(..., stats=True)``); the statistics pass is skipped.
     """
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (weight is not None and weight.requires_grad)
                                               or (residual is not None and residual.requires_grad))
@@ -222,7 +225,7 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
     if fused:
         _need_native("batch_norm_act")
         return _BNFn.apply(x, weight, bias, residual, running_mean, running_var,
-                           num_batches_tracked if training else None, training, momentum, eps, relu)
+                           num_batches_tracked if training else None, training, momentum, eps, relu, stats)
     return reference.batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_tracked,
                                     training=training, momentum=momentum, eps=eps, relu=relu, residual=residual)
 
@@ -377,6 +380,114 @@ def attention_qkvpacked(qkv, heads: int, kv_heads: int, *, causal: bool = True, 
     return reference.attention(q, k, v, causal=causal, scale=scale)
 
 
+# ---------------------------------------------------------------------- K9
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """[M, C] view of an NHWC (or 2-D) tensor."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.size(1)) if t.dim() == 4 else t
+
+
+def conv1x1_route(cin: int, cout: int) -> tuple:
+    """Which implementation runs each pass of a stride-1 1x1 conv, from the per-shape A/B of
+    ResNet-50's convolutions on MI355X (bench/conv1x1_vs_gemm.py, profiles/r1_k9_conv1x1_ab.json):
+
+    * forward: K9 (+ the BatchNorm statistics in its epilogue) where it is at least as fast as
+      MIOpen once the BN statistics pass it removes is counted -- the HBM-bound shapes
+      (Cin <= 256, or an expanding Cout >= 2 Cin); MIOpen for deep-reduction shapes;
+    * data grad: K9 on the HBM-bound shapes (Cin <= 256 and Cout <= 512), hipBLASLt GEMM on the
+      deep ones; both fuse the residual-gradient add (K9 epilogue / GEMM beta = 1);
+    * weight grad: MIOpen (at the HBM bound on layer1, ahead of K9's split-M atomics elsewhere).
+    """
+    fwd = "k9" if (cin <= 256 or cout >= 2 * cin) else "miopen"
+    dgrad = "k9" if (cin <= 256 and cout <= 512) else "gemm"
+    return fwd, dgrad, "miopen"
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    """Stride-1 1x1 convolution on NHWC bf16 (see :func:`conv1x1_route`).  With ``fork`` the
+    input is also returned (as the block's identity path); its gradient is then accumulated
+    inside the data-grad kernel instead of by a separate autograd add."""
+
+    @staticmethod
+    def forward(ctx, x, w, stats, fork):
+        fwd, dgrad, wgrad = conv1x1_route(x.size(1), w.size(0))
+        if fwd == "k9":
+            y, part = torch.ops.madnn.conv1x1_fwd(x, w, bool(stats))
+        else:
+            y = torch.nn.functional.conv2d(x, w) if x.dim() == 4 else torch.mm(x, w.reshape(w.size(0), -1).t())
+            part = x.new_empty((0, 2, w.size(0)), dtype=torch.float32)
+        ctx.save_for_backward(x, w)
+        ctx.route = (dgrad, wgrad)
+        ctx.mark_non_differentiable(part)
+        if fork:
+            return y, part, x.view_as(x)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart, dfork=None):
+        x, w = ctx.saved_tensors
+        dgrad, _ = ctx.route
+        dy = _nhwc(dy.to(x.dtype))
+        res = _nhwc(dfork.to(x.dtype)) if dfork is not None else None
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if dgrad == "k9":
+                dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res)
+            else:
+                w2 = w.reshape(w.size(0), -1)
+                if res is not None:
+                    dx = torch.empty_like(res)
+                    torch.addmm(_rows(res), _rows(dy), w2, out=_rows(dx))
+                else:
+                    dx = torch.empty_like(x)
+                    torch.mm(_rows(dy), w2, out=_rows(dx))
+        elif res is not None:
+            dx = res
+        if ctx.needs_input_grad[1]:
+            if x.dim() == 4:
+                dw = torch.ops.aten.convolution_backward(dy, x, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0),
+                                                         (1, 1), False, (0, 0), 1, (False, True, False))[1]
+                dw = dw.view(w.shape)
+            else:
+                dw = torch.mm(dy.t(), x).view(w.shape)
+        return dx, dw, None, None
+
+
+def conv1x1_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Inputs the K9 path takes: bf16 HIP tensors, NHWC (or 2-D [M, C]), channels % 64 == 0."""
+    if x.device.type != "cuda" or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.numel() == 0:
+        return False
+    if x.dim() == 4:
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            return False
+    elif x.dim() != 2 or not x.is_contiguous():
+        return False
+    cin, cout = x.size(1), w.size(0)
+    if w.numel() != cin * cout or w.stride(0) != cin or w.stride(1) != 1:
+        return False
+    return cin % 64 == 0 and cout % 64 == 0
+
+
+def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool = False):
+    """Stride-1 1x1 convolution ``x (*) w`` of an NHWC bf16 HIP tensor (K9 / library per pass,
+    :func:`conv1x1_route`).  ``stats``: also return the per-workgroup channel sums / sums of
+    squares of y for :func:`batch_norm_act` (None when the forward did not run on K9).
+    ``fork``: also return an alias of ``x`` to use as the residual path, whose gradient is then
+    added inside this convolution's data-grad kernel."""
+    _need_native("conv1x1")
+    outs = _Conv1x1Fn.apply(x, w, stats, fork)
+    y, part = outs[0], outs[1]
+    ret = [y]
+    if stats:
+        ret.append(part if part.numel() else None)
+    if fork:
+        ret.append(outs[2])
+    return ret[0] if len(ret) == 1 else tuple(ret)
+
+
 def hidden_supported(h: int) -> bool:
     return h % 8 == 0 and h <= 16384
 
@@ -384,7 +495,7 @@ def hidden_supported(h: int) -> bool:
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
-    "max_pool2d", "max_pool_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "conv1x1_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

@@ -35,7 +35,7 @@ int madnn_bn_supported(int);
 int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
                         const float*, const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*,
-                        hipStream_t);
+                        const float*, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
@@ -50,6 +50,11 @@ hipError_t madnn_xent_bwd(const void*, int, const int64_t*, const float*, int64_
 hipError_t madnn_bn_bwd(const void*, const void*, const unsigned char*, int, void*, void*, int64_t, int, int, int,
                         const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
                         float*, hipStream_t);
+int madnn_conv1x1_supported(int64_t, int64_t);
+int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
+hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, hipStream_t);
+hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, hipStream_t);
+hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, hipStream_t);
 }
 
 namespace {
@@ -286,7 +291,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
     const at::Tensor& x, const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& w,
     const c10::optional<at::Tensor>& b, const c10::optional<at::Tensor>& run_mean,
     const c10::optional<at::Tensor>& run_var, const c10::optional<at::Tensor>& nbt, bool training, double momentum,
-    double eps, bool relu) {
+    double eps, bool relu, const c10::optional<at::Tensor>& partial) {
   check_dev(x, "x");
   const int64_t C = x.size(1);
   TORCH_CHECK(madnn_bn_supported((int)C), "bn kernel needs C % 8 == 0 and C <= 2048, got ", C);
@@ -298,7 +303,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
   auto fo = x.options().dtype(at::kFloat);
   at::Tensor save_mean = at::empty({C}, fo), save_invstd = at::empty({C}, fo);
   at::Tensor scale = at::empty({C}, fo), shift = at::empty({C}, fo);
-  at::Tensor ws = at::empty({training ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C : 1}, fo);
+  // statistics produced upstream (K9 conv epilogue): [rows, 2, C] partial sums
+  const bool ext = training && partial.has_value() && partial->defined() && partial->numel() > 0;
+  if (ext) {
+    TORCH_CHECK(partial->scalar_type() == at::kFloat && partial->is_contiguous() && partial->dim() == 3 &&
+                    partial->size(1) == 2 && partial->size(2) == C,
+                "bn: partial statistics must be fp32 [rows, 2, C]");
+  }
+  at::Tensor ws = at::empty({training && !ext ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C : 1}, fo);
   // training with a fused residual + ReLU: 1-bit ReLU mask for the backward passes
   const bool need_mask = training && relu && res.has_value();
   at::Tensor mask = at::empty({need_mask ? x.numel() / 8 : 0}, x.options().dtype(at::kByte));
@@ -312,7 +324,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                      relu ? 1 : 0, training ? 1 : 0, (float)eps, (float)momentum, optf(w), optf(b),
                      training ? optf_mut(run_mean) : const_cast<float*>(optf(run_mean)), optf_mut(run_var),
                      training ? nb : nullptr, save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
-                     scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(x)),
+                     scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(),
+                     ext ? partial->data_ptr<float>() : nullptr, ext ? (int)partial->size(0) : 0, cur_stream(x)),
         "bn_fwd");
   return {y, save_mean, save_invstd, scale, shift, mask};
 }
@@ -353,6 +366,81 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
 }
 
 bool bn_supported(int64_t C) { return madnn_bn_supported((int)C) != 0; }
+
+// ---- K9 NHWC 1x1 convolution (stride 1) on MFMA --------------------------------
+// Activations: 4-D channels_last [N, C, H, W] or 2-D contiguous [M, C], bf16.
+// Weight: [Cout, Cin] or [Cout, Cin, 1, 1] with contiguous rows (either memory format).
+int64_t conv_rows(const at::Tensor& t, int64_t C, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "conv1x1: ", name, " must be bf16");
+  if (t.dim() == 2) {
+    TORCH_CHECK(t.is_contiguous(), "conv1x1: 2-D ", name, " must be contiguous");
+  } else {
+    TORCH_CHECK(t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast), "conv1x1: 4-D ", name,
+                " must be channels_last");
+  }
+  TORCH_CHECK(t.size(1) == C, "conv1x1: ", name, " channel mismatch");
+  return t.numel() / C;
+}
+
+at::Tensor conv_out_like(const at::Tensor& t, int64_t C) {
+  if (t.dim() == 2) return at::empty({t.size(0), C}, t.options());
+  return at::empty({t.size(0), C, t.size(2), t.size(3)}, t.options().memory_format(at::MemoryFormat::ChannelsLast));
+}
+
+void conv_check_w(const at::Tensor& w, int64_t cout, int64_t cin) {
+  check_dev(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16, "conv1x1: weight must be bf16");
+  TORCH_CHECK(w.size(0) == cout && w.numel() == cout * cin, "conv1x1: weight must be [Cout, Cin(, 1, 1)]");
+  TORCH_CHECK(w.stride(0) == cin && w.stride(1) == 1, "conv1x1: weight rows must be contiguous");
+  TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64, got ", cin, " -> ",
+              cout);
+}
+
+// y = conv(x, w); with stats: partial [rows, 2, Cout] per-channel (sum, sum of squares) of y
+std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
+  const int64_t cin = x.size(1), cout = w.size(0);
+  const int64_t M = conv_rows(x, cin, "x");
+  conv_check_w(w, cout, cin);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = conv_out_like(x, cout);
+  const int64_t rows = stats ? madnn_conv1x1_stat_rows(M, cin, cout) : 0;
+  at::Tensor part = at::empty({rows, 2, cout}, x.options().dtype(at::kFloat));
+  check(madnn_conv1x1_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, M, cin,
+                          cout, cur_stream(x)),
+        "conv1x1_fwd");
+  return {y, part};
+}
+
+// dx = dy (*) w^T, plus `res` (a gradient of x's layout accumulated from another path) if given
+at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res) {
+  const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
+  const int64_t M = conv_rows(dy, cout, "dy");
+  conv_check_w(w, cout, cin);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dx = conv_out_like(dy, cin);
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) {
+    TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad: residual layout");
+  }
+  check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
+                            cout, cur_stream(dy)),
+        "conv1x1_dgrad");
+  return dx;
+}
+
+// fp32 [Cout, Cin] weight gradient
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x) {
+  const int64_t cout = dy.size(1), cin = x.size(1);
+  const int64_t M = conv_rows(x, cin, "x");
+  TORCH_CHECK(conv_rows(dy, cout, "dy") == M && dy.dim() == x.dim(), "conv1x1_wgrad: dy / x pixel mismatch");
+  TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor dw = at::zeros({cout, cin}, x.options().dtype(at::kFloat));
+  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, cin, cout, cur_stream(x)),
+        "conv1x1_wgrad");
+  return dw;
+}
 
 // ---- K6 fused softmax cross-entropy ------------------------------------------
 // logits: [N, ld] or [B, S, ld] contiguous; V <= ld valid columns.  shift: causal
@@ -523,8 +611,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
 TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
-      "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor, Tensor, "
-      "Tensor)");
+      "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu, Tensor? partial=None) -> (Tensor, Tensor, "
+      "Tensor, Tensor, Tensor, Tensor)");
   m.def("xent_fwd(Tensor logits, Tensor targets, bool shift, int V, int ignore_index) -> (Tensor, Tensor)");
   m.def(
       "xent_bwd(Tensor logits, Tensor targets, Tensor lse, bool shift, int V, int ignore_index, Tensor gscale) -> "
@@ -536,6 +624,9 @@ TORCH_LIBRARY(madnn, m) {
   m.def(
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
       "Tensor(c!) dv, bool causal, float scale) -> ()");
+  m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
+  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
+  m.def("conv1x1_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
@@ -572,4 +663,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_bwd", attn_bwd);
   m.impl("maxpool_bwd", maxpool_bwd);
+  m.impl("conv1x1_fwd", conv1x1_fwd);
+  m.impl("conv1x1_dgrad", conv1x1_dgrad);
+  m.impl("conv1x1_wgrad", conv1x1_wgrad);
 }

@@ -410,22 +410,31 @@ int madnn_bn_supported(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 :
 int madnn_bn_partial_rows(int64_t M, int C) { return madnn::bn_grid_rows(M, C); }
 
 // Forward. training: compute batch stats (+ running update); else use running stats.
+// ext_partial: [ext_rows][2][C] per-channel (sum, sum of squares) of x already produced by
+// the kernel that wrote x (K9 conv1x1 epilogue); the statistics pass over x is skipped.
 hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, unsigned char* mask, int64_t M, int C, int xdt,
                         int relu, int training, float eps, float momentum, const float* w, const float* b,
                         float* run_mean, float* run_var, int64_t* nbt, float* save_mean, float* save_invstd,
-                        float* scale, float* shift, float* workspace, hipStream_t stream) {
+                        float* scale, float* shift, float* workspace, const float* ext_partial, int ext_rows,
+                        hipStream_t stream) {
   using namespace madnn;
   if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
-  const int G = bn_grid_rows(M, C);
+  int G = bn_grid_rows(M, C);
   const BnGeom g = bn_geom(C);
   const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
   if (training) {
-    MADNN_DISPATCH_DT(xdt, XDT, {
-      hipLaunchKernelGGL((bn_stats_kernel<XDT>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
-    });
-    MADNN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C, M, eps,
+    const float* part = workspace;
+    if (ext_partial != nullptr && ext_rows > 0) {
+      part = ext_partial;
+      G = ext_rows;
+    } else {
+      MADNN_DISPATCH_DT(xdt, XDT, {
+        hipLaunchKernelGGL((bn_stats_kernel<XDT>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
+      });
+      MADNN_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, part, G, C, M, eps,
                        momentum, w, b, save_mean, save_invstd, scale, shift, run_mean, run_var, nbt);
   } else {
     hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, C, eps, w, b, run_mean,

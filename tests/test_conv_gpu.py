@@ -1,0 +1,162 @@
+"""K9: NHWC 1x1 convolution on MFMA vs fp32 PyTorch references of the same op — forward,
+data gradient, weight gradient, the fused BatchNorm statistics, and the ResNet bottleneck
+that uses them."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from madnn import ops
+
+pytestmark = pytest.mark.gpu
+
+# (N, Cin, Cout, H, W): pixel counts that are / are not multiples of the 128-row tile,
+# 64- and 128-wide channel tiles on both sides, deep reductions
+SHAPES = [(2, 64, 256, 7, 7), (3, 128, 64, 5, 9), (2, 256, 128, 14, 14), (1, 512, 2048, 3, 3),
+          (4, 2048, 512, 7, 7), (2, 64, 64, 16, 16), (1, 192, 320, 11, 13)]
+
+
+def _rand(shape, dev, scale=1.0):
+    t = (torch.randn(shape, device=dev) * scale).bfloat16()
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t
+
+
+def _close(a, b, rel):
+    torch.testing.assert_close(a, b, atol=rel * b.abs().max().item() + 1e-6, rtol=rel)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv1x1_three_passes_match_fp32(cuda, shape):
+    n, cin, cout, h, w = shape
+    torch.manual_seed(0)
+    x = _rand((n, cin, h, w), cuda)
+    wt = _rand((cout, cin, 1, 1), cuda, cin ** -0.5).contiguous(memory_format=torch.channels_last)
+    dy = _rand((n, cout, h, w), cuda)
+    assert ops.conv1x1_supported(x, wt)
+    y, part = torch.ops.madnn.conv1x1_fwd(x, wt, True)
+    yr = F.conv2d(x.float(), wt.float())
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y.float(), yr, 2e-2)
+    # fused BN statistics = per-channel sum / sum of squares of the stored bf16 output
+    yf = y.double().permute(0, 2, 3, 1).reshape(-1, cout)
+    assert part.dim() == 3 and part.size(1) == 2 and part.size(2) == cout
+    tol = 1e-5 * yf.abs().sum(0).max().item()
+    torch.testing.assert_close(part[:, 0].double().sum(0), yf.sum(0), atol=tol, rtol=1e-5)
+    torch.testing.assert_close(part[:, 1].double().sum(0), (yf * yf).sum(0), atol=tol, rtol=1e-5)
+    dx = torch.ops.madnn.conv1x1_dgrad(dy, wt)
+    dxr = torch.einsum("nkhw,kc->nchw", dy.float(), wt.float().reshape(cout, cin))
+    assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    _close(dx.float(), dxr, 2e-2)
+    dw = torch.ops.madnn.conv1x1_wgrad(dy, x)
+    dwr = torch.einsum("nkhw,nchw->kc", dy.float(), x.float())
+    _close(dw, dwr, 1e-2)
+
+
+def test_conv1x1_asymmetric_identity(cuda):
+    """A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)."""
+    c = 128
+    x = (torch.arange(64 * c, device=cuda, dtype=torch.float32).reshape(64, c) % 97 - 48).bfloat16()
+    eye = torch.eye(c, device=cuda).bfloat16()
+    y, _ = torch.ops.madnn.conv1x1_fwd(x, eye, False)
+    torch.testing.assert_close(y, x, atol=0, rtol=0)
+    dx = torch.ops.madnn.conv1x1_dgrad(x, eye)
+    torch.testing.assert_close(dx, x, atol=0, rtol=0)
+
+
+def test_fused_conv_module_autograd(cuda):
+    from madnn.nn import FusedConv2d
+
+    torch.manual_seed(1)
+    m = FusedConv2d(128, 256, 1, bias=False).to(cuda)
+    ref = torch.nn.Conv2d(128, 256, 1, bias=False).to(cuda)
+    ref.weight.data.copy_(m.weight.data.bfloat16().float())
+    m = m.bfloat16().to(memory_format=torch.channels_last)
+    x = _rand((4, 128, 9, 9), cuda).requires_grad_(True)
+    xr = x.detach().float().requires_grad_(True)
+    y = m(x)
+    g = torch.randn(y.shape, device=cuda)
+    y.float().backward(g)
+    yr = ref(xr)
+    yr.backward(g)
+    _close(y.float(), yr, 2e-2)
+    _close(x.grad.float(), xr.grad, 3e-2)
+    _close(m.weight.grad.float().reshape(256, 128), ref.weight.grad.reshape(256, 128), 2e-2)
+    # configurations K9 does not take fall back to nn.Conv2d
+    m2 = FusedConv2d(128, 256, 1, stride=2, bias=False).to(cuda).bfloat16().to(memory_format=torch.channels_last)
+    y2, st = m2(x, stats=True)
+    assert st is None and y2.shape == (4, 256, 5, 5)
+
+
+def test_bn_with_conv_statistics_matches_own_pass(cuda):
+    """BatchNorm fed the K9 epilogue statistics == BatchNorm computing them itself."""
+    torch.manual_seed(2)
+    x = _rand((8, 256, 14, 14), cuda)
+    wt = _rand((512, 256, 1, 1), cuda, 256 ** -0.5)
+    y, part = ops.conv1x1(x, wt, stats=True)
+    w, b = torch.rand(512, device=cuda) + 0.5, torch.randn(512, device=cuda)
+    outs = []
+    for st in (part, None):
+        rm, rv = torch.zeros(512, device=cuda), torch.ones(512, device=cuda)
+        outs.append((ops.batch_norm_act(y, w, b, rm, rv, training=True, relu=True, stats=st), rm, rv))
+    (o1, m1, v1), (o2, m2, v2) = outs
+    torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(m1, m2, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(v1, v2, atol=1e-5, rtol=1e-4)
+
+
+def test_bf16_bottleneck_k9_matches_miopen_and_fp32(cuda, monkeypatch):
+    """Bottleneck in bf16 NHWC: K9 convs + fused-statistics BN vs the same bf16 block on MIOpen
+    (same rounding points: tight), and vs fp32 eager on the CPU (loose, in norm)."""
+    import madnn.nn.conv as mconv
+    from madnn.models.resnet import Bottleneck
+
+    torch.manual_seed(3)
+    blk = Bottleneck(256, 64)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    ref = Bottleneck(256, 64)
+    ref.load_state_dict(blk.state_dict())
+    blk = blk.to(cuda).to(memory_format=torch.channels_last)
+    for p in blk.parameters():
+        if p.dim() == 4:
+            p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
+    x0 = _rand((4, 256, 14, 14), cuda)
+    g = torch.randn(4, 256, 14, 14, device=cuda)
+    res = []
+    for k9 in (True, False):
+        monkeypatch.setattr(mconv, "_K9", k9)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        y.float().backward(g)
+        res.append((y.float(), x.grad.float(), blk.conv1.weight.grad.float(), blk.conv3.weight.grad.float()))
+    for a, b in zip(*res):
+        assert ((a - b).norm() / b.norm()).item() < 2e-2
+    xr = x0.float().cpu().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g.cpu())
+    for a, b in zip(res[0], (yr, xr.grad, ref.conv1.weight.grad, ref.conv3.weight.grad)):
+        a = a.cpu().reshape(b.shape)
+        assert ((a - b).norm() / b.norm()).item() < 0.1  # bf16 activations vs fp32: ~7 % on dx
+
+
+@pytest.mark.parametrize("cin,cout", [(256, 64), (1024, 256), (128, 512), (2048, 512)])
+def test_conv1x1_fork_accumulates_residual_grad(cuda, cin, cout):
+    """fork=True: the identity path's gradient is summed inside the data-grad pass (K9 epilogue or
+    hipBLASLt beta=1, per conv1x1_route) -- equal to autograd's separate add."""
+    torch.manual_seed(4)
+    x0 = _rand((2, cin, 7, 9), cuda)
+    wt = _rand((cout, cin, 1, 1), cuda, cin ** -0.5).requires_grad_(True)
+    g1 = torch.randn(2, cout, 7, 9, device=cuda)
+    g2 = torch.randn(2, cin, 7, 9, device=cuda)
+    x = x0.clone().requires_grad_(True)
+    y, st, idt = ops.conv1x1(x, wt, stats=True, fork=True)
+    assert idt.shape == x.shape and torch.equal(idt, x0)
+    ((y.float() * g1).sum() + (idt.float() * g2).sum()).backward()
+    xr = x0.float().requires_grad_(True)
+    wr = wt.detach().float().requires_grad_(True)
+    ((F.conv2d(xr, wr) * g1).sum() + (xr * g2).sum()).backward()
+    _close(x.grad.float(), xr.grad, 3e-2)
+    _close(wt.grad.float(), wr.grad, 3e-2)
+    if ops.conv1x1_route(cin, cout)[0] == "k9":
+        assert st is not None and st.size(2) == cout
