@@ -439,8 +439,10 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 w2 = w.reshape(w.size(0), -1)
                 if res is not None:
-                    dx = torch.empty_like(res)
-                    torch.addmm(_rows(res), _rows(dy), w2, out=_rows(dx))
+                    # beta = 1 GEMM accumulating straight into the identity path's gradient buffer
+                    # (addmm with out= would first copy it); res is this backward's own tensor
+                    dx = res if res._base is None else _nhwc(res.clone())
+                    _rows(dx).addmm_(_rows(dy), w2)
                 else:
                     dx = torch.empty_like(x)
                     torch.mm(_rows(dy), w2, out=_rows(dx))

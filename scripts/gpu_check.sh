@@ -22,7 +22,7 @@ stage() {  # stage <name> <timeout> <cmd...>; pytest exit 1 (test failures) is n
 STAGES=${STAGES:-tests smoke bench prof}
 for s in $STAGES; do
   case $s in
-    tests) stage tests 900 python -m pytest tests -m gpu -q -x ;;
+    tests) stage tests 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ;;
     ktests) stage ktests 600 python -m pytest tests/test_kernels_gpu.py -q ;;
     smoke) stage smoke 400 python __graft_entry__.py smoke ;;
     bench) stage bench 600 python bench.py --steps 30 --warmup 10 ;;
