@@ -392,18 +392,29 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 def conv1x1_route(cin: int, cout: int) -> tuple:
     """Which implementation runs each pass of a stride-1 1x1 conv, from the per-shape A/B of
-    ResNet-50's convolutions on MI355X (bench/conv1x1_vs_gemm.py, profiles/r1_k9_conv1x1_ab.json):
+    ResNet-50's convolutions on MI355X (bench/conv1x1_vs_gemm.py + bench/k9_tune.py,
+    profiles/r1_k9_conv1x1_ab.json):
 
     * forward: K9 (+ the BatchNorm statistics in its epilogue) where it is at least as fast as
       MIOpen once the BN statistics pass it removes is counted -- the HBM-bound shapes
-      (Cin <= 256, or an expanding Cout >= 2 Cin); MIOpen for deep-reduction shapes;
+      (Cin <= 256, or an expanding Cout >= 2 Cin); MIOpen on the deep contracting reductions;
     * data grad: K9 on the HBM-bound shapes (Cin <= 256 and Cout <= 512), hipBLASLt GEMM on the
-      deep ones; both fuse the residual-gradient add (K9 epilogue / GEMM beta = 1);
-    * weight grad: MIOpen (at the HBM bound on layer1, ahead of K9's split-M atomics elsewhere).
+      deep ones; both add the identity path's gradient in the epilogue / with beta = 1;
+    * weight grad: MIOpen.  K9's split-M weight grad is faster per call on every ResNet-50 shape
+      in isolation but not in the full step (its zero-fill + cast launches), so MIOpen stays.
+    Same-box full-step A/B of these choices: docs/PERF.md ("K9 routing").
+    ``MADNN_K9_DGRAD=wide`` / ``MADNN_K9_WGRAD=k9`` select the alternatives.
     """
     fwd = "k9" if (cin <= 256 or cout >= 2 * cin) else "miopen"
-    dgrad = "k9" if (cin <= 256 and cout <= 512) else "gemm"
-    return fwd, dgrad, "miopen"
+    if _K9_DGRAD == "narrow":
+        dgrad = "k9" if (cin <= 256 and cout <= 512) else "gemm"
+    else:
+        dgrad = "gemm" if (cout >= 1024 and cout >= 4 * cin) else "k9"
+    return fwd, dgrad, _K9_WGRAD
+
+
+_K9_WGRAD = os.environ.get("MADNN_K9_WGRAD", "miopen")  # "k9" | "miopen" (A/B runs)
+_K9_DGRAD = os.environ.get("MADNN_K9_DGRAD", "narrow")  # "wide" | "narrow" (A/B runs)
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -429,7 +440,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dpart, dfork=None):
         x, w = ctx.saved_tensors
-        dgrad, _ = ctx.route
+        dgrad, wgrad = ctx.route
         dy = _nhwc(dy.to(x.dtype))
         res = _nhwc(dfork.to(x.dtype)) if dfork is not None else None
         dx = dw = None
@@ -449,7 +460,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         elif res is not None:
             dx = res
         if ctx.needs_input_grad[1]:
-            if x.dim() == 4:
+            if wgrad == "k9":
+                dw = torch.ops.madnn.conv1x1_wgrad(dy, x).to(w.dtype).view(w.shape)
+            elif x.dim() == 4:
                 dw = torch.ops.aten.convolution_backward(dy, x, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0),
                                                          (1, 1), False, (0, 0), 1, (False, True, False))[1]
                 dw = dw.view(w.shape)

@@ -45,6 +45,17 @@ constexpr int kThreads = 256;
 constexpr int kBK = 64;                // reduction depth of one pipeline step
 constexpr int kTargetWG = 2 * kNumCU;  // resident workgroups: 2 per CU
 
+// run-time tunables (bench/conv1x1_vs_gemm.py sweeps them through madnn_conv1x1_tune)
+struct Tune {
+  int fwd_wg = kTargetWG;  // forward / dgrad persistent grid target
+  int wgrad_wg = 2 * kNumCU;  // weight-grad workgroups (tiles x m splits)
+  int xcd = 1;             // XCD-aware workgroup remap
+};
+inline Tune& tune() {
+  static Tune t;
+  return t;
+}
+
 enum Mode : int { kStoreT = 0, kAtomic = 1 };
 
 struct GemmArgs {
@@ -56,6 +67,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldo;
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
+  int xcd;  // 1: remap workgroup ids so consecutive logical ids share an XCD (and its L2)
 };
 
 // One operand's 64-deep slice, register-staged: R rows of "row" memory ([x][ld], k
@@ -125,8 +137,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * SE];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
   const int wi = wave / WJ, wj = wave % WJ;
-  const int it = blockIdx.x % p.i_tiles;
-  const int grp = blockIdx.x / p.i_tiles;
+  // logical id: consecutive ids share the B (j) panel.  The dispatcher deals ids round-robin
+  // over the 8 XCDs; the bijective remap of cdna_hip_programming.md T1 gives each XCD a
+  // contiguous range of logical ids so the shared panels hit in that XCD's L2.
+  int wid = blockIdx.x;
+  if (p.xcd) {
+    const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
+    wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
+  }
+  const int it = wid % p.i_tiles;
+  const int grp = wid / p.i_tiles;
   const int64_t i0 = (int64_t)it * BI;
   const int nk = (int)((p.K + kBK - 1) / kBK);
   int jt, kbeg, kend, jstride;
@@ -299,23 +319,17 @@ hipError_t launch(const GemmArgs& p, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
-// forward / dgrad: i tiles x j groups, each workgroup walking an equal share of the j tiles
-inline void plan_persistent(GemmArgs& p, int64_t J, int BI, int64_t I) {
+// forward / dgrad: i tiles x j groups, each workgroup walking an equal share of the j tiles.
+// Shallow reductions (K < 512: one tile is a few k steps, HBM-bound) stay persistent so the next
+// tile's loads overlap this tile's epilogue; deep ones get one tile per workgroup (measured
+// faster: bench/k9_tune.py, profiles/r1_k9_tune.json).
+inline void plan_persistent(GemmArgs& p, int64_t J, int BI, int64_t I, int64_t K) {
   p.i_tiles = (int)(I / BI);
   p.j_tiles = (int)((J + 127) / 128);
   const int64_t total = (int64_t)p.i_tiles * p.j_tiles;
-  const int64_t per = (total + kTargetWG - 1) / kTargetWG;
+  const int64_t per = K >= 8 * kBK ? 1 : (total + tune().fwd_wg - 1) / tune().fwd_wg;
   p.j_groups = (int)((p.j_tiles + per - 1) / per);
   p.k_chunk = 0;
-}
-
-inline int wgrad_target_wg() {
-  static int v = [] {
-    const char* e = getenv("MADNN_K9_WGRAD_WG");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : kNumCU;
-  }();
-  return v;
 }
 
 }  // namespace conv
@@ -325,6 +339,15 @@ using namespace madnn::conv;
 
 extern "C" {
 
+// key 0: forward/dgrad grid target, 1: weight-grad workgroups, 2: XCD remap (0/1); returns the old value
+int madnn_conv1x1_tune(int key, int value) {
+  int* f = key == 0 ? &tune().fwd_wg : key == 1 ? &tune().wgrad_wg : key == 2 ? &tune().xcd : nullptr;
+  if (f == nullptr) return -1;
+  const int old = *f;
+  if (value >= 0) *f = value;
+  return old;
+}
+
 int madnn_conv1x1_supported(int64_t cin, int64_t cout) {
   return (cin % 64 == 0 && cout % 64 == 0 && cin >= 64 && cout >= 64 && cin <= 16384 && cout <= 16384) ? 1 : 0;
 }
@@ -333,7 +356,7 @@ int madnn_conv1x1_supported(int64_t cin, int64_t cout) {
 int madnn_conv1x1_stat_rows(int64_t M, int64_t cin, int64_t cout) {
   if (!madnn_conv1x1_supported(cin, cout) || M <= 0) return 0;
   GemmArgs p{};
-  plan_persistent(p, M, cout % 128 == 0 ? 128 : 64, cout);
+  plan_persistent(p, M, cout % 128 == 0 ? 128 : 64, cout, cin);
   return p.j_groups;
 }
 
@@ -349,11 +372,12 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
   p.out = y;
   p.ldo = cout;
   p.stats = stats;
+  p.xcd = tune().xcd;
   p.I = cout;
   p.J = M;
   p.K = cin;
   const bool wide = cout % 128 == 0;
-  plan_persistent(p, M, wide ? 128 : 64, cout);
+  plan_persistent(p, M, wide ? 128 : 64, cout, cin);
   const int grid = p.i_tiles * p.j_groups;
   if (wide) {
     return stats ? launch<false, false, 128, 128, kStoreT, true>(p, grid, s)
@@ -375,12 +399,13 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   p.ldb = cout;
   p.out = dx;
   p.res = static_cast<const uint16_t*>(res);
+  p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cin;
   p.J = M;
   p.K = cout;
   const bool wide = cin % 128 == 0;
-  plan_persistent(p, M, wide ? 128 : 64, cin);
+  plan_persistent(p, M, wide ? 128 : 64, cin, cout);
   const int grid = p.i_tiles * p.j_groups;
   return wide ? launch<true, false, 128, 128, kStoreT, false>(p, grid, s)
               : launch<true, false, 64, 128, kStoreT, false>(p, grid, s);
@@ -397,6 +422,7 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t
   p.b = static_cast<const uint16_t*>(x);  // B[k = m][j = ci] = X[m][ci]: column memory
   p.ldb = cin;
   p.out = dw;
+  p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cout;
   p.J = cin;
@@ -406,7 +432,7 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t
   p.j_tiles = (int)(cin / bj);
   const int64_t nk = (M + kBK - 1) / kBK;
   const int64_t tiles = (int64_t)p.i_tiles * p.j_tiles;
-  int64_t splits = (wgrad_target_wg() + tiles - 1) / tiles;
+  int64_t splits = (tune().wgrad_wg + tiles - 1) / tiles;
   splits = splits < 1 ? 1 : (splits > nk ? nk : splits);
   p.k_chunk = (int)((nk + splits - 1) / splits);
   splits = (nk + p.k_chunk - 1) / p.k_chunk;
