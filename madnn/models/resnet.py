@@ -4,7 +4,8 @@ torchvision is not installed.  BASELINE config 2:
 
 The bottleneck 1x1 convolutions (stride 1) run on madnn's K9 MFMA GEMM kernels,
 which also compute the following BatchNorm's batch statistics in their epilogue; the
-3x3 / stride-2 / stem convolutions run on MIOpen through PyTorch-ROCm; the stem max-pool is madnn's
+3x3 / stride-2 convolutions run on MIOpen through PyTorch-ROCm; the 7x7 stem runs on K10 (MFMA
+forward with the BatchNorm statistics in its epilogue, MFMA weight gradient); the stem max-pool is madnn's
 NHWC kernel (K7, byte argmax + gather backward); every
 BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
 end of each block, the residual add folded in: ``relu(bn3(conv3(h)) + idt)`` is
@@ -81,7 +82,7 @@ class ResNet(nn.Module):
                  zero_init_residual: bool = True, width: int = 64):
         super().__init__()
         self.inplanes = width
-        self.conv1 = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        self.conv1 = FusedConv2d(3, width, 7, stride=2, padding=3, bias=False)   # K10 stem
         self.bn1 = BN(width)
         self.maxpool = FusedMaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, width, layers[0])
@@ -114,7 +115,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x), relu=True))
+        y, st = self.conv1(x, stats=True)
+        x = self.maxpool(self.bn1(y, relu=True, stats=st))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

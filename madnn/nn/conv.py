@@ -6,7 +6,9 @@ NHWC (channels_last) bf16 HIP tensor runs as three MFMA GEMMs (``madnn.ops.conv1
 forward, data grad, weight grad) and can hand the following
 :class:`~madnn.nn.FusedBatchNorm2d` its batch statistics, computed in the GEMM
 epilogue, so the BatchNorm skips its statistics pass.  Every other configuration runs
-``nn.Conv2d`` (MIOpen on the GPU).  ``MADNN_CONV1X1=0`` disables the K9 path (A/B runs).
+``nn.Conv2d`` (MIOpen on the GPU), except the ResNet stem (7x7, stride 2, pad 3, 3 -> 64
+channels), which runs on K10 (``madnn.ops.stem_conv``, also with the BatchNorm statistics).
+``MADNN_CONV1X1=0`` / ``MADNN_STEM=0`` disable the K9 / K10 paths (A/B runs).
 """
 from __future__ import annotations
 
@@ -26,6 +28,11 @@ class FusedConv2d(nn.Conv2d):
                 and self.groups == 1 and self.bias is None and self.padding in ((0, 0), "valid")
                 and ops.conv1x1_supported(x, self.weight))
 
+    def _k10(self, x: torch.Tensor) -> bool:
+        return (self.kernel_size == (7, 7) and self.stride == (2, 2) and self.padding == (3, 3)
+                and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
+                and ops.stem_supported(x, self.weight))
+
     def forward(self, x: torch.Tensor, stats: bool = False, fork: bool = False):
         """``conv(x)``.  ``stats=True`` also returns ``partial``, the batch statistics of ``y`` for
         :class:`~madnn.nn.FusedBatchNorm2d` (None when not computed by the kernel); ``fork=True``
@@ -33,6 +40,8 @@ class FusedConv2d(nn.Conv2d):
         inside this convolution's data-grad kernel instead of by a separate add."""
         if self._k9(x):
             return ops.conv1x1(x, self.weight, stats=stats, fork=fork)
+        if not fork and self._k10(x):
+            return ops.stem_conv(x, self.weight, stats=stats)
         out = [super().forward(x)]
         if stats:
             out.append(None)
@@ -41,4 +50,5 @@ class FusedConv2d(nn.Conv2d):
         return out[0] if len(out) == 1 else tuple(out)
 
     def extra_repr(self):
-        return super().extra_repr() + (", kernel=madnn.K9" if self.kernel_size == (1, 1) else "")
+        k = {(1, 1): ", kernel=madnn.K9", (7, 7): ", kernel=madnn.K10"}.get(self.kernel_size, "")
+        return super().extra_repr() + k

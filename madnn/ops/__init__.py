@@ -503,6 +503,66 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
     return ret[0] if len(ret) == 1 else tuple(ret)
 
 
+# ---------------------------------------------------------------------- K10
+_K10 = os.environ.get("MADNN_STEM", "1") != "0"
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Inputs the K10 stem kernels take: NHWC bf16 HIP image [N, 3, H, W] (W % 8 == 0, W <= 250),
+    bf16 weight [64, 3, 7, 7]."""
+    if not _K10 or x.device.type != "cuda" or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if x.dim() != 4 or x.size(1) != 3 or tuple(w.shape) != (64, 3, 7, 7) or x.numel() == 0:
+        return False
+    H, W = x.size(2), x.size(3)
+    return (x.is_contiguous(memory_format=torch.channels_last) and H >= 7 and W >= 8 and W % 8 == 0
+            and (W - 1) // 2 + 1 <= 128 and 7 * (3 * W // 8) <= 1024)
+
+
+def _stem_pack(w: torch.Tensor) -> torch.Tensor:
+    """[64, 3, 7, 7] -> [64, 7 (kh), 8 (kw), 4 (c)] bf16, zero at kw = 7 and c = 3."""
+    wp = w.new_zeros((64, 7, 8, 4))
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    return wp
+
+
+class _StemFn(torch.autograd.Function):
+    """ResNet stem, 7x7 / stride 2 / pad 3, 3 -> 64 channels (K10): MFMA implicit GEMM forward
+    with the BatchNorm statistics in its epilogue; MFMA weight gradient reading the im2col
+    fragments straight from LDS-staged input rows.  The input gradient (never needed for an
+    image batch) goes to MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, stats):
+        y, part = torch.ops.madnn.stem_fwd(x, _stem_pack(w), bool(stats))
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        dy = _nhwc(dy.to(x.dtype))
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, (2, 2), (3, 3), (1, 1), False, (0, 0), 1,
+                                                     (True, False, False))[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.madnn.stem_wgrad(dy, x).to(w.dtype)
+            if not dw.is_contiguous(memory_format=torch.contiguous_format) or w.stride() != dw.stride():
+                dw = torch.empty_like(w).copy_(dw)
+        return dx, dw, None
+
+
+def stem_conv(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False):
+    """``conv2d(x, w, stride=2, padding=3)`` for the ResNet stem on K10 (see
+    :func:`stem_supported`).  ``stats``: also return the per-workgroup channel (sum, sum of
+    squares) partials of y for :func:`batch_norm_act`."""
+    _need_native("stem_conv")
+    y, part = _StemFn.apply(x, w, stats)
+    return (y, part) if stats else y
+
+
 def hidden_supported(h: int) -> bool:
     return h % 8 == 0 and h <= 16384
 
@@ -510,7 +570,7 @@ def hidden_supported(h: int) -> bool:
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
-    "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "conv1x1_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

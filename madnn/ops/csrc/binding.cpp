@@ -55,6 +55,11 @@ int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, hipStream_t);
 hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, hipStream_t);
+int madnn_stem_supported(int, int);
+int madnn_stem_stat_rows(int, int, int);
+hipError_t madnn_stem_fwd(const void*, const void*, void*, float*, int, int, int, hipStream_t);
+int64_t madnn_stem_wgrad_ws(int, int, int);
+hipError_t madnn_stem_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
 }
 
 namespace {
@@ -442,6 +447,51 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x) {
   return dw;
 }
 
+// ---- K10 ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 ---------
+void stem_check_x(const at::Tensor& x) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3, "stem: x must be bf16 [N, 3, H, W]");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "stem: x must be channels_last");
+  TORCH_CHECK(madnn_stem_supported((int)x.size(2), (int)x.size(3)), "stem: unsupported image size ", x.size(2), "x",
+              x.size(3));
+}
+
+// y = conv7x7s2(x, w) with w packed [64][7][8][4]; stats: partial [rows, 2, 64] (sum, sum sq) of y
+std::tuple<at::Tensor, at::Tensor> stem_fwd(const at::Tensor& x, const at::Tensor& wp, bool stats) {
+  stem_check_x(x);
+  check_dev(wp, "wp");
+  TORCH_CHECK(wp.scalar_type() == at::kBFloat16 && wp.is_contiguous() && wp.numel() == 64 * 224,
+              "stem: packed weight must be contiguous bf16 [64, 7, 8, 4]");
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({N, 64, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t rows = stats ? madnn_stem_stat_rows(N, H, W) : 0;
+  at::Tensor part = at::empty({rows, 2, 64}, x.options().dtype(at::kFloat));
+  check(madnn_stem_fwd(x.data_ptr(), wp.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, N, H, W,
+                       cur_stream(x)),
+        "stem_fwd");
+  return {y, part};
+}
+
+// fp32 [64, 3, 7, 7] weight gradient
+at::Tensor stem_wgrad(const at::Tensor& dy, const at::Tensor& x) {
+  stem_check_x(x);
+  check_dev(dy, "dy");
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 &&
+                  dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1,
+              "stem_wgrad: dy must be bf16 [N, 64, Ho, Wo]");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_wgrad: dy must be channels_last");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor ws = at::empty({madnn_stem_wgrad_ws(N, H, W)}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({64, 3, 7, 7}, x.options().dtype(at::kFloat));
+  check(madnn_stem_wgrad(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(), dw.data_ptr<float>(), N, H, W,
+                         cur_stream(x)),
+        "stem_wgrad");
+  return dw;
+}
+
 // ---- K6 fused softmax cross-entropy ------------------------------------------
 // logits: [N, ld] or [B, S, ld] contiguous; V <= ld valid columns.  shift: causal
 // LM (logit row (b, s) predicts target (b, s+1); the last position has no loss).
@@ -627,6 +677,8 @@ TORCH_LIBRARY(madnn, m) {
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
   m.def("conv1x1_wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
+  m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
@@ -666,4 +718,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("conv1x1_fwd", conv1x1_fwd);
   m.impl("conv1x1_dgrad", conv1x1_dgrad);
   m.impl("conv1x1_wgrad", conv1x1_wgrad);
+  m.impl("stem_fwd", stem_fwd);
+  m.impl("stem_wgrad", stem_wgrad);
 }
