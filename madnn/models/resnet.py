@@ -15,6 +15,7 @@ convolutions prefer.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type
 
 import torch
@@ -23,6 +24,9 @@ from torch import nn
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedMaxPool2d
+
+# A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
+_FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -68,6 +72,10 @@ class Bottleneck(nn.Module):
             # K9: BN statistics from the GEMM epilogue; the identity path's gradient is added
             # inside conv1's data-grad kernel (no separate residual-gradient add)
             y, st, idt = self.conv1(x, stats=True, fork=True)
+        elif _FORK_DS:
+            # the downsample path's input gradient is likewise summed inside conv1's data grad
+            y, st, xf = self.conv1(x, stats=True, fork=True)
+            idt = self.downsample(xf)
         else:
             idt = self.downsample(x)
             y, st = self.conv1(x, stats=True)

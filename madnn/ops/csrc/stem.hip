@@ -347,20 +347,30 @@ __global__ __launch_bounds__(kThreads, 2) void stem_wgrad_kernel(const StemWArgs
   }
 }
 
-// dw[i] = sum_g ws[g][i], i < 64 * 147
+// dw[i] = sum_g ws[g][i], i < 64 * 147: a block sums 32 columns, its 8 waves-worth of lane groups
+// each a strided eighth of the partials (8 independent loads in flight per lane), then LDS combine
 __global__ __launch_bounds__(256) void stem_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw, int parts) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= kCo * 147) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int g = 0;
-  for (; g + 4 <= parts; g += 4) {
-    s0 += ws[(int64_t)g * kCo * 147 + i];
-    s1 += ws[(int64_t)(g + 1) * kCo * 147 + i];
-    s2 += ws[(int64_t)(g + 2) * kCo * 147 + i];
-    s3 += ws[(int64_t)(g + 3) * kCo * 147 + i];
+  __shared__ float red[8][32];
+  const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + col;
+  const int64_t stride = (int64_t)kCo * 147;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < kCo * 147) {
+    int g = grp;
+    for (; g + 56 < parts; g += 64) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += ws[(int64_t)(g + 8 * u) * stride + i];
+    }
+    for (; g < parts; g += 8) s[0] += ws[(int64_t)g * stride + i];
   }
-  for (; g < parts; ++g) s0 += ws[(int64_t)g * kCo * 147 + i];
-  dw[i] = (s0 + s1) + (s2 + s3);
+  red[grp][col] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (grp == 0 && i < kCo * 147) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][col];
+    dw[i] = t;
+  }
 }
 
 inline int wgrad_grid(int rows) { return rows < 2 * kNumCU ? rows : 2 * kNumCU; }
@@ -436,7 +446,7 @@ hipError_t madnn_stem_wgrad(const void* x, const void* dy, float* ws, float* dw,
   const size_t lds = (size_t)(9 * (2 * WOP + 6) * 4 + WOP * kCo) * sizeof(uint16_t);
   hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kThreads), lds, s, a);
   MADNN_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(stem_wgrad_reduce, dim3((kCo * 147 + 255) / 256), dim3(256), 0, s, ws, dw, grid);
+  hipLaunchKernelGGL(stem_wgrad_reduce, dim3((kCo * 147 + 31) / 32), dim3(256), 0, s, ws, dw, grid);
   return hipGetLastError();
 }
 
