@@ -1,0 +1,47 @@
+"""Model-level GPU checks for the transformer zoo on the HIP kernels (K3 norms, K6 cross-entropy,
+K8 attention): causal models must not see the future, and the fused shifted LM loss must equal
+the plain shifted cross-entropy of the same logits."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _models():
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.models.llama import Llama, llama_config
+
+    return {
+        # head dim 64 so K8 attention runs (RoPE + grouped-query heads for Llama)
+        "gpt2": lambda: GPT2(gpt2_config("gpt2-tiny", n_embd=256, n_head=4, n_layer=2, dropout=0.0)),
+        "llama": lambda: Llama(llama_config("llama3-tiny", hidden=256, heads=4, kv_heads=2, intermediate=512,
+                                            layers=2)),
+    }
+
+
+@pytest.mark.parametrize("name", ["gpt2", "llama"])
+def test_causal_lm_does_not_see_the_future(cuda, name):
+    torch.manual_seed(0)
+    model = _models()[name]().to(cuda).bfloat16().eval()
+    vocab = model.config.vocab_size
+    ids = torch.randint(0, vocab, (2, 96), device=cuda)
+    t = 70
+    ids2 = ids.clone()
+    ids2[:, t:] = (ids2[:, t:] + 1 + torch.randint(0, vocab - 1, ids2[:, t:].shape, device=cuda)) % vocab
+    with torch.no_grad():
+        a, b = model(ids).float(), model(ids2).float()
+    torch.testing.assert_close(a[:, :t], b[:, :t], atol=1e-3, rtol=0)
+    assert (a[:, t:] - b[:, t:]).abs().max().item() > 1e-2
+
+
+@pytest.mark.parametrize("name", ["gpt2", "llama"])
+def test_fused_lm_loss_is_shifted_cross_entropy(cuda, name):
+    torch.manual_seed(1)
+    model = _models()[name]().to(cuda).bfloat16()
+    vocab = model.config.vocab_size
+    ids = torch.randint(0, vocab, (2, 64), device=cuda)
+    logits = model(ids)
+    loss = model.loss_fn(logits, ids)
+    ref = F.cross_entropy(logits[:, :-1, :vocab].float().reshape(-1, vocab), ids[:, 1:].reshape(-1))
+    torch.testing.assert_close(loss.detach().float(), ref.detach(), atol=2e-3, rtol=2e-3)
