@@ -31,6 +31,49 @@ struct BnGeom {
   int tpr, rpi;
 };
 
+// Run-time tunables of the two elementwise apply passes (bench/bn_order_ab.py sweeps them
+// through madnn_bn_tune).
+//  reverse: walk the tensor from its far end.  The pass before an apply (statistics /
+//    backward reduction, or the conv that produced x) streams the same tensors front to back,
+//    so its last ~100-250 MB are still in the 256 MiB Infinity Cache: a back-to-front apply
+//    reads those first instead of evicting them on the way (MI355X_MICROARCH.md "Infinity
+//    Cache"); the consumer of the apply's output (the next conv) then starts on lines the
+//    apply wrote last.
+//  wg_per_cu: grid = wg_per_cu x 256 CUs workgroups of 256 lanes.  At <= 8 (32 waves per CU)
+//    every workgroup is resident at once, so the whole grid walks the tensor as one front;
+//    above 8 the later workgroups only start when the first ones finish, which splits each
+//    pass into several interleaved sweeps and spoils the reuse order.
+struct BnTune {
+  int reverse = 1;
+  int wg_per_cu = 8;
+};
+inline BnTune& bn_tune() {
+  static BnTune t;
+  return t;
+}
+
+// grid-stride walk of [0, total) in 8-element lane chunks, forward or back-to-front; c0 tracks
+// the channel of the chunk without a 64-bit modulo per step
+struct StripeWalk {
+  int64_t i, di, n;
+  int c0, dc, C;
+  __device__ StripeWalk(int64_t total, int C_, bool reverse) : C(C_) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+    const int sC = (int)(stride % C);
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+    n = i0 < total ? (total - 1 - i0) / stride + 1 : 0;
+    i = reverse && n > 0 ? i0 + (n - 1) * stride : i0;
+    di = reverse ? -stride : stride;
+    c0 = (int)(i % C);
+    dc = reverse ? C - sC : sC;
+  }
+  __device__ void next() {
+    --n;
+    i += di;
+    c0 = (c0 + dc >= C) ? c0 + dc - C : c0 + dc;
+  }
+};
+
 __host__ __device__ inline BnGeom bn_geom(int C) {
   BnGeom g;
   g.tpr = C / 8;
@@ -180,12 +223,11 @@ template <int XDT, bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, void* __restrict__ y,
-                                                       unsigned char* __restrict__ mask, int64_t total, int C) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-  const int sC = (int)(stride % C);  // channel advance per grid-stride step (no 64-bit modulo in the loop)
-  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  int c0 = (int)(i % C);
-  for (; i < total; i += stride, c0 = (c0 + sC >= C) ? c0 + sC - C : c0 + sC) {
+                                                       unsigned char* __restrict__ mask, int64_t total, int C,
+                                                       int reverse) {
+  for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
+    const int64_t i = w.i;
+    const int c0 = w.c0;
     float v[8], sc[8], sh[8];
     load8<XDT>(x, i, v);
     load8<kF32>(scale, c0, sc);
@@ -355,12 +397,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const unsigned char* __restrict__ mask,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ ca,
     const float* __restrict__ cb, const float* __restrict__ cc, void* __restrict__ dx, void* __restrict__ dres,
-    int64_t total, int C) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
-  const int sC = (int)(stride % C);
-  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  int c0 = (int)(i % C);
-  for (; i < total; i += stride, c0 = (c0 + sC >= C) ? c0 + sC - C : c0 + sC) {
+    int64_t total, int C, int reverse) {
+  for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
+    const int64_t i = w.i;
+    const int c0 = w.c0;
     float dv[8], xv[8], a[8], b[8], c[8];
     load8<XDT>(dy, i, dv);
     load8<XDT>(x, i, xv);
@@ -405,6 +445,16 @@ static int bn_grid_rows(int64_t M, int C) {
 
 extern "C" {
 
+// key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU; value < 0 only reads.
+// Returns the old value (-1 for an unknown key).
+int madnn_bn_tune(int key, int value) {
+  int* f = key == 0 ? &madnn::bn_tune().reverse : key == 1 ? &madnn::bn_tune().wg_per_cu : nullptr;
+  if (f == nullptr) return -1;
+  const int old = *f;
+  if (value >= 0) *f = key == 1 ? (value < 1 ? 1 : value) : (value != 0);
+  return old;
+}
+
 int madnn_bn_supported(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 : 0; }
 
 int madnn_bn_partial_rows(int64_t M, int C) { return madnn::bn_grid_rows(M, C); }
@@ -442,10 +492,10 @@ hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, unsigned char* 
   }
   MADNN_HIP_CHECK(hipGetLastError());
   const int64_t total = M * C;
-  const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
+  const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, res != nullptr, RELU, RES, {
     hipLaunchKernelGGL((bn_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, x, res, scale, shift, y,
-                       mask, total, C);
+                       mask, total, C, bn_tune().reverse);
   }));
   return hipGetLastError();
 }
@@ -473,10 +523,10 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const unsigned char* mask
                      save_mean, save_invstd, dw, db, ca, cb, cc);
   MADNN_HIP_CHECK(hipGetLastError());
   const int64_t total = M * C;
-  const int grid = stream_grid(total, 256 * 8, 16 * kNumCU);
+  const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, dy, x, mask, scale,
-                       shift, ca, cb, cc, dx, dres, total, C);
+                       shift, ca, cb, cc, dx, dres, total, C, bn_tune().reverse);
   }));
   return hipGetLastError();
 }
