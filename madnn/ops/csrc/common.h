@@ -12,6 +12,7 @@ namespace madnn {
 
 constexpr int kWave = 64;          // CDNA wavefront width (never 32)
 constexpr int kNumCU = 256;        // MI355X: 8 XCDs x 32 CUs
+constexpr int kNumXCD = 8;
 
 // dtype codes shared with the Python side (madnn/ops/_native.py)
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };

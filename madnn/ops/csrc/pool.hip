@@ -104,11 +104,148 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const void* __restrict
   }
 }
 
+// Workgroup ids are dispatched round-robin over the 8 XCDs, each with its own L2.  Adjacent
+// output rows share an input row (and adjacent input rows share a dy row in backward), so
+// the k3s2 kernels renumber workgroups to give each XCD one contiguous 1/8 of every
+// grid-stride sweep: neighbours then hit the same L2 instead of fetching the shared row
+// from HBM twice (MI355X_MICROARCH.md "XCD").  Needs gridDim.x % 8 == 0 (host guarantees).
+__device__ __forceinline__ unsigned xcd_block_id(int swz) {
+  if (!swz) return blockIdx.x;
+  return (blockIdx.x % kNumXCD) * (gridDim.x / kNumXCD) + blockIdx.x / kNumXCD;
+}
+
+// k = 3, s = 2 (the ResNet stem pool): the generic kernels' data-dependent window loops issue
+// one load at a time (9 dependent trips forward, up to 4 backward), so the pass was
+// latency-bound at ~3 TB/s.  These variants compute every window address up front and
+// issue all loads before the first compare, keeping 9 (forward) / 8 (backward) 16-byte
+// loads in flight per lane.  Same scan order, tie-breaking and NaN rule as above.
+template <int XDT>
+__global__ __launch_bounds__(256) void maxpool_k3s2_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                               uint64_t* __restrict__ arg, int N, int H, int W,
+                                                               int C, int Ho, int Wo, int p, int swz) {
+  const unsigned CG = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * Ho * Wo * CG;
+  for (unsigned idx = xcd_block_id(swz) * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned cg = idx % CG;
+    const unsigned pix = idx / CG;
+    const int ow = (int)(pix % (unsigned)Wo);
+    const unsigned t = pix / (unsigned)Wo;
+    const int oh = (int)(t % (unsigned)Ho);
+    const int n = (int)(t / (unsigned)Ho);
+    const int h0 = oh * 2 - p, w0 = ow * 2 - p;
+    float v[9][8];
+    bool ok[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int h = h0 + kh, w = w0 + kw;
+        const int q = kh * 3 + kw;
+        ok[q] = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        if (ok[q]) {
+          load8<XDT>(x, ((unsigned)(n * H + h) * W + (unsigned)w) * C + cg * 8, v[q]);
+        }
+      }
+    }
+    float best[8];
+    unsigned char a[8];
+    unsigned char first = 0;
+#pragma unroll
+    for (int q = 8; q >= 0; --q)
+      if (ok[q]) first = (unsigned char)q;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -__builtin_inff();
+      a[j] = first;
+    }
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      if (!ok[q]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (v[q][j] > best[j] || __builtin_isnan(v[q][j])) {
+          best[j] = v[q][j];
+          a[j] = (unsigned char)q;
+        }
+      }
+    }
+    store8<XDT>(y, (int64_t)pix * C + cg * 8, best);
+    if (arg) {
+      uint64_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) packed |= (uint64_t)a[j] << (8 * j);
+      arg[idx] = packed;
+    }
+  }
+}
+
+template <int XDT>
+__global__ __launch_bounds__(256) void maxpool_k3s2_bwd_kernel(const void* __restrict__ dy,
+                                                               const uint64_t* __restrict__ arg,
+                                                               void* __restrict__ dx, int N, int H, int W, int C,
+                                                               int Ho, int Wo, int p, int swz) {
+  const unsigned CG = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CG;
+  for (unsigned idx = xcd_block_id(swz) * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned cg = idx % CG;
+    const unsigned pix = idx / CG;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    // the (at most 2 x 2) output pixels whose window holds (h, w): o in {o1 - 1, o1}, o1 = (h+p)/2
+    const int oh1 = (h + p) >> 1, ow1 = (w + p) >> 1;
+    uint64_t pk[4];
+    float g[4][8];
+    unsigned pos[4];
+    bool ok[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int oh = oh1 - 1 + i, ow = ow1 - 1 + j;
+        const int dh = h - (oh * 2 - p), dw = w - (ow * 2 - p);
+        const int q = i * 2 + j;
+        ok[q] = oh >= 0 && oh < Ho && ow >= 0 && ow < Wo && dh <= 2 && dw <= 2;
+        pos[q] = (unsigned)(dh * 3 + dw);
+        if (ok[q]) {
+          const unsigned oidx = ((unsigned)(n * Ho + oh) * Wo + ow) * CG + cg;
+          pk[q] = arg[oidx];
+          load8<XDT>(dy, (int64_t)oidx * 8, g[q]);
+        }
+      }
+    }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ok[q]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (((pk[q] >> (8 * j)) & 0xffu) == pos[q]) ? g[q][j] : 0.f;
+    }
+    store8<XDT>(dx, (int64_t)idx * 8, acc);
+  }
+}
+
 }  // namespace madnn
 
 using namespace madnn;
 
+// k=3/s=2 routing (A/B runs, bench/pool_ab.py, profiles/r1_pool_ab.json): 0 generic loops,
+// 1 unrolled kernels (default), 2 unrolled kernels with the XCD-contiguous workgroup numbering.
+// At the stem shape (batch 512): fwd 389 / 379 / 408 us, bwd 434 / 398 / 398 us; the full
+// training step is unchanged within 0.1 % by either, so the pass is not latency- or L2-reuse-
+// bound in the way the kernel comments above assumed.
+static int g_pool_k3s2 = 1;
+
 extern "C" {
+
+int madnn_maxpool_set_k3s2(int on) {
+  const int old = g_pool_k3s2;
+  if (on >= 0) g_pool_k3s2 = on;
+  return old;
+}
 
 int madnn_maxpool_supported(int64_t numel, int C, int k) { return numel < (1ll << 31) && C % 8 == 0 && k * k <= 255; }
 
@@ -116,6 +253,15 @@ hipError_t madnn_maxpool_fwd(const void* x, void* y, void* arg, int N, int H, in
                              int s, int p, int xdt, hipStream_t stream) {
   const int64_t work = (int64_t)N * Ho * Wo * (C / 8);
   const int grid = stream_grid(work, 256, 16 * kNumCU);
+  if (k == 3 && s == 2 && p <= 2 && g_pool_k3s2) {
+    const int g8 = (grid + kNumXCD - 1) / kNumXCD * kNumXCD;
+    MADNN_DISPATCH_DT(xdt, XDT, {
+      hipLaunchKernelGGL((maxpool_k3s2_fwd_kernel<XDT>), dim3(g_pool_k3s2 == 2 ? g8 : grid), dim3(256), 0, stream, x, y,
+                         static_cast<uint64_t*>(arg), N, H, W, C, Ho, Wo, p,
+                         (int)(g_pool_k3s2 == 2));
+    });
+    return hipGetLastError();
+  }
   MADNN_DISPATCH_DT(xdt, XDT, {
     hipLaunchKernelGGL((maxpool_fwd_kernel<XDT>), dim3(grid), dim3(256), 0, stream, x, y,
                        static_cast<uint64_t*>(arg), N, H, W, C, Ho, Wo, k, s, p);
@@ -127,6 +273,15 @@ hipError_t madnn_maxpool_bwd(const void* dy, const void* arg, void* dx, int N, i
                              int k, int s, int p, int xdt, hipStream_t stream) {
   const int64_t work = (int64_t)N * H * W * (C / 8);
   const int grid = stream_grid(work, 256, 16 * kNumCU);
+  if (k == 3 && s == 2 && p <= 2 && g_pool_k3s2) {
+    const int g8 = (grid + kNumXCD - 1) / kNumXCD * kNumXCD;
+    MADNN_DISPATCH_DT(xdt, XDT, {
+      hipLaunchKernelGGL((maxpool_k3s2_bwd_kernel<XDT>), dim3(g_pool_k3s2 == 2 ? g8 : grid), dim3(256), 0, stream, dy,
+                         static_cast<const uint64_t*>(arg), dx, N, H, W, C, Ho, Wo, p,
+                         (int)(g_pool_k3s2 == 2));
+    });
+    return hipGetLastError();
+  }
   MADNN_DISPATCH_DT(xdt, XDT, {
     hipLaunchKernelGGL((maxpool_bwd_kernel<XDT>), dim3(grid), dim3(256), 0, stream, dy,
                        static_cast<const uint64_t*>(arg), dx, N, H, W, C, Ho, Wo, k, s, p);
