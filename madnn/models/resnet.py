@@ -23,7 +23,7 @@ from torch import nn
 
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
-from ..nn.norm import FusedMaxPool2d
+from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
 
 # A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
 _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
@@ -97,7 +97,7 @@ class ResNet(nn.Module):
         self.layer2 = self._make_layer(block, width * 2, layers[1], stride=2)
         self.layer3 = self._make_layer(block, width * 4, layers[2], stride=2)
         self.layer4 = self._make_layer(block, width * 8, layers[3], stride=2)
-        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.avgpool = FusedGlobalAvgPool2d((1, 1))
         self.fc = nn.Linear(width * 8 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):

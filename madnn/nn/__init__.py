@@ -1,8 +1,9 @@
 """madnn layers: fused-kernel norms / convolution and tensor-parallel (model-parallel) layers."""
 from .conv import FusedConv2d
-from .norm import FusedBatchNorm2d, FusedLayerNorm, FusedMaxPool2d, FusedRMSNorm, swap_layernorms
+from .norm import (FusedBatchNorm2d, FusedGlobalAvgPool2d, FusedLayerNorm, FusedMaxPool2d, FusedRMSNorm,
+                   swap_layernorms)
 
-__all__ = ["FusedBatchNorm2d", "FusedConv2d", "FusedLayerNorm", "FusedMaxPool2d", "FusedRMSNorm", "swap_layernorms"]
+__all__ = ["FusedBatchNorm2d", "FusedConv2d", "FusedGlobalAvgPool2d", "FusedLayerNorm", "FusedMaxPool2d", "FusedRMSNorm", "swap_layernorms"]
 from ..parallel.tp import (ColumnParallelLinear, MPBaseLinear, MPBaseReshape, MPInitialLinear, MPInitialReshape,
                            MPTanh, RowParallelLinear, set_debug_shapes)
 

@@ -112,3 +112,37 @@ class FusedMaxPool2d(nn.MaxPool2d):
         if self.return_indices:
             return super().forward(x)
         return ops.max_pool2d(x, self.kernel_size, self.stride, self.padding, self.dilation, self.ceil_mode)
+
+
+class _GlobalAvgPool(torch.autograd.Function):
+    """mean over H, W.  Backward writes dx = dy/(H*W) broadcast in ONE pass straight into the
+    input's memory format; ATen's AdaptiveAvgPool2d backward on a channels_last input ran an
+    NCHW-strided expand plus a slow strided layout copy (188 us/step on ResNet-50 batch 512,
+    profiles/r1_resnet50_dp1_pool.md) in front of the first BatchNorm backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        ctx.cl = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+        return x.mean((2, 3), keepdim=True)
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w = ctx.shape
+        g = (g.reshape(n, c).float() * (1.0 / (h * w))).to(g.dtype)
+        if ctx.cl:
+            return g.view(n, 1, 1, c).expand(n, h, w, c).contiguous().permute(0, 3, 1, 2)
+        return g.view(n, c, 1, 1).expand(n, c, h, w).contiguous()
+
+
+class FusedGlobalAvgPool2d(nn.AdaptiveAvgPool2d):
+    """``nn.AdaptiveAvgPool2d((1, 1))`` with a single-pass, memory-format-preserving backward."""
+
+    def __init__(self, output_size=(1, 1)):
+        super().__init__(output_size)
+
+    def forward(self, x: torch.Tensor):
+        os_ = self.output_size
+        if x.dim() == 4 and (os_ == 1 or tuple(os_) == (1, 1)):
+            return _GlobalAvgPool.apply(x)
+        return super().forward(x)

@@ -351,3 +351,22 @@ def test_distribute_meta_model_remaps_optimizer():
     opt.step()
     assert torch.isfinite(loss)
     assert any(not torch.equal(b, p.detach()) for b, p in zip(before, model.parameters()))
+
+
+@pytest.mark.parametrize("cl", [True, False])
+def test_global_avgpool_grad_and_layout(cl):
+    """FusedGlobalAvgPool2d == AdaptiveAvgPool2d((1,1)) in value and gradient; dx keeps x's layout."""
+    from madnn.nn import FusedGlobalAvgPool2d
+
+    x = torch.randn(3, 5, 4, 6, dtype=torch.float64)
+    if cl:
+        x = x.contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = FusedGlobalAvgPool2d((1, 1))(xa), torch.nn.AdaptiveAvgPool2d((1, 1))(xb)
+    assert ya.shape == yb.shape == (3, 5, 1, 1)
+    torch.testing.assert_close(ya, yb)
+    g = torch.randn_like(yb)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(xa.grad, xb.grad)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
