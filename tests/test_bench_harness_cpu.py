@@ -50,3 +50,20 @@ def test_launcher_tears_down_on_failure():
     assert out.returncode == 3
     assert time.time() - t0 < 30  # rank 0 was torn down, not waited for
     os.remove(script)
+
+
+def test_bench_py_gpt2_pipeline_four_ranks_cpu():
+    """``bench.py --model gpt2-medium`` at 4 ranks = the 4-stage pipeline (first, two interior and
+    last stage) of the BASELINE's GPT-2 PP config; short sequences, CPU/gloo."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1",
+           "--device", "cpu", "--model", "gpt2-medium", "--batch", "4", "--seq-len", "32", "--microbatches", "4"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 4 and res["scaling"] == "strong" and res["value"] > 0
+    assert res["config"]["parallelism"] == "pp4" and res["config"]["global_batch"] == 4
