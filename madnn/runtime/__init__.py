@@ -118,29 +118,60 @@ def seed_all(seed: int, rank_offset: bool = False) -> None:
         pass
 
 
+AXES = ("dp", "pp", "cp", "tp")  # outermost -> innermost rank order
+
+
 @dataclass(frozen=True)
 class Mesh:
+    """Logical device mesh over the world: data x pipeline x context x tensor parallel.
+
+    ``cp`` (context / sequence parallel) is the extension axis SURVEY §5.7 asks for: no BASELINE
+    config needs it, so it defaults to 1, but its process groups already exist, so ring attention
+    or Ulysses can be added without changing this API.  Ranks are laid out tp innermost, then cp,
+    pp and dp."""
+
     dp: int
     pp: int
     tp: int
+    cp: int = 1
 
     @property
     def size(self) -> int:
-        return self.dp * self.pp * self.tp
+        return self.dp * self.pp * self.cp * self.tp
+
+    def _dims(self):
+        return [getattr(self, a) for a in AXES]
+
+    def coord(self, rank: int) -> dict:
+        """rank -> {axis: index} for every axis."""
+        out = {}
+        for a, n in zip(reversed(AXES), reversed(self._dims())):
+            out[a] = rank % n
+            rank //= n
+        return out
 
     def coords(self, rank: int):
-        """rank -> (dp_idx, pp_idx, tp_idx); tp innermost, then pp, then dp."""
-        tp_i = rank % self.tp
-        pp_i = (rank // self.tp) % self.pp
-        dp_i = rank // (self.tp * self.pp)
-        return dp_i, pp_i, tp_i
+        """rank -> (dp_idx, pp_idx, tp_idx) (the cp index is in :meth:`coord`)."""
+        c = self.coord(rank)
+        return c["dp"], c["pp"], c["tp"]
 
-    def rank_of(self, dp_i: int, pp_i: int, tp_i: int) -> int:
-        return (dp_i * self.pp + pp_i) * self.tp + tp_i
+    def rank_of(self, dp_i: int, pp_i: int, tp_i: int, cp_i: int = 0) -> int:
+        return ((dp_i * self.pp + pp_i) * self.cp + cp_i) * self.tp + tp_i
+
+    def axis_groups(self, axis: str):
+        """Every rank list that varies only along ``axis`` (one group per other-axes coordinate)."""
+        if axis not in AXES:
+            raise KeyError(f"unknown mesh axis {axis!r}; expected one of {AXES}")
+        groups = {}
+        for r in range(self.size):
+            c = self.coord(r)
+            key = tuple(c[a] for a in AXES if a != axis)
+            groups.setdefault(key, []).append(r)
+        return [groups[k] for k in sorted(groups)]
 
 
 class ProcessGroups:
-    """dp / pp / tp sub-groups over the world (every rank creates every group
+    """dp / pp / cp / tp sub-groups over the world (every rank creates every group
     in the same order, as torch.distributed requires).
 
     On one MI355X node all 8 GPUs are xGMI peers (7 links each), so no axis is
@@ -156,37 +187,20 @@ class ProcessGroups:
             raise ValueError(f"mesh {mesh} does not cover world size {world}")
         self.mesh = mesh
         self.rank = get_rank()
-        self.dp_idx, self.pp_idx, self.tp_idx = mesh.coords(self.rank)
-        self.dp_group = self.pp_group = self.tp_group = None
-        self.dp_ranks = [mesh.rank_of(d, self.pp_idx, self.tp_idx) for d in range(mesh.dp)]
-        self.pp_ranks = [mesh.rank_of(self.dp_idx, p, self.tp_idx) for p in range(mesh.pp)]
-        self.tp_ranks = [mesh.rank_of(self.dp_idx, self.pp_idx, t) for t in range(mesh.tp)]
+        c = mesh.coord(self.rank)
+        self.dp_idx, self.pp_idx, self.cp_idx, self.tp_idx = c["dp"], c["pp"], c["cp"], c["tp"]
+        for axis in AXES:
+            setattr(self, f"{axis}_group", None)
+            setattr(self, f"{axis}_ranks", next(g for g in mesh.axis_groups(axis) if self.rank in g))
         if not dist.is_initialized():
             return
-        for axis in ("dp", "pp", "tp"):
-            for ranks in self._all_groups(axis):
+        for axis in AXES:
+            for ranks in mesh.axis_groups(axis):
                 key = tuple(ranks)
                 if key not in ProcessGroups._cache:
                     ProcessGroups._cache[key] = dist.new_group(list(ranks)) if len(ranks) < world else None
                 if self.rank in ranks:
                     setattr(self, f"{axis}_group", ProcessGroups._cache[key])
-
-    def _all_groups(self, axis):
-        m = self.mesh
-        out = []
-        if axis == "dp":
-            for p in range(m.pp):
-                for t in range(m.tp):
-                    out.append([m.rank_of(d, p, t) for d in range(m.dp)])
-        elif axis == "pp":
-            for d in range(m.dp):
-                for t in range(m.tp):
-                    out.append([m.rank_of(d, p, t) for p in range(m.pp)])
-        else:
-            for d in range(m.dp):
-                for p in range(m.pp):
-                    out.append([m.rank_of(d, p, t) for t in range(m.tp)])
-        return out
 
 
 def topology() -> dict:

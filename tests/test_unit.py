@@ -370,3 +370,21 @@ def test_global_avgpool_grad_and_layout(cl):
     yb.backward(g)
     torch.testing.assert_close(xa.grad, xb.grad)
     assert xa.grad.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
+
+
+def test_mesh_axes_and_cp_extension_point():
+    """Mesh: tp innermost, then cp, pp, dp; rank_of inverts coord; axis groups partition the world."""
+    from madnn.runtime import AXES, Mesh
+
+    m = Mesh(dp=2, pp=2, tp=2)
+    assert m.cp == 1 and m.size == 8
+    assert m.coords(5) == (1, 0, 1) and m.rank_of(1, 0, 1) == 5
+    m4 = Mesh(dp=2, pp=2, tp=2, cp=2)
+    for r in range(m4.size):
+        c = m4.coord(r)
+        assert m4.rank_of(c["dp"], c["pp"], c["tp"], c["cp"]) == r
+    for axis in AXES:
+        groups = m4.axis_groups(axis)
+        assert sorted(r for g in groups for r in g) == list(range(16))
+        assert all(len(g) == getattr(m4, axis) for g in groups)
+    assert m4.axis_groups("tp")[0] == [0, 1] and m4.axis_groups("cp")[0] == [0, 2]
