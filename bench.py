@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu (gloo; for testing the harness)")
+    ap.add_argument("--backend", default=None,
+                    help="process-group backend override (default: nccl=RCCL on cuda, gloo on cpu); gloo on cuda "
+                         "lets tests run several ranks on one GPU, which RCCL refuses")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--miopen-benchmark", type=int, default=0,
                     help="torch.backends.cudnn.benchmark (MIOpen find).  Both modes read the shipped MI355X "
@@ -61,7 +64,10 @@ def _sync_all():
         return
     torch.cuda.synchronize()
     if dist.is_initialized():
-        dist.barrier(device_ids=[torch.cuda.current_device()])
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
         torch.cuda.synchronize()
 
 
@@ -151,7 +157,7 @@ def main():
     import madnn
 
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
-    madnn.init(device=args.device)
+    madnn.init(device=args.device, backend=args.backend)
     rank = madnn.get_rank()
     if args.model == "resnet50":
         dt, samples_per_step, config = bench_resnet(args, world, rank)
