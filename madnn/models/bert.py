@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedLayerNorm
-from .common import init_module_, SelfAttention, init_normal_, mlm_loss
+from .common import init_module_, SelfAttention, init_normal_, linear, mlm_loss
 
 
 @dataclass
@@ -79,7 +79,7 @@ class BertLayer(nn.Module):
 
     def forward(self, x):
         y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
-        z, _ = self.ffn_norm(self.drop(self.fc2(F.gelu(self.fc1(y)))), residual=y)
+        z, _ = self.ffn_norm(self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y)))), residual=y)
         return z
 
 

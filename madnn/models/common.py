@@ -35,6 +35,16 @@ def mlm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None) -> 
     return ops.cross_entropy(logits, targets, shift=False, vocab=vocab, ignore_index=-100)
 
 
+def linear(mod: nn.Module, x: torch.Tensor, gelu: bool = False) -> torch.Tensor:
+    """``mod(x)`` (then tanh-GELU if asked).  A plain biased ``nn.Linear`` runs through
+    ``ops.linear``, whose backward produces the bias gradient (and the GELU backward) in one
+    K11 pass; any other module (e.g. a tensor-parallel replacement) is called as is."""
+    if ops.FUSED_LINEAR and type(mod) is nn.Linear and mod.bias is not None:
+        return ops.linear(x, mod.weight, mod.bias, gelu=gelu)
+    y = mod(x)
+    return F.gelu(y, approximate="tanh") if gelu else y
+
+
 class SelfAttention(nn.Module):
     """Multi-head (optionally grouped-query) self-attention with one QKV GEMM."""
 
@@ -50,7 +60,7 @@ class SelfAttention(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         b, s, _ = x.shape
-        qkv = self.qkv(x).view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
+        qkv = linear(self.qkv, x).view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
         drop = self.dropout if self.training else 0.0
         if ops.attention_supported(qkv, self.head_dim, drop):
             # K8 HIP attention on the [B, S, heads, D] layout the projection produced: no
@@ -61,7 +71,7 @@ class SelfAttention(nn.Module):
                 q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
                 q, k = self.rope(q, k, seq_dim=1)
                 o = ops.attention(q, k, v, causal=self.causal)
-            return self.proj(o.view(b, s, self.heads * self.head_dim))
+            return linear(self.proj, o.view(b, s, self.heads * self.head_dim))
         q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         if self.rope is not None:
@@ -69,7 +79,7 @@ class SelfAttention(nn.Module):
         gqa = self.kv_heads != self.heads
         o = F.scaled_dot_product_attention(q, k, v, is_causal=self.causal,
                                            dropout_p=self.dropout if self.training else 0.0, enable_gqa=gqa)
-        return self.proj(o.transpose(1, 2).reshape(b, s, self.heads * self.head_dim))
+        return linear(self.proj, o.transpose(1, 2).reshape(b, s, self.heads * self.head_dim))
 
 
 class RotaryEmbedding(nn.Module):

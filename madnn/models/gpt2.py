@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedLayerNorm
-from .common import init_module_, SelfAttention, causal_lm_loss, init_normal_, scale_residual_proj_
+from .common import init_module_, SelfAttention, causal_lm_loss, init_normal_, linear, scale_residual_proj_
 
 
 @dataclass
@@ -71,7 +71,7 @@ class GPT2MLP(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x):
-        return self.drop(self.c_proj(F.gelu(self.c_fc(x), approximate="tanh")))
+        return self.drop(linear(self.c_proj, linear(self.c_fc, x, gelu=True)))
 
 
 class GPT2Block(nn.Module):

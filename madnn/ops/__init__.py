@@ -14,6 +14,7 @@ from pathlib import Path
 from typing import Optional, Sequence
 
 import torch
+import torch.nn.functional as F
 
 from . import reference
 
@@ -575,3 +576,75 @@ __all__ = [
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":
     load_kernels()
+
+
+# --------------------------------------------------------------------------- K11
+FUSED_LINEAR = os.environ.get("MADNN_FUSED_LINEAR", "1") != "0"  # models.common.linear routing (A/B switch)
+
+def _gelu_tanh_grad(p: torch.Tensor) -> torch.Tensor:
+    k0, k1 = 0.7978845608028654, 0.044715
+    t = torch.tanh(k0 * (p + k1 * p * p * p))
+    return 0.5 * (1 + t) + 0.5 * p * (1 - t * t) * k0 * (1 + 3 * k1 * p * p)
+
+
+def bias_grad(dy: torch.Tensor, pre: Optional[torch.Tensor] = None, bias_dtype: Optional[torch.dtype] = None):
+    """A Linear's bias gradient: the column sum of ``dy`` over every leading dim (K11, bias.hip).
+
+    With ``pre`` (the tanh-GELU input) the GELU backward is fused into the same pass: returns
+    ``(db, dp)`` with ``dp = dy * gelu'(pre)`` and ``db = sum(dp)``; otherwise ``(db, None)``."""
+    bias_dtype = bias_dtype or dy.dtype
+    n = dy.shape[-1]
+    if not _is_dev(dy) or n % 8:
+        acc = torch.promote_types(dy.dtype, torch.float32)
+        g = dy.to(acc)
+        if pre is not None:
+            g = g * _gelu_tanh_grad(pre.to(acc))
+        return g.reshape(-1, n).sum(0).to(bias_dtype), (g.to(dy.dtype) if pre is not None else None)
+    db, dp = _need_native("bias_grad").bias_grad(dy, pre, bias_dtype)
+    return db, (dp.view(dy.shape) if pre is not None else None)
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) with act in {identity, tanh-GELU}; the backward's bias gradient (and the
+    GELU backward) come from one K11 pass, the two GEMMs stay on hipBLASLt."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gelu):
+        pre = F.linear(x, weight, bias)
+        ctx.gelu = gelu
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        if gelu:
+            ctx.save_for_backward(x, weight, pre)
+            return F.gelu(pre, approximate="tanh")
+        ctx.save_for_backward(x, weight)
+        return pre
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.gelu:
+            x, weight, pre = ctx.saved_tensors
+        else:
+            (x, weight), pre = ctx.saved_tensors, None
+        db = None
+        if ctx.gelu:
+            db, g = bias_grad(g, pre, ctx.bias_dtype or g.dtype)
+            if ctx.bias_dtype is None:
+                db = None
+        elif ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
+            db, _ = bias_grad(g, None, ctx.bias_dtype)
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ weight).view(*x.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = (g2.t() @ x.reshape(-1, x.shape[-1])).to(weight.dtype)
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False):
+    """``F.linear`` (optionally followed by tanh-GELU) whose backward fuses the bias gradient (K11).
+    Falls back to eager ops on CPU tensors."""
+    if not _is_dev(x) or weight.shape[0] % 8 or not torch.is_grad_enabled():
+        y = F.linear(x, weight, bias)
+        return F.gelu(y, approximate="tanh") if gelu else y
+    return _LinearFn.apply(x, weight, bias, gelu)

@@ -32,7 +32,7 @@ RUNTIME_SO = HERE / "_madnn_runtime.so"
 
 ARCH = os.environ.get("MADNN_OFFLOAD_ARCH", "gfx950")
 KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "pool.hip", "attn.hip", "conv.hip",
-                  "stem.hip", "binding.cpp"]
+                  "stem.hip", "bias.hip", "binding.cpp"]
 RUNTIME_SOURCES = ["runtime.cpp"]
 # per-source extra flags: MFMA kernels keep their accumulators in the (unified) VGPR file
 # instead of AGPRs, which removes a v_accvgpr_read/write around every softmax element

@@ -1,0 +1,172 @@
+// K11: bias gradient of a Linear layer, optionally fused with the tanh-GELU backward.
+//
+//   plain : db[n]  = sum_m dy[m, n]
+//   GELU  : dp     = dy * gelu'(p)   (p = the pre-activation x W^T + b, written out for the GEMMs)
+//           db[n]  = sum_m dp[m, n]
+//
+// Why: on GPT-2 medium (profiles/r1_gpt2m_dp1_k8.md) ATen spent ~30 us per Linear on the
+// bias-gradient column sum (97 per step) and ran the GELU backward as its own pass, re-reading
+// dp afterwards for c_fc's bias.  Both are HBM streams; here one pass reads dy (and p), writes dp
+// and produces the column sums.
+// Layout: [M, N] row-major, N % 8 == 0.  A lane owns 8 consecutive columns (16-byte access);
+// a 256-lane workgroup covers a strip of min(2048, N) columns (blockIdx.x) in 256/(strip/8)
+// row slots and walks rows with 4 in flight per lane; its row slots are summed in LDS into ONE
+// fp32 partial row.  A finalize (32 columns x 32 row slices per 1024-lane block) sums the
+// partial rows in a fixed order (deterministic, no float atomics) and casts to the bias dtype.
+#include "common.h"
+
+namespace madnn {
+
+constexpr int kBiasLanes = 256;
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float t = tanhf(k0 * (x + k1 * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+// Row slots: a 256-lane workgroup is RPI = 256 / TPR row slots of TPR = min(256, N/8) lanes,
+// so narrow layers (N = 1024: TPR 128, 2 rows per step) still run 4 full waves per workgroup.
+struct BiasGeom {
+  int tpr, rpi, strips;
+};
+__host__ __device__ inline BiasGeom bias_geom(int N) {
+  const int lanes = N / 8;
+  const int tpr = lanes < kBiasLanes ? lanes : kBiasLanes;
+  return {tpr, kBiasLanes / tpr, (lanes + tpr - 1) / tpr};
+}
+
+template <int XDT, bool GELU>
+__global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
+                                                               const void* __restrict__ pre, void* __restrict__ dp,
+                                                               int64_t M, int N, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) float slab[kBiasLanes * 8];  // [rpi][tpr * 8]
+  const BiasGeom g = bias_geom(N);
+  const int t = threadIdx.x;
+  const int cl = t % g.tpr, rs = t / g.tpr;
+  const int col = blockIdx.x * g.tpr * 8 + cl * 8;
+  const bool active = rs < g.rpi && col < N;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (active) {
+    const int64_t step = (int64_t)gridDim.y * g.rpi;
+    int64_t r = (int64_t)blockIdx.y * g.rpi + rs;
+    for (; r + 3 * step < M; r += 4 * step) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8<XDT>(dy, (r + u * step) * N + col, v[u]);
+      if constexpr (GELU) {
+        float p[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load8<XDT>(pre, (r + u * step) * N + col, p[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad(p[u][j]);
+          store8<XDT>(dp, (r + u * step) * N + col, v[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[u][j];
+    }
+    for (; r < M; r += step) {
+      float v[8];
+      load8<XDT>(dy, r * N + col, v);
+      if constexpr (GELU) {
+        float p[8];
+        load8<XDT>(pre, r * N + col, p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad(p[j]);
+        store8<XDT>(dp, r * N + col, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+  }
+  if (g.rpi == 1) {
+    if (active) store8<kF32>(partial, (int64_t)blockIdx.y * N + col, s);
+    return;
+  }
+  if (rs < g.rpi) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) slab[rs * g.tpr * 8 + cl * 8 + j] = s[j];
+  }
+  __syncthreads();
+  const int width = g.tpr * 8;
+  for (int c = t; c < width; c += kBiasLanes) {
+    const int n = blockIdx.x * width + c;
+    if (n >= N) continue;
+    float a = 0.f;
+    for (int q = 0; q < g.rpi; ++q) a += slab[q * width + c];
+    partial[(int64_t)blockIdx.y * N + n] = a;
+  }
+}
+
+// 32 columns x 32 row slices per 1024-lane block; slices combined in a fixed order
+template <int ODT>
+__global__ __launch_bounds__(1024) void bias_grad_finalize_kernel(const float* __restrict__ partial, int R, int N,
+                                                                  void* __restrict__ db) {
+  __shared__ float red[32][33];
+  const int c = threadIdx.x % 32, sl = threadIdx.x / 32;
+  const int n = blockIdx.x * 32 + c;
+  float a = 0.f;
+  if (n < N)
+    for (int r = sl; r < R; r += 32) a += partial[(int64_t)r * N + n];
+  red[sl][c] = a;
+  __syncthreads();
+  if (sl == 0 && n < N) {
+    float tot = 0.f;
+    for (int q = 0; q < 32; ++q) tot += red[q][c];
+    Elem<ODT>::store(static_cast<typename Elem<ODT>::T*>(db), n, tot);
+  }
+}
+
+}  // namespace madnn
+
+using namespace madnn;
+
+extern "C" {
+
+int madnn_bias_grad_supported(int64_t M, int N) { return N % 8 == 0 && N > 0 && M > 0; }
+
+// partial rows R: ~4 workgroups per CU in total, each walking >= 4 row steps
+int madnn_bias_grad_rows(int64_t M, int N) {
+  const BiasGeom g = bias_geom(N);
+  int64_t r = (4 * kNumCU + g.strips - 1) / g.strips;
+  const int64_t cap = (M + 4 * g.rpi - 1) / (4 * g.rpi);
+  if (r > cap) r = cap;
+  if (r < 1) r = 1;
+  if (r > 4096) r = 4096;
+  return (int)r;
+}
+
+// dy, pre, dp: [M, N] of dtype xdt; partial: [R, N] fp32 with R = madnn_bias_grad_rows; db: [N] of odt
+hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M, int N, int xdt, float* partial,
+                           void* db, int odt, hipStream_t stream) {
+  if (!madnn_bias_grad_supported(M, N)) return hipErrorInvalidValue;
+  const BiasGeom g = bias_geom(N);
+  const int R = madnn_bias_grad_rows(M, N);
+  const dim3 grid(g.strips, R);
+  MADNN_DISPATCH_DT(xdt, XDT, {
+    if (pre) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
+                         partial);
+    } else {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, false>), grid, dim3(kBiasLanes), 0, stream, dy, nullptr, nullptr,
+                         M, N, partial);
+    }
+  });
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  MADNN_DISPATCH_DT(odt, ODT, {
+    hipLaunchKernelGGL((bias_grad_finalize_kernel<ODT>), dim3((N + 31) / 32), dim3(1024), 0, stream, partial, R, N,
+                       db);
+  });
+  return hipGetLastError();
+}
+
+}  // extern "C"

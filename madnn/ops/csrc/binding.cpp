@@ -36,6 +36,9 @@ int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
                         const float*, const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*,
                         const float*, int, hipStream_t);
+int madnn_bias_grad_supported(int64_t, int);
+int madnn_bias_grad_rows(int64_t, int);
+hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
@@ -581,6 +584,31 @@ at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, i
   return dx;
 }
 
+// K11 Linear bias gradient.  dy (and pre): [..., N], row-major contiguous.  Returns
+// (db [N] in bias_dtype, dp) where dp = dy * gelu_tanh'(pre) when pre is given (else empty).
+std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::optional<at::Tensor>& pre,
+                                             at::ScalarType bias_dtype) {
+  check_dev(dy, "dy");
+  at::Tensor g = dy.contiguous();
+  const int64_t N = g.size(-1), M = g.numel() / N;
+  TORCH_CHECK(madnn_bias_grad_supported(M, (int)N), "bias_grad: last dim must be a multiple of 8");
+  at::Tensor pc, dp;
+  if (pre.has_value()) {
+    pc = pre->contiguous();
+    TORCH_CHECK(pc.sizes() == g.sizes() && pc.scalar_type() == g.scalar_type(), "bias_grad: pre mismatch");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  if (pc.defined()) dp = at::empty_like(g);
+  else dp = at::empty({0}, g.options());
+  const int R = madnn_bias_grad_rows(M, (int)N);
+  at::Tensor partial = at::empty({R, N}, g.options().dtype(at::kFloat));
+  at::Tensor db = at::empty({N}, g.options().dtype(bias_dtype));
+  check(madnn_bias_grad(g.data_ptr(), pc.defined() ? pc.data_ptr() : nullptr, pc.defined() ? dp.data_ptr() : nullptr,
+                        M, (int)N, dt_code(g), partial.data_ptr<float>(), db.data_ptr(), dt_code(db), cur_stream(g)),
+        "bias_grad");
+  return {db, dp};
+}
+
 // K8 attention.  q: [B, S, H, D], k/v: [B, S, Hkv, D] bf16 views with a contiguous last dim
 // (any other strides, e.g. slices of one packed QKV projection).
 void attn_check(const at::Tensor& t, const char* name, int64_t D) {
@@ -679,6 +707,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("conv1x1_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
@@ -712,6 +741,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
   m.impl("maxpool_fwd", maxpool_fwd);
+  m.impl("bias_grad", bias_grad);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_bwd", attn_bwd);
   m.impl("maxpool_bwd", maxpool_bwd);

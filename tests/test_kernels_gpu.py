@@ -318,3 +318,44 @@ def test_maxpool_module_fallback_and_resnet_stem(cuda):
     xc = x.contiguous(memory_format=torch.channels_last)
     assert ops.max_pool_supported(xc, 3, 2, 1)
     torch.testing.assert_close(m(xc), torch.nn.functional.max_pool2d(x, 3, 2, 1), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("shape", [(4, 512, 1024), (3, 77, 4096), (1000, 264), (2, 64, 3072)])
+@pytest.mark.parametrize("gelu", [False, True])
+def test_bias_grad_k11(cuda, shape, gelu):
+    """K11: column sum (and fused tanh-GELU backward) vs the fp32 PyTorch reference."""
+    torch.manual_seed(5)
+    dy = torch.randn(*shape, device=cuda).bfloat16()
+    pre = torch.randn(*shape, device=cuda).bfloat16() * 2 if gelu else None
+    db, dp = ops.bias_grad(dy, pre, torch.float32)
+    g = dy.float()
+    if gelu:
+        pr = pre.float().requires_grad_(True)
+        torch.nn.functional.gelu(pr, approximate="tanh").backward(g)
+        g = pr.grad
+        torch.testing.assert_close(dp.float(), g, atol=2e-2, rtol=1e-2)
+    else:
+        assert dp is None
+    ref = g.reshape(-1, shape[-1]).sum(0)
+    torch.testing.assert_close(db, ref, atol=1e-3 * ref.abs().max().item() + 1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+def test_fused_linear_matches_eager(cuda, gelu):
+    """ops.linear (K11 bias grad in the backward) == F.linear (+gelu) in output and all three grads."""
+    torch.manual_seed(6)
+    x = torch.randn(4, 128, 256, device=cuda).bfloat16().requires_grad_(True)
+    w = (torch.randn(512, 256, device=cuda) * 0.05).bfloat16().requires_grad_(True)
+    b = (torch.randn(512, device=cuda) * 0.1).bfloat16().requires_grad_(True)
+    y = ops.linear(x, w, b, gelu=gelu)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.linear(xr, wr, br)
+    if gelu:
+        yr = torch.nn.functional.gelu(yr, approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        assert a.dtype == torch.bfloat16
+        torch.testing.assert_close(a.float(), r, atol=3e-2 * r.abs().max().item(), rtol=3e-2)

@@ -388,3 +388,19 @@ def test_mesh_axes_and_cp_extension_point():
         assert sorted(r for g in groups for r in g) == list(range(16))
         assert all(len(g) == getattr(m4, axis) for g in groups)
     assert m4.axis_groups("tp")[0] == [0, 1] and m4.axis_groups("cp")[0] == [0, 2]
+
+
+def test_fused_linear_cpu_fallback_and_reference_gelu_grad():
+    """ops.linear on CPU is F.linear(+gelu); ops.bias_grad's eager path matches autograd's GELU backward."""
+    from madnn import ops
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, dtype=torch.float64)
+    w, b = torch.randn(24, 16, dtype=torch.float64), torch.randn(24, dtype=torch.float64)
+    torch.testing.assert_close(ops.linear(x, w, b, gelu=True), F.gelu(F.linear(x, w, b), approximate="tanh"))
+    pre = torch.randn(7, 24, dtype=torch.float64, requires_grad=True)
+    dy = torch.randn(7, 24, dtype=torch.float64)
+    F.gelu(pre, approximate="tanh").backward(dy)
+    db, dp = ops.bias_grad(dy, pre.detach())
+    torch.testing.assert_close(dp, pre.grad)
+    torch.testing.assert_close(db, pre.grad.sum(0))
