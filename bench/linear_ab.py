@@ -16,6 +16,9 @@ def main():
     from madnn.optim import FusedAdam
 
     madnn.init()
+    import ctypes
+
+    tune = ctypes.CDLL(str(ops.kernels_path())).madnn_bias_tune
     kern = {}
     for n in (1024, 3072, 4096):
         dy = torch.randn(16384, n, device="cuda").bfloat16()
@@ -31,6 +34,12 @@ def main():
             e_.synchronize()
             return round(s_.elapsed_time(e_) / it * 1e3, 1)
 
+        for wg in (1, 2, 4, 8):
+            old = (tune(0, wg), tune(1, wg))
+            kern[f"{n}_wg{wg}"] = {"k11_sum_us": t(lambda: ops.bias_grad(dy, None, torch.bfloat16)),
+                                   "k11_gelu_us": t(lambda: ops.bias_grad(dy, pre, torch.bfloat16))}
+            tune(0, old[0])
+            tune(1, old[1])
         kern[n] = {"k11_sum_us": t(lambda: ops.bias_grad(dy, None, torch.bfloat16)),
                    "aten_sum_us": t(lambda: dy.sum(0)),
                    "k11_gelu_us": t(lambda: ops.bias_grad(dy, pre, torch.bfloat16)),

@@ -129,14 +129,26 @@ __global__ __launch_bounds__(1024) void bias_grad_finalize_kernel(const float* _
 
 using namespace madnn;
 
+// partial-row count = wg_per_cu x 256 CUs / strips (A/B knob: madnn_bias_tune).  Measured at
+// M = 16384 (profiles/r1_linear_ab.json): the plain column sum is fastest at 1 workgroup per CU
+// (N=1024/3072/4096: 11.6/20.2/23.3 us vs 17.4/24.2/28.6 at 4: fewer partial rows to write and
+// re-read), the GELU variant, which also writes dp, at 4 (36.4/80.9/92.3 us vs 40.6/135/134 at 1).
+static int g_bias_wg_per_cu[2] = {1, 4};
+
 extern "C" {
+
+int madnn_bias_tune(int gelu, int wg_per_cu) {
+  const int old = g_bias_wg_per_cu[gelu ? 1 : 0];
+  if (wg_per_cu > 0) g_bias_wg_per_cu[gelu ? 1 : 0] = wg_per_cu;
+  return old;
+}
 
 int madnn_bias_grad_supported(int64_t M, int N) { return N % 8 == 0 && N > 0 && M > 0; }
 
-// partial rows R: ~4 workgroups per CU in total, each walking >= 4 row steps
-int madnn_bias_grad_rows(int64_t M, int N) {
+// partial rows R: ~wg_per_cu workgroups per CU in total, each walking >= 4 row steps
+int madnn_bias_grad_rows(int64_t M, int N, int gelu) {
   const BiasGeom g = bias_geom(N);
-  int64_t r = (4 * kNumCU + g.strips - 1) / g.strips;
+  int64_t r = (g_bias_wg_per_cu[gelu ? 1 : 0] * kNumCU + g.strips - 1) / g.strips;
   const int64_t cap = (M + 4 * g.rpi - 1) / (4 * g.rpi);
   if (r > cap) r = cap;
   if (r < 1) r = 1;
@@ -144,12 +156,13 @@ int madnn_bias_grad_rows(int64_t M, int N) {
   return (int)r;
 }
 
-// dy, pre, dp: [M, N] of dtype xdt; partial: [R, N] fp32 with R = madnn_bias_grad_rows; db: [N] of odt
+// dy, pre, dp: [M, N] of dtype xdt; partial: [R, N] fp32 with R = madnn_bias_grad_rows(M, N, pre != 0);
+// db: [N] of odt
 hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M, int N, int xdt, float* partial,
                            void* db, int odt, hipStream_t stream) {
   if (!madnn_bias_grad_supported(M, N)) return hipErrorInvalidValue;
   const BiasGeom g = bias_geom(N);
-  const int R = madnn_bias_grad_rows(M, N);
+  const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
     if (pre) {

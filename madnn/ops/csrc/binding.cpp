@@ -37,7 +37,7 @@ hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t
                         const float*, const float*, float*, float*, int64_t*, float*, float*, float*, float*, float*,
                         const float*, int, hipStream_t);
 int madnn_bias_grad_supported(int64_t, int);
-int madnn_bias_grad_rows(int64_t, int);
+int madnn_bias_grad_rows(int64_t, int, int);
 hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
@@ -600,7 +600,7 @@ std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::op
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   if (pc.defined()) dp = at::empty_like(g);
   else dp = at::empty({0}, g.options());
-  const int R = madnn_bias_grad_rows(M, (int)N);
+  const int R = madnn_bias_grad_rows(M, (int)N, pc.defined() ? 1 : 0);
   at::Tensor partial = at::empty({R, N}, g.options().dtype(at::kFloat));
   at::Tensor db = at::empty({N}, g.options().dtype(bias_dtype));
   check(madnn_bias_grad(g.data_ptr(), pc.defined() ? pc.data_ptr() : nullptr, pc.defined() ? dp.data_ptr() : nullptr,
