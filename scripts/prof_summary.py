@@ -15,7 +15,7 @@ CATS = [
     ("conv bwd-data (MIOpen)", r"igemm_bwd|ConvBwd|naive_conv.*bwd"),
     ("conv bwd-weight (MIOpen)", r"igemm_wrw|ConvWrw|naive_conv.*wrw"),
     ("batchnorm (MIOpen)", r"BatchNorm"),
-    ("GEMM (hipBLASLt/rocBLAS)", r"^Cijk_|gemm|Gemm"),
+    ("GEMM (hipBLASLt/rocBLAS)", r"^Cijk_|^Custom_Cijk_|gemm|Gemm"),
     ("attention", r"attn|flash|fmha"),
     ("RCCL", r"ncclDevKernel|rccl|nccl"),
     ("elementwise / reduce (ATen)", r"elementwise|vectorized|reduce_kernel|unrolled|SubTensorOp|Op2d|Op1d"),
