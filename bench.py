@@ -3,13 +3,21 @@
 
   "samples/sec whole-node ResNet-50 DP + GPT-2 PP at 1/2/4/8 MI355X; scaling eff"
 
-Default (the driver's contract): ResNet-50, automatic data parallelism
-(``madnn.distribute``), bf16 compute with fp32 master weights and fp32 BatchNorm,
-channels_last, FusedSGD (momentum 0.9, wd 5e-5) on the hand-written gfx950 kernel,
-bucketed RCCL all-reduce overlapped with backward; synthetic ImageNet-shaped
-data and random init (no network on the box); fixed per-GPU batch => weak
-scaling.  ``--model gpt2-medium`` runs the GPT-2 medium pipeline-parallel
-config instead.
+Default (the driver's contract) measures BOTH halves of the metric in one run:
+
+* the primary ``value``: ResNet-50, automatic data parallelism
+  (``madnn.distribute``), bf16 compute with fp32 master weights and fp32 BatchNorm,
+  channels_last, FusedSGD (momentum 0.9, wd 5e-5) on the hand-written gfx950 kernel,
+  bucketed RCCL all-reduce overlapped with backward; 512 images per GPU (weak scaling);
+* ``gpt2_pp``: GPT-2 medium (seq 1024, bf16, FusedAdam), pipeline parallel over
+  RCCL P2P -- ``pp2`` at 2 GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1
+  GPU (a pipeline needs two stages); 16 sequences per GPU (weak scaling), 4-sequence
+  microbatches.
+
+Synthetic data and random init (no network on the box).  ``--model resnet50`` /
+``--model gpt2-medium`` run one half only.  Without a launcher environment the
+process still joins a world-1 RCCL group (``--no-pg`` disables it), so the 1-GPU
+number is taken on the same communicator / reducer path as the 8-GPU one.
 
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -38,8 +46,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "gpt2-medium"])
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50) / global batch (gpt2)")
+    ap.add_argument("--model", default="all", choices=["all", "resnet50", "gpt2-medium"])
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
+    ap.add_argument("--gpt2-batch-per-gpu", type=int, default=16, help="GPT-2 sequences per GPU (global = this x N)")
+    ap.add_argument("--gpt2-config", default="gpt2-medium", help="GPT-2 size (gpt2-tiny for CPU harness tests)")
+    ap.add_argument("--gpt2-mb", type=int, default=4, help="GPT-2 sequences per pipeline microbatch")
+    ap.add_argument("--gpt2-steps", type=int, default=None, help="GPT-2 timed steps (default: --steps)")
+    ap.add_argument("--gpt2-warmup", type=int, default=None, help="GPT-2 warmup steps (default: --warmup)")
+    ap.add_argument("--schedule", default=None, help="pipeline schedule override (gpipe | 1f1b | interleaved)")
+    ap.add_argument("--no-pg", action="store_true", help="no world-1 process group when run without a launcher")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--channels-last", type=int, default=1)
@@ -108,9 +123,22 @@ def bench_resnet(args, world, rank):
         loss = step()
     _sync_all()
     dt = time.perf_counter() - t0
-    return dt, per_gpu * world, {"warmup_s": round(t0 - tw, 1), "model": "resnet50", "global_batch": per_gpu * world, "per_gpu_batch": per_gpu,
-                                 "seq_len": None, "image": [3, args.image_size, args.image_size], "parallelism": f"dp{world}",
-                                 "optimizer": "FusedSGD(momentum=0.9)", "loss": float(loss.detach())}
+    out = (dt, per_gpu * world, {"warmup_s": round(t0 - tw, 1), "model": "resnet50", "global_batch": per_gpu * world,
+                                 "per_gpu_batch": per_gpu, "seq_len": None,
+                                 "image": [3, args.image_size, args.image_size], "parallelism": f"dp{world}",
+                                 "optimizer": "FusedSGD(momentum=0.9)", "loss": float(loss.detach()),
+                                 "process_group": dist.get_backend() if dist.is_initialized() else None})
+    dmodel.remove_hooks()
+    return out
+
+
+def gpt2_layout(world: int):
+    """(strategy, pp stages, parallelism label) of the GPT-2 half at ``world`` GPUs."""
+    if world == 1:
+        return "dp", 1, "dp1"
+    stages = 4 if world % 4 == 0 else (2 if world % 2 == 0 else world)
+    dp = world // stages
+    return "pp", stages, (f"pp{stages}" if dp == 1 else f"dp{dp}xpp{stages}")
 
 
 def bench_gpt2(args, world, rank):
@@ -118,35 +146,69 @@ def bench_gpt2(args, world, rank):
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.optim import FusedAdam
 
-    cfg = gpt2_config("gpt2-medium")
-    gbatch = args.batch or 8 * max(world, 1)
+    cfg = gpt2_config(args.gpt2_config)
+    gbatch = args.gpt2_batch_per_gpu * world
+    strategy, stages, par = gpt2_layout(world)
+    dp = world // stages
+    per_replica = gbatch // dp
+    micro = args.microbatches or (max(per_replica // args.gpt2_mb, 1) if stages > 1 else None)
     torch.manual_seed(0)
     model = GPT2(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
-    stages = min(4, world)
-    strategy = "pp" if world > 1 else "dp"
-    engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if world > 1 else None,
-                                   microbatches=args.microbatches)
+    kw = {}
+    if args.schedule:
+        kw["schedule"] = args.schedule
+    engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if stages > 1 else None,
+                                   microbatches=micro, checkpointing="none", **kw)
     dev = madnn.device()
-    ids, _ = madnn.data.synthetic_batch("tokens", gbatch, dev, seq_len=args.seq_len, vocab=cfg.vocab_size)
+    # every dp replica draws its own token batch; pipeline stages of one replica share it
+    g = torch.Generator(device="cpu").manual_seed(4321 + (rank // stages))
+    ids = torch.randint(0, cfg.vocab_size, (per_replica if stages > 1 else gbatch // world, args.seq_len),
+                        generator=g).to(dev)
 
     def step():
         loss = engine.train_step(ids, ids)
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
+    steps = args.gpt2_steps or args.steps
+    warm = args.warmup if args.gpt2_warmup is None else args.gpt2_warmup
+    for _ in range(warm):
         step()
     _sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     _sync_all()
     dt = time.perf_counter() - t0
-    par = f"pp{stages}" if strategy == "pp" and world == stages else (f"dp{world // stages}xpp{stages}"
-                                                                     if strategy == "pp" else f"dp{world}")
-    return dt, gbatch, {"model": "gpt2-medium", "global_batch": gbatch, "seq_len": args.seq_len,
-                        "parallelism": par, "optimizer": "FusedAdam", "loss": float(loss.detach()) if loss is not None else None}
+    lv = None
+    if loss is not None and (stages == 1 or rank % stages == stages - 1):
+        lv = float(loss.detach())
+    info = {"model": args.gpt2_config, "global_batch": gbatch, "per_gpu_batch": args.gpt2_batch_per_gpu,
+            "seq_len": args.seq_len, "parallelism": par, "microbatches": micro if stages > 1 else 1,
+            "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
+            "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "loss_last_stage": lv}
+    return dt, steps, gbatch, info
+
+
+def _max_over_ranks(dt: float) -> float:
+    import madnn
+
+    t = torch.tensor([dt], dtype=torch.float64, device=madnn.device())
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _release(*objs):
+    import gc
+
+    for o in objs:
+        del o
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
 
 def main():
@@ -154,37 +216,56 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if not args.no_pg and "RANK" not in os.environ:
+        # no launcher: join a world-1 group anyway (same RCCL path as the N-GPU run)
+        from madnn.launch import _free_port
+
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=os.environ.get("MASTER_PORT") or str(_free_port()))
     import madnn
 
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
     madnn.init(device=args.device, backend=args.backend)
     rank = madnn.get_rank()
-    if args.model == "resnet50":
+    on_gpu = madnn.device().type == "cuda"
+    res = None
+    if args.model in ("all", "resnet50"):
         dt, samples_per_step, config = bench_resnet(args, world, rank)
-    else:
-        dt, samples_per_step, config = bench_gpt2(args, world, rank)
-    t = torch.tensor([dt], dtype=torch.float64, device=madnn.device())
-    if dist.is_initialized():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    ms = dt / args.steps * 1000.0
-    value = samples_per_step * args.steps / dt
-    res = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "samples/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms, 3),
-        "higher_is_better": True,
-        "scaling": "weak" if args.model == "resnet50" else "strong",
-        "vs_baseline": None,
-        "dtype": "bf16" if madnn.device().type == "cuda" else "fp32",
-        "data": "synthetic (random ImageNet-shaped images, random-init weights)" if args.model == "resnet50"
-        else "synthetic (random tokens, random-init weights)",
-        "config": config,
-    }
+        dt = _max_over_ranks(dt)
+        res = {
+            "metric": METRIC,
+            "value": round(samples_per_step * args.steps / dt, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1000.0, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if on_gpu else "fp32",
+            "data": "synthetic (random ImageNet-shaped images / random tokens, random-init weights)",
+            "config": config,
+        }
+        _release()
+    if args.model in ("all", "gpt2-medium"):
+        if args.model == "all":
+            import gc
+
+            gc.collect()
+        dt, steps, gbatch, info = bench_gpt2(args, world, rank)
+        dt = _max_over_ranks(dt)
+        sps = gbatch * steps / dt
+        g = dict(info, samples_per_s=round(sps, 2), tokens_per_s=round(sps * args.seq_len, 1),
+                 ms_per_step=round(dt / steps * 1000.0, 3), n_gpus=world, scaling="weak",
+                 dtype="bf16" if on_gpu else "fp32", data="synthetic (random tokens, random-init weights)")
+        if res is None:
+            res = {"metric": METRIC, "value": round(sps, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
+                   "warmup": info["warmup"], "ms_per_step": g["ms_per_step"], "higher_is_better": True,
+                   "scaling": "weak", "vs_baseline": None, "dtype": g["dtype"], "data": g["data"],
+                   "config": {"model": args.gpt2_config, "global_batch": gbatch, "seq_len": args.seq_len,
+                              "parallelism": info["parallelism"]}}
+        res["gpt2_pp"] = g
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

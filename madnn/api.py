@@ -28,7 +28,7 @@ from torch import nn
 from . import comm, ops
 from . import runtime as rt
 from .config import Config, torch_dtype
-from .parallel.dp import DataParallel, default_sync_period
+from .parallel.dp import DataParallel, default_sync_period, robustness_tick
 from .parallel.flat import FlatParamSpace
 from .utils.logging import get_logger
 
@@ -103,6 +103,7 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
     if strategy is not None:
         cfg.strategy = strategy
     rt.init(timeout_s=cfg.timeout_s)
+    apply_debug_flags(cfg)
     device = rt.device()
     strat = cfg.strategy
     plan = None
@@ -134,6 +135,19 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
         return model, optimizer
     engine, optimizer = _distribute_dp(model, optimizer, cfg, device, loss_fn=loss_fn, plan=plan)
     return engine, optimizer
+
+
+def apply_debug_flags(cfg: Config) -> None:
+    """Wire the debug/robustness switches of ``cfg`` into the subsystems that implement them:
+    ``debug_shapes`` (reference ``printDims``, nodemodule.lua:3) turns on the per-layer shape
+    trace of the tensor-parallel layers; ``check_collectives`` turns on the collective-order
+    fingerprint that the engines compare across ranks every ``MADNN_CHECK_EVERY`` steps."""
+    from .parallel.tp import set_debug_shapes
+
+    if cfg.debug_shapes:
+        set_debug_shapes(True)
+    if cfg.check_collectives and not comm.order_check_enabled():
+        comm.enable_order_check(True)
 
 
 def enable_checkpointing(module: nn.Module) -> None:
@@ -215,33 +229,48 @@ def _after_plain_step(engine: DataParallel):
 # --------------------------------------------------------------------------
 # Reference-compatible surface
 # --------------------------------------------------------------------------
+def _flat_collective(tensors, op: str, group=None, src: int = 0, scale: float = 1.0) -> int:
+    """One collective per (device, dtype) class of ``tensors``: K4 pack into an fp32 flat
+    buffer, the collective chosen by the selector (R9), K4 unpack with ``scale`` fused.
+    Returns the number of collectives issued."""
+    classes = {}
+    for t in tensors:
+        if t is not None:
+            classes.setdefault((t.device, t.dtype), []).append(t)
+    n_calls = 0
+    for (dev, dt), ts in sorted(classes.items(), key=lambda kv: (str(kv[0][0]), str(kv[0][1]))):
+        offs, n = [], 0
+        for t in ts:
+            offs.append(n)
+            n += (t.numel() + 15) // 16 * 16
+        flat = torch.zeros(n, dtype=torch.float64 if dt == torch.float64 else torch.float32, device=dev)
+        ops.bucket_pack(ts, flat, offs, 1.0)
+        coll = comm.select(flat, op, group)
+        if op == "broadcast":
+            coll(flat, src=src, group=group)
+        else:
+            coll(flat, "sum", group=group)
+        ops.bucket_unpack(ts, flat, offs, scale)
+        n_calls += 1
+    return n_calls
+
+
 def synchronize_model(model: nn.Module, group=None, params: bool = True, grads: bool = True) -> None:
     """Average every parameter and gradient across ranks (R10, datamodule.lua:211-224).
 
-    Bucketed: one K4 pack, one all-reduce and one K4 unpack (1/W fused) per
-    (device, dtype) class instead of one blocking collective per tensor.
-    """
-    world = rt.get_world_size(group)
-    if world == 1:
+    Bucketed: one K4 pack, one all-reduce (through the collective selector, R9) and one
+    K4 unpack (1/W fused) per (device, dtype) class instead of one blocking collective per
+    tensor."""
+    if comm._local(group):
         return
+    world = rt.get_world_size(group)
     if isinstance(model, DataParallel):
         model = model.module
     with torch.no_grad():
-        for kind in (("params",) if params else ()) + (("grads",) if grads else ()):
-            tensors = [p if kind == "params" else p.grad for p in model.parameters()]
-            tensors = [t for t in tensors if t is not None]
-            classes = {}
-            for t in tensors:
-                classes.setdefault((t.device, t.dtype), []).append(t)
-            for (dev, dt), ts in sorted(classes.items(), key=lambda kv: (str(kv[0][0]), str(kv[0][1]))):
-                offs, n = [], 0
-                for t in ts:
-                    offs.append(n)
-                    n += (t.numel() + 15) // 16 * 16
-                flat = torch.zeros(n, dtype=torch.float32, device=dev)
-                ops.bucket_pack(ts, flat, offs, 1.0)
-                comm.all_reduce(flat, "sum", group=group)
-                ops.bucket_unpack(ts, flat, offs, 1.0 / world)
+        if params:
+            _flat_collective(list(model.parameters()), "all_reduce", group, scale=1.0 / world)
+        if grads:
+            _flat_collective([p.grad for p in model.parameters()], "all_reduce", group, scale=1.0 / world)
 
 
 class _PeriodicSync:
@@ -305,10 +334,13 @@ def parallelize(data, targets, model: nn.Module, size: Optional[int] = None, syn
     if size is None:
         size = len(data)
     with torch.no_grad():
-        if rt.get_world_size(group) > 1:
-            for p in model.parameters():
-                comm.broadcast(p.data, src=0, group=group)
-            for b in model.buffers():
+        # bucketed broadcast of the initial parameters and buffers (reference
+        # synchronizeParameters, datamodule.lua:33, sent one tensor at a time)
+        _flat_collective([p.data for p in model.parameters()] + [b for b in model.buffers()
+                                                                 if b.is_floating_point()],
+                         "broadcast", group, src=0)
+        for b in model.buffers():
+            if not b.is_floating_point():
                 comm.broadcast(b, src=0, group=group)
     from .data import shard
 
@@ -351,6 +383,7 @@ class Trainer:
             optimizer = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=learning_rate)
         self.optimizer = optimizer
         self.history = []
+        self.global_step = 0
         self.meter = None
         if metrics_path:  # per-step JSONL metrics
             from .utils.metrics import StepMeter
@@ -382,6 +415,11 @@ class Trainer:
                 loss = self.criterion(out, y)
                 loss.backward()
                 self.optimizer.step()
+                self.global_step += 1
+                if not hasattr(self.model, "after_step"):
+                    # engines tick in their own after_step; a parallelize()-synchronised model
+                    # gets the fault-injection / order-check hooks here
+                    robustness_tick(self.global_step)
                 if self.meter is not None:
                     self.meter.stop(loss, epoch=epoch + 1, lr=lr)
                 tot += float(loss.detach()) * len(idx)

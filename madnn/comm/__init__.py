@@ -25,9 +25,20 @@ _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 _checker = {"on": os.environ.get("MADNN_CHECK_COLLECTIVES", "0") == "1", "hash": None}
 
 
-def enable_order_check(on: bool = True) -> None:
+def enable_order_check(on: bool = True, every: Optional[int] = None) -> None:
     _checker["on"] = on
     _checker["hash"] = None
+    if every is not None:
+        _checker["every"] = int(every)
+
+
+def order_check_enabled() -> bool:
+    return _checker["on"]
+
+
+def check_every() -> int:
+    """Steps between two cross-rank fingerprint comparisons (``MADNN_CHECK_EVERY``, default 50)."""
+    return _checker.get("every") or int(os.environ.get("MADNN_CHECK_EVERY", "50"))
 
 
 def _record(op: str, group, t: Optional[torch.Tensor]):
@@ -66,35 +77,71 @@ def device_kind(t: torch.Tensor) -> str:
     return "gpu" if t.device.type == "cuda" else "cpu"
 
 
-def select(t: torch.Tensor, op: str, group=None) -> Callable:
-    """Collective selector (R9): returns a callable bound to the right backend.
+class Selected:
+    """What :func:`select` chose for one tensor: the bound collective and the path label
+    ``(device kind, transport)`` -- ``("gpu", "rccl")``, ``("gpu", "gloo-host")`` or
+    ``("cpu", "gloo")`` -- mirroring the reference's ``collectiveSelector[dev][topo][sync]``
+    table lookup (datamodule.lua:199-208)."""
 
-    The reference keys on [cpu|gpu][singlenode|multinode][sync][op]; on a single
-    MI355X node the topology axis collapses (all peers are xGMI), and the
-    backend is fixed by the tensor's device.
-    """
+    __slots__ = ("fn", "device", "transport", "op")
+
+    def __init__(self, fn, device, transport, op):
+        self.fn, self.device, self.transport, self.op = fn, device, transport, op
+
+    def __call__(self, *args, **kwargs):
+        return self.fn(*args, **kwargs)
+
+    def __repr__(self):
+        return f"Selected({self.op}, {self.device}/{self.transport})"
+
+
+def select(t: torch.Tensor, op: str, group=None) -> Selected:
+    """Collective selector (R9): the implementation for ``op`` on ``t`` over ``group``.
+
+    The reference keys on [cpu|gpu][singlenode|multinode][sync][op]; on one MI355X node the
+    topology axis collapses (all 8 GPUs are xGMI peers) and the transport follows from the
+    tensor's device and the group's backend: HIP tensors on an RCCL ("nccl") group travel
+    over xGMI; HIP tensors on a gloo group (several ranks sharing one GPU in tests) are
+    staged through host memory by gloo; host tensors go to gloo.  A host tensor on an RCCL
+    group is refused (RCCL cannot move it).  Without a process group the returned callable
+    is the local no-op of every collective."""
     if op not in _OPS:
         raise KeyError(f"unknown collective {op!r}")
-    if not dist.is_initialized():
-        return lambda *a, **k: None
-    be = dist.get_backend(group)
+    fn = {"all_reduce": all_reduce, "broadcast": broadcast, "all_gather": all_gather_into,
+          "reduce_scatter": reduce_scatter, "send": send, "recv": recv, "barrier": None}[op]
     kind = device_kind(t)
-    if kind == "gpu" and be not in ("nccl",):
-        raise RuntimeError(f"device tensor on backend {be}: madnn routes HIP tensors to RCCL ('nccl')")
+    if not dist.is_initialized():
+        return Selected(fn or (lambda *a, **k: None), kind, "local", op)
+    be = dist.get_backend(group)
     if kind == "cpu" and be == "nccl":
         raise RuntimeError("CPU tensor on an RCCL group: use a gloo group for host tensors")
-    fn = {"all_reduce": all_reduce, "broadcast": broadcast, "all_gather": all_gather_into,
-          "reduce_scatter": reduce_scatter, "send": send, "recv": recv}.get(op)
-    return fn
+    transport = "rccl" if be == "nccl" else ("gloo-host" if kind == "gpu" else "gloo")
+    if fn is None:
+        from .. import runtime as rt
+
+        fn = lambda *a, **k: rt.barrier(group)  # noqa: E731
+    return Selected(fn, kind, transport, op)
+
+
+def _local(group) -> bool:
+    """True when a collective over ``group`` needs no communication at all: there is no
+    process group, or ``group`` is a singleton SUB-group of a larger world (e.g. the pp
+    axis of a pure-DP mesh).  The WORLD group is never local, even at world size 1: a
+    launched world-1 job (``torch.distributed.run --nproc-per-node 1``) issues its
+    RCCL collectives exactly like the 8-GPU job does, so the communicator setup and
+    the reducer's stream/event protocol run on the 1-GPU box too."""
+    if not dist.is_initialized():
+        return True
+    return group is not None and group is not dist.group.WORLD and dist.get_world_size(group) == 1
 
 
 def all_reduce(t: torch.Tensor, op: str = "sum", group=None, async_op: bool = False):
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if _local(group):
         return None
     _record("all_reduce", group, t)
     rop = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX}[op]
     if rop == dist.ReduceOp.AVG and dist.get_backend(group) == "gloo":
-        w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=False)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=False)
         t.div_(dist.get_world_size(group))
         return None
     return dist.all_reduce(t, op=rop, group=group, async_op=async_op)
@@ -102,7 +149,7 @@ def all_reduce(t: torch.Tensor, op: str = "sum", group=None, async_op: bool = Fa
 
 def broadcast(t: torch.Tensor, src: int = 0, group=None, async_op: bool = False):
     """Broadcast from global rank ``src`` (reference synchronizeParameters, datamodule.lua:33)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if _local(group):
         return None
     _record("broadcast", group, t)
     return dist.broadcast(t, src=src, group=group, async_op=async_op)
@@ -110,7 +157,7 @@ def broadcast(t: torch.Tensor, src: int = 0, group=None, async_op: bool = False)
 
 def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """out = cat over ranks of inp along dim 0 (reference allgatherTensor, nodemodule.lua:166,266)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if _local(group):
         out.copy_(inp.reshape(out.shape))
         return None
     _record("all_gather", group, inp)
@@ -118,7 +165,7 @@ def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: 
 
 
 def reduce_scatter(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if _local(group):
         out.copy_(inp.reshape(out.shape))
         return None
     _record("reduce_scatter", group, inp)

@@ -28,8 +28,42 @@ def kernels_path() -> Path:
     return _KERNELS
 
 
+class StaleKernelsError(RuntimeError):
+    """The in-tree kernel library was built from different sources than the tree holds."""
+
+
+def check_fresh(rebuild: bool = True) -> None:
+    """Stale-binary guard: compare the build manifest's source digests with the sources.
+
+    On a mismatch the library is rebuilt in-tree when ``rebuild`` and hipcc is present;
+    otherwise (or if the rebuild leaves it stale) :class:`StaleKernelsError` names the
+    changed sources -- an edited kernel never silently runs its old binary.
+    ``MADNN_ALLOW_STALE=1`` skips the check (debugging a deliberately old binary)."""
+    if os.environ.get("MADNN_ALLOW_STALE", "0") == "1":
+        return
+    from . import build as _b
+
+    stale = _b.stale_sources()
+    if not stale:
+        return
+    if rebuild:
+        try:
+            _b._hipcc()
+        except RuntimeError:
+            rebuild = False
+    if rebuild:
+        import sys
+
+        print(f"[madnn] kernel library is stale ({', '.join(stale)}); rebuilding in-tree", file=sys.stderr)
+        _b.build()
+        stale = _b.stale_sources()
+    if stale:
+        raise StaleKernelsError(f"madnn: {_KERNELS.name} was built from other sources than the tree holds "
+                                f"(changed: {', '.join(stale)}); run `python -m madnn.ops.build`")
+
+
 def load_kernels(build_if_missing: bool = True) -> bool:
-    """Load the HIP kernel library (building it in-tree if absent and hipcc exists)."""
+    """Load the HIP kernel library (building it in-tree if absent or stale and hipcc exists)."""
     with _lock:
         if _loaded["kernels"]:
             return True
@@ -38,9 +72,12 @@ def load_kernels(build_if_missing: bool = True) -> bool:
                 from .build import build
 
                 build()
+            check_fresh(rebuild=build_if_missing)
             torch.ops.load_library(str(_KERNELS))
             _loaded["kernels"] = True
             _loaded["error"] = None
+        except StaleKernelsError:
+            raise
         except Exception as e:  # noqa: BLE001
             _loaded["error"] = e
         return _loaded["kernels"]

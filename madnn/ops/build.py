@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -29,6 +30,8 @@ CSRC = HERE / "csrc"
 BUILD = HERE / "_build"
 KERNELS_SO = HERE / "_madnn_kernels.so"
 RUNTIME_SO = HERE / "_madnn_runtime.so"
+# source digests the shipped .so files were linked from (stale-binary guard, see stale_sources)
+MANIFEST = HERE / "_madnn_build_manifest.json"
 
 ARCH = os.environ.get("MADNN_OFFLOAD_ARCH", "gfx950")
 KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "pool.hip", "attn.hip", "conv.hip",
@@ -74,6 +77,34 @@ def _digest(paths, flags) -> str:
         h.update(Path(p).read_bytes())
     h.update(" ".join(flags).encode())
     return h.hexdigest()[:16]
+
+
+def source_digests(csrc: Path = CSRC) -> dict:
+    """sha256[:16] of every native source and header (what a built .so depends on)."""
+    out = {}
+    for name in KERNEL_SOURCES + RUNTIME_SOURCES + sorted(p.name for p in csrc.glob("*.h")):
+        f = csrc / name
+        if f.exists():
+            out[name] = hashlib.sha256(f.read_bytes()).hexdigest()[:16]
+    return out
+
+
+def write_manifest(csrc: Path = CSRC, path: Path = MANIFEST) -> None:
+    path.write_text(json.dumps({"arch": ARCH, "sources": source_digests(csrc)}, indent=1, sort_keys=True))
+
+
+def stale_sources(csrc: Path = CSRC, path: Path = MANIFEST) -> list:
+    """Sources whose current content differs from what the shipped .so was built from
+    (every source if there is no manifest).  Empty list = the binary matches the tree."""
+    cur = source_digests(csrc)
+    try:
+        built = json.loads(Path(path).read_text())
+    except (OSError, ValueError):
+        return sorted(cur)
+    if built.get("arch") != ARCH:
+        return sorted(cur)
+    old = built.get("sources", {})
+    return sorted(n for n in set(cur) | set(old) if cur.get(n) != old.get(n))
 
 
 def _compile(src: Path, obj: Path, cmd_prefix, flags, verbose: bool):
@@ -130,6 +161,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"link failed: {RUNTIME_SO.name}\n{res.stdout}\n{res.stderr}")
+    if changed or not MANIFEST.exists() or stale_sources():
+        write_manifest()
     return {"kernels": str(KERNELS_SO), "runtime": str(RUNTIME_SO), "arch": ARCH}
 
 

@@ -38,7 +38,7 @@ def bucket_pack(tensors: Sequence[torch.Tensor], flat: torch.Tensor, offsets: Se
     for t, off in zip(tensors, offsets):
         n = t.numel()
         v = _flat_view(t)
-        flat[off:off + n].copy_(v.to(torch.float32).mul(scale) if scale != 1.0 else v)
+        flat[off:off + n].copy_(v.to(flat.dtype).mul(scale) if scale != 1.0 else v)
 
 
 def bucket_unpack(tensors: Sequence[torch.Tensor], flat: torch.Tensor, offsets: Sequence[int], scale: float = 1.0):
@@ -46,7 +46,7 @@ def bucket_unpack(tensors: Sequence[torch.Tensor], flat: torch.Tensor, offsets: 
         n = t.numel()
         src = flat[off:off + n]
         if scale != 1.0:
-            src = src.to(torch.float32).mul(scale)
+            src = src.to(torch.promote_types(src.dtype, torch.float32)).mul(scale)
         if t.is_contiguous():
             t.view(-1).copy_(src)
         else:

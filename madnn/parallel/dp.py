@@ -44,6 +44,23 @@ def default_sync_period(local_size: int) -> int:
     return 100
 
 
+def robustness_tick(step: int, group=None) -> None:
+    """Per-optimizer-step robustness hooks shared by every engine and the Trainer:
+
+    * ``MADNN_FAULT=rank:step:kind`` fault injection (``utils.fault``), used by the tests that
+      prove a hung or crashed rank becomes a process-group timeout and a launcher teardown;
+    * with ``check_collectives`` on (``Config.check_collectives`` / ``MADNN_CHECK_COLLECTIVES=1``),
+      every ``MADNN_CHECK_EVERY`` (default 50) steps all ranks compare the running fingerprint
+      of their collective sequence and raise on divergence."""
+    from ..utils.fault import maybe_fail
+
+    maybe_fail(step)
+    if comm.order_check_enabled():
+        every = comm.check_every()
+        if every > 0 and step % every == 0:
+            comm.verify_order(group)
+
+
 def _cast_inputs(obj, dtype, channels_last):
     if isinstance(obj, torch.Tensor):
         if obj.is_floating_point() and dtype is not None and obj.dtype != dtype:
@@ -103,8 +120,10 @@ class DataParallel(nn.Module):
     # ---------------------------------------------------------------- setup
     @torch.no_grad()
     def broadcast_state(self, buffers: bool = True):
-        """Identical start on every replica (fixes SURVEY A-6: always broadcast)."""
-        if self.world == 1:
+        """Identical start on every replica (fixes SURVEY A-6: always broadcast).  Issued
+        whenever a process group exists -- also at world size 1 under a launcher, so the
+        RCCL broadcast path is the one the 1-GPU rehearsal exercises."""
+        if comm._local(self.group):
             return
         for bk in self.space.buckets:
             comm.broadcast(bk.master, src=self.src_rank, group=self.group)
@@ -126,6 +145,13 @@ class DataParallel(nn.Module):
                 return
             if not self._in_backward:
                 self._in_backward = True
+                if self._needs_finalize:
+                    # a second backward before the optimizer consumed the first one's reduced
+                    # gradients (plain accumulation without no_sync): p.grad now holds the local
+                    # SUM of both, so re-pack and re-reduce every bucket (torch DDP semantics:
+                    # each backward reduces).  forward() already ordered this backward's in-place
+                    # accumulation after the first reduction's packs.
+                    self._rearm()
                 torch.autograd.Variable._execution_engine.queue_callback(self._on_backward_end)
             bk.pending -= 1
             if bk.pending == 0 and not bk.launched:
@@ -171,10 +197,8 @@ class DataParallel(nn.Module):
                 self._launch(bk)
         self._needs_finalize = True
 
-    def finalize_grads(self):
-        """Make the current stream wait for every bucket's reduction (idempotent)."""
-        if not self._needs_finalize:
-            return
+    def _wait_works(self, record_end: bool = False):
+        """The current stream waits for every outstanding bucket reduction; buckets re-armed."""
         cur = torch.cuda.current_stream() if self.is_cuda else None
         if self.comm_stream is not None:
             with torch.cuda.stream(self.comm_stream):
@@ -182,7 +206,7 @@ class DataParallel(nn.Module):
                     if bk.work is not None:
                         bk.work.wait()  # comm stream waits for the collective
                         bk.work = None
-                if "comm_start" in self._ev:
+                if record_end and "comm_start" in self._ev:
                     self._ev["comm_end"] = torch.cuda.Event(enable_timing=True)
                     self._ev["comm_end"].record(self.comm_stream)
             cur.wait_stream(self.comm_stream)
@@ -192,6 +216,18 @@ class DataParallel(nn.Module):
                 bk.work = None
             bk.launched = False
             bk.pending = len(bk.params)
+        return cur
+
+    def _rearm(self):
+        self._wait_works()
+        self._needs_finalize = False
+        self.stats["rearmed"] = self.stats.get("rearmed", 0) + 1
+
+    def finalize_grads(self):
+        """Make the current stream wait for every bucket's reduction (idempotent)."""
+        if not self._needs_finalize:
+            return
+        cur = self._wait_works(record_end=True)
         if self.is_cuda and "bwd_end" in self._ev:
             self._ev["final"] = torch.cuda.Event(enable_timing=True)
             self._ev["final"].record(cur)
@@ -226,15 +262,17 @@ class DataParallel(nn.Module):
         return out
 
     def after_step(self):
-        """Called by the fused optimizer after each step (sync="params" period)."""
+        """Called by the fused optimizer after each step: the sync="params" period, then the
+        robustness hooks (fault injection, collective-order check)."""
         self._steps += 1
         if self.sync == "params" and self._steps % self.sync_every == 0:
             self.average_parameters()
+        robustness_tick(self._steps, self.group)
 
     @torch.no_grad()
     def average_parameters(self):
         """Reference periodic model averaging (datamodule.lua:214-218), bucketed."""
-        if self.world == 1:
+        if comm._local(self.group):
             return
         for bk in self.space.buckets:
             comm.all_reduce(bk.master, "sum", group=self.group)
@@ -243,6 +281,10 @@ class DataParallel(nn.Module):
 
     # -------------------------------------------------------------- forward
     def forward(self, *args, **kwargs):
+        if self._needs_finalize and self.comm_stream is not None:
+            # gradients are about to be accumulated again before the optimizer ran: the next
+            # backward's in-place adds into p.grad must follow the packs still reading it
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
         if self.cast_dtype is not None or self.channels_last:
             args = _cast_inputs(args, self.cast_dtype, self.channels_last)
             kwargs = _cast_inputs(kwargs, self.cast_dtype, self.channels_last)

@@ -29,12 +29,22 @@ def is_initialized() -> bool:
     return _STATE["initialized"]
 
 
+def launched() -> bool:
+    """True when a launcher (``torch.distributed.run``, ``madnn.launch``, bench.py) set up a
+    rendezvous environment: RANK, WORLD_SIZE and MASTER_ADDR are all present."""
+    return all(k in os.environ for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR"))
+
+
 def init(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[str] = None) -> None:
     """Bind this process to its GPU and join the process group (idempotent).
 
     Reads the torchrun / ``madnn.launch`` environment (RANK, WORLD_SIZE,
-    LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  A process started without a
-    launcher is a world of one and creates no process group.
+    LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Under a launcher the process group
+    is created even for a world of ONE, so the RCCL communicator setup, the
+    reducer's all-reduce/broadcast and the device barrier run exactly as they do
+    at 8 GPUs (``torch.distributed.run --nproc-per-node 1`` is the 1-GPU rehearsal
+    of the 8-GPU path).  A plain ``python script.py`` without a launcher
+    environment is a world of one with no process group.
     """
     if _STATE["initialized"]:
         return
@@ -51,7 +61,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0, device: Option
     else:
         dev = torch.device("cpu")
     backend = backend or ("nccl" if use_gpu else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or launched()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
@@ -95,12 +105,26 @@ def backend() -> str:
     return _STATE["backend"]
 
 
-def barrier(group=None) -> None:
-    """Global barrier (reference ``mpi.barrier()``, datamodule.lua:50)."""
+def barrier(group=None, monitored: Optional[bool] = None, timeout_s: Optional[float] = None) -> None:
+    """Global barrier (reference ``mpi.barrier()``, datamodule.lua:50).
+
+    RCCL groups barrier on this rank's device.  gloo groups use
+    ``monitored_barrier``: a rank that never arrives is NAMED in
+    the error raised on rank 0 instead of every rank hanging silently.  Set
+    ``monitored=False`` (or ``MADNN_MONITORED_BARRIER=0``) for a plain barrier."""
     if not dist.is_initialized():
         return
-    if dist.get_backend(group) == "nccl":
+    be = dist.get_backend(group)
+    if be == "nccl":
         dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+        return
+    if monitored is None:
+        monitored = os.environ.get("MADNN_MONITORED_BARRIER", "1") != "0"
+    if monitored and be == "gloo":
+        kw = {}
+        if timeout_s is not None:
+            kw["timeout"] = datetime.timedelta(seconds=timeout_s)
+        dist.monitored_barrier(group=group, wait_all_ranks=True, **kw)
     else:
         dist.barrier(group=group)
 

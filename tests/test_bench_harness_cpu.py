@@ -19,7 +19,8 @@ def test_bench_py_two_ranks_cpu():
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--device", "cpu", "--batch", "2", "--image-size", "32"]
+           "--device", "cpu", "--batch", "2", "--image-size", "32", "--gpt2-config", "gpt2-tiny", "--seq-len", "32",
+           "--gpt2-batch-per-gpu", "4", "--gpt2-mb", "2"]
     env = dict(os.environ, OMP_NUM_THREADS="2", MADNN_LOG_LEVEL="WARNING")
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -32,6 +33,26 @@ def test_bench_py_two_ranks_cpu():
     assert res["n_gpus"] == 2 and res["steps"] == 2 and res["config"]["global_batch"] == 4
     assert res["config"]["parallelism"] == "dp2" and res["value"] > 0
     assert abs(res["value"] - 4 * 2 / (res["ms_per_step"] * 2 / 1000)) / res["value"] < 0.01
+    assert res["config"]["process_group"] == "gloo"
+    # the GPT-2 pipeline half of the BASELINE metric rides in the same line
+    g = res["gpt2_pp"]
+    assert g["parallelism"] == "pp2" and g["n_gpus"] == 2 and g["global_batch"] == 8 and g["microbatches"] == 4
+    assert g["samples_per_s"] > 0 and g["tokens_per_s"] == pytest.approx(g["samples_per_s"] * 32, rel=1e-3)
+    assert abs(g["samples_per_s"] - 8 * g["steps"] / (g["ms_per_step"] * g["steps"] / 1000)) / g["samples_per_s"] < 0.01
+    assert g["loss_last_stage"] is None or g["loss_last_stage"] > 0
+
+
+def test_bench_py_single_process_joins_world1_group():
+    """No launcher: bench.py still creates a world-1 process group (gloo here, RCCL on the GPU)."""
+    cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--device", "cpu", "--batch", "2",
+           "--image-size", "32", "--gpt2-config", "gpt2-tiny", "--seq-len", "16", "--gpt2-batch-per-gpu", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", MADNN_LOG_LEVEL="WARNING")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert res["n_gpus"] == 1 and res["config"]["process_group"] == "gloo"
+    assert res["config"]["parallelism"] == "dp1" and res["gpt2_pp"]["parallelism"] == "dp1"
 
 
 def test_launcher_tears_down_on_failure():
@@ -58,12 +79,14 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1",
-           "--device", "cpu", "--model", "gpt2-medium", "--batch", "4", "--seq-len", "32", "--microbatches", "4"]
+           "--device", "cpu", "--model", "gpt2-medium", "--gpt2-batch-per-gpu", "1", "--seq-len", "32",
+           "--microbatches", "4"]
     env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING")
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     res = json.loads(lines[0])
-    assert res["n_gpus"] == 4 and res["scaling"] == "strong" and res["value"] > 0
+    assert res["n_gpus"] == 4 and res["scaling"] == "weak" and res["value"] > 0
     assert res["config"]["parallelism"] == "pp4" and res["config"]["global_batch"] == 4
+    assert res["gpt2_pp"]["microbatches"] == 4 and res["gpt2_pp"]["model"] == "gpt2-medium"

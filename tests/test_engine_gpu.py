@@ -160,6 +160,50 @@ def test_dp_two_ranks_on_device(cuda):
     run_dist(_w_dp_gpu, 2, device="cuda", backend="gloo")
 
 
+def _w_rccl_world1(rank, world):
+    import torch.distributed as dist
+
+    import madnn
+    from madnn import comm
+    from madnn import runtime as rt
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.optim import FusedAdam
+
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    groups = rt.ProcessGroups(rt.Mesh(1, 1, 1))
+    assert groups.dp_ranks == [0] and groups.pp_ranks == [0]
+    rt.barrier()  # device barrier on the RCCL group
+    sel = comm.select(torch.zeros(1, device="cuda"), "all_reduce")
+    assert (sel.device, sel.transport) == ("gpu", "rccl")
+    torch.manual_seed(0)
+    model = GPT2(gpt2_config("gpt2-tiny"))
+    ref = copy.deepcopy(model).cuda()
+    opt = FusedAdam(model.parameters(), lr=3e-3, weight_decay=0.01)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=3e-3, weight_decay=0.01)
+    dm, opt = madnn.distribute(model, opt, strategy="dp", bucket_mb=0.25)
+    assert dm.comm_stream is not None and len(dm.space.buckets) > 1
+    ids = torch.randint(0, 512, (4, 64), generator=torch.Generator().manual_seed(3)).cuda()
+    for step in range(3):
+        loss = dm.train_step(ids, ids)
+        opt.step()
+        rl = ref.loss_fn(ref(ids), ids)
+        rl.backward()
+        ropt.step()
+        ropt.zero_grad()
+        assert abs(float(loss) - float(rl)) < 3e-2 * float(rl), (step, float(loss), float(rl))
+    # every bucket went through pack -> RCCL all_reduce -> optimizer, each step
+    assert dm.stats["buckets_launched"] == 3 * len(dm.space.buckets)
+    m = dm.comm_metrics()
+    assert m["allreduce_bytes"] > 0 and m["comm_ms"] >= 0
+
+
+def test_rccl_world1_reducer_path(cuda):
+    """World-1 RCCL group (as under torch.distributed.run --nproc-per-node 1): eager device-bound
+    communicator, ProcessGroups of a 1x1x1 mesh, device barrier, and the DP reducer issuing its
+    real RCCL all-reduce per bucket from the comm stream during backward."""
+    run_dist(_w_rccl_world1, 1, device="cuda", backend="nccl")
+
+
 def test_measured_costs(cuda):
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.planner import estimate, trace
