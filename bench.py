@@ -159,7 +159,8 @@ def bench_gpt2(args, world, rank):
     if args.schedule:
         kw["schedule"] = args.schedule
     engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if stages > 1 else None,
-                                   microbatches=micro, checkpointing="none", **kw)
+                                   microbatches=micro, checkpointing="none", global_batch=gbatch,
+                                   example_input=torch.zeros(1, args.seq_len, dtype=torch.long), **kw)
     dev = madnn.device()
     # every dp replica draws its own token batch; pipeline stages of one replica share it
     g = torch.Generator(device="cpu").manual_seed(4321 + (rank // stages))

@@ -120,7 +120,8 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
             plan = None
         if plan is not None:
             strat = plan.strategy
-            get_logger().info("madnn plan: %s", plan.describe())
+            if strat == "tp":
+                cfg.tp_size = plan.tp
         else:
             strat = "dp"
     if strat in ("pp", "dp_pp"):

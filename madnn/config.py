@@ -49,7 +49,8 @@ class Config:
     # pipeline parallel
     pp_stages: Optional[int] = None
     microbatches: Optional[int] = None
-    schedule: str = "1f1b"               # gpipe | 1f1b
+    schedule: str = "1f1b"               # gpipe | 1f1b | interleaved
+    virtual_stages: Optional[int] = None  # model chunks per rank for schedule="interleaved" (None => 2)
     # tensor parallel
     tp_size: int = 1
     tp_backward: str = "allgather"
@@ -77,7 +78,7 @@ class Config:
                 continue
             cur = getattr(cfg, f.name)
             if cur is None:
-                cast = int if f.name in ("sync_every", "pp_stages", "microbatches") else str
+                cast = int if f.name in ("sync_every", "pp_stages", "microbatches", "virtual_stages") else str
                 if f.name == "channels_last":
                     cast = bool
             else:
@@ -98,7 +99,7 @@ class Config:
             raise ValueError(f"unknown strategy {self.strategy!r}")
         if self.sync not in ("grads", "params", "manual"):
             raise ValueError(f"unknown sync mode {self.sync!r}")
-        if self.schedule not in ("gpipe", "1f1b"):
+        if self.schedule not in ("gpipe", "1f1b", "interleaved"):
             raise ValueError(f"unknown pipeline schedule {self.schedule!r}")
         if self.remainder not in ("drop", "last", "pad"):
             raise ValueError(f"unknown remainder policy {self.remainder!r}")

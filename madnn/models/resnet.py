@@ -122,12 +122,36 @@ class ResNet(nn.Module):
         layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
-    def forward(self, x):
+    def stem(self, x):
         y, st = self.conv1(x, stats=True)
-        x = self.maxpool(self.bn1(y, relu=True, stats=st))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        return self.maxpool(self.bn1(y, relu=True, stats=st))
+
+    def head(self, x):
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def forward(self, x):
+        x = self.layer4(self.layer3(self.layer2(self.layer1(self.stem(x)))))
+        return self.head(x)
+
+    def pipeline_layers(self):
+        """The spine the planner costs / partitions: stem, every residual block, head."""
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        return [_Bound(self, "stem"), *blocks, _Bound(self, "head")]
+
+
+class _Bound(nn.Module):
+    """One single-tensor piece of a model's forward as a layer (shares the model's modules)."""
+
+    def __init__(self, model: nn.Module, method: str):
+        super().__init__()
+        self.parts = nn.ModuleDict({n: m for n, m in model.named_children()
+                                    if n in {"stem": ("conv1", "bn1", "maxpool"),
+                                             "head": ("avgpool", "fc")}[method]})
+        object.__setattr__(self, "_model", model)
+        self.method = method
+
+    def forward(self, x):
+        return getattr(self._model, self.method)(x)
 
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:

@@ -11,7 +11,9 @@
 //                            bucket starts on a 16-byte boundary for the K4
 //                            vector path (replaces datamodule.lua:211-224's
 //                            one-collective-per-tensor loop).
-//  * madnn_pipeline_schedule — GPipe / 1F1B action lists per stage.
+//  * madnn_pipeline_order — per-rank compute order of GPipe / 1F1B / interleaved
+//                            1F1B pipelines; the engine derives all
+//                            communication from it.
 //  * madnn_hash_*         — collective-order fingerprint used by the debug
 //                            checker to catch rank divergence.
 #include <algorithm>
@@ -94,61 +96,59 @@ int madnn_plan_buckets(const int64_t* numels, int n, int64_t cap_elems, int alig
   return b;
 }
 
-// Action encoding: op * 1'000'000 + microbatch, op 0 = forward, 1 = backward.
-// kind 0 = GPipe (all F then all B), kind 1 = 1F1B (PipeDream-flush).
-// Writes 2*M actions into out; returns the count.
-int madnn_pipeline_schedule(int kind, int stage, int nstages, int nmicro, int* out) {
+// Per-rank COMPUTE order of a (possibly interleaved) pipeline as (op, chunk, microbatch)
+// triples, op 0 = forward, 1 = backward.  Communication is not part of the order: every
+// message travels on a one-directional FIFO channel (activations r -> r+1, gradients
+// r+1 -> r, plus the two ring edges S-1 -> 0 / 0 -> S-1 of the interleaved layout), and
+// the orders below make every channel's send order equal its receive order, so the engine
+// can post receives ahead of time and never wait on a send.
+//   kind 0 GPipe: all forwards, then all backwards (V = 1).
+//   kind 1 1F1B (PipeDream-flush, V = 1): S-s-1 warm-up forwards, then F/B pairs.
+//   kind 2 interleaved 1F1B with V model chunks per rank; chunk c of rank s is virtual
+//          stage c*S + s.  Forward step k runs chunk (k mod SV) / S on microbatch
+//          (k / SV) * S + k mod S; backward step k runs chunk V-1-(k mod SV)/S on the same
+//          microbatch formula; warm-up = 2(S-s-1) + (V-1)S forwards.  Needs M % S == 0.
+// Returns the number of triples (2*M*V), or -1 on invalid arguments.
+int madnn_pipeline_order(int kind, int stage, int nstages, int nmicro, int nchunks, int* out) {
+  if (nstages <= 0 || stage < 0 || stage >= nstages || nmicro <= 0 || nchunks <= 0) return -1;
   int k = 0;
-  if (kind == 0) {
-    for (int m = 0; m < nmicro; ++m) out[k++] = m;
-    for (int m = 0; m < nmicro; ++m) out[k++] = 1000000 + m;
-    return k;
-  }
-  const int warm = std::min(nstages - stage - 1, nmicro);
-  int f = 0, b = 0;
-  for (int i = 0; i < warm; ++i) out[k++] = f++;
-  while (f < nmicro) {
-    out[k++] = f++;
-    out[k++] = 1000000 + b++;
-  }
-  while (b < nmicro) out[k++] = 1000000 + b++;
-  return k;
-}
-
-// Full per-stage pipeline PROGRAM, communication included, as (op, a, b)
-// triples.  Ops: 0 RECV_FWD m | 1 FWD m | 2 SEND_FWD m | 3 RECV_BWD m | 4 BWD m |
-// 5 SEND_BWD m | 6 SEND_FWD_RECV_BWD (send m=a, recv m=b) |
-// 7 SEND_BWD_RECV_FWD (send m=a, recv m=b).
-// 1F1B follows the non-interleaved PipeDream-flush order with the steady-state
-// send/recv pairs batched into one group, which is what keeps two adjacent
-// stages from both blocking in a send on a shared point-to-point channel.
-// Returns the number of triples written (<= 6*M: GPipe; 1F1B <= 4*M + 1).
-int madnn_pipeline_program(int kind, int stage, int nstages, int nmicro, int* out) {
-  int k = 0;
-  auto emit = [&](int op, int a, int b) {
+  auto emit = [&](int op, int c, int m) {
     out[3 * k] = op;
-    out[3 * k + 1] = a;
-    out[3 * k + 2] = b;
+    out[3 * k + 1] = c;
+    out[3 * k + 2] = m;
     ++k;
   };
-  if (kind == 0) {  // GPipe
-    for (int m = 0; m < nmicro; ++m) { emit(0, m, -1); emit(1, m, -1); emit(2, m, -1); }
-    for (int m = 0; m < nmicro; ++m) { emit(3, m, -1); emit(4, m, -1); emit(5, m, -1); }
+  if (kind == 0 || kind == 1) {
+    if (nchunks != 1) return -1;
+    if (kind == 0) {
+      for (int m = 0; m < nmicro; ++m) emit(0, 0, m);
+      for (int m = 0; m < nmicro; ++m) emit(1, 0, m);
+      return k;
+    }
+    const int warm = std::min(nstages - stage - 1, nmicro);
+    int f = 0, b = 0;
+    for (int i = 0; i < warm; ++i) emit(0, 0, f++);
+    while (f < nmicro) {
+      emit(0, 0, f++);
+      emit(1, 0, b++);
+    }
+    while (b < nmicro) emit(1, 0, b++);
     return k;
   }
-  const int warm = std::min(nstages - stage - 1, nmicro);
-  const int steady = nmicro - warm;
-  for (int i = 0; i < warm; ++i) { emit(0, i, -1); emit(1, i, -1); emit(2, i, -1); }
-  if (steady > 0) emit(0, warm, -1);
-  for (int i = 0; i < steady; ++i) {
-    const int f = warm + i;
-    emit(1, f, -1);
-    emit(6, f, i);
-    emit(4, i, -1);
-    if (i == steady - 1) emit(5, i, -1);
-    else emit(7, i, f + 1);
+  if (kind != 2 || nmicro % nstages != 0) return -1;
+  const int S = nstages, V = nchunks, SV = S * V, total = nmicro * V;
+  auto mb = [&](int step) { return (step / SV) * S + step % S; };
+  auto fchunk = [&](int step) { return (step % SV) / S; };
+  const int warm = std::min(2 * (S - stage - 1) + (V - 1) * S, total);
+  int f = 0, b = 0;
+  for (; f < warm; ++f) emit(0, fchunk(f), mb(f));
+  while (f < total) {
+    emit(0, fchunk(f), mb(f));
+    ++f;
+    emit(1, V - 1 - fchunk(b), mb(b));
+    ++b;
   }
-  for (int i = steady; i < nmicro; ++i) { emit(3, i, -1); emit(4, i, -1); emit(5, i, -1); }
+  for (; b < total; ++b) emit(1, V - 1 - fchunk(b), mb(b));
   return k;
 }
 

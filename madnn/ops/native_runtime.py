@@ -32,10 +32,8 @@ def _load():
         lib.madnn_plan_buckets.restype = I
         lib.madnn_plan_buckets.argtypes = [ctypes.POINTER(L), I, L, I, ctypes.POINTER(I), ctypes.POINTER(L),
                                            ctypes.POINTER(L)]
-        lib.madnn_pipeline_schedule.restype = I
-        lib.madnn_pipeline_schedule.argtypes = [I, I, I, I, ctypes.POINTER(I)]
-        lib.madnn_pipeline_program.restype = I
-        lib.madnn_pipeline_program.argtypes = [I, I, I, I, ctypes.POINTER(I)]
+        lib.madnn_pipeline_order.restype = I
+        lib.madnn_pipeline_order.argtypes = [I, I, I, I, I, ctypes.POINTER(I)]
         lib.madnn_hash_init.restype = U
         lib.madnn_hash_init.argtypes = []
         lib.madnn_hash_event.restype = U
@@ -77,29 +75,23 @@ def plan_buckets(numels: Sequence[int], cap_elems: int, align: int = 16):
     return list(bo)[:n], list(oo)[:n], list(bs)[:nb]
 
 
-def pipeline_schedule(kind: str, stage: int, nstages: int, nmicro: int) -> List[Tuple[str, int]]:
-    """Per-stage action list: [("F", m) | ("B", m)], GPipe or 1F1B."""
+SCHEDULE_KINDS = {"gpipe": 0, "1f1b": 1, "interleaved": 2}
+
+
+def pipeline_order(kind: str, stage: int, nstages: int, nmicro: int, nchunks: int = 1) -> List[Tuple[str, int, int]]:
+    """Per-rank compute order [("F"|"B", chunk, microbatch)] of a pipeline schedule
+    (GPipe, 1F1B, or interleaved 1F1B with ``nchunks`` model chunks per rank)."""
     lib = _load()
-    out = (ctypes.c_int * (2 * nmicro))()
-    k = lib.madnn_pipeline_schedule(0 if kind == "gpipe" else 1, stage, nstages, nmicro, out)
-    res = []
-    for v in list(out)[:k]:
-        res.append(("B", v - 1000000) if v >= 1000000 else ("F", v))
-    return res
-
-
-PROGRAM_OPS = ("RECV_FWD", "FWD", "SEND_FWD", "RECV_BWD", "BWD", "SEND_BWD", "SEND_FWD_RECV_BWD",
-               "SEND_BWD_RECV_FWD")
-
-
-def pipeline_program(kind: str, stage: int, nstages: int, nmicro: int) -> List[Tuple[str, int, int]]:
-    """Per-stage instruction list (op, a, b) including the point-to-point steps."""
-    lib = _load()
-    cap = 6 * nmicro + 8
-    out = (ctypes.c_int * (3 * cap))()
-    k = lib.madnn_pipeline_program(0 if kind == "gpipe" else 1, stage, nstages, nmicro, out)
+    if kind not in SCHEDULE_KINDS:
+        raise ValueError(f"unknown pipeline schedule {kind!r}")
+    n = 2 * nmicro * nchunks
+    out = (ctypes.c_int * (3 * n + 3))()
+    k = lib.madnn_pipeline_order(SCHEDULE_KINDS[kind], stage, nstages, nmicro, nchunks, out)
+    if k < 0:
+        raise ValueError(f"invalid pipeline order: kind={kind} stage={stage}/{nstages} microbatches={nmicro} "
+                         f"chunks={nchunks} (interleaved needs microbatches % stages == 0; gpipe/1f1b one chunk)")
     vals = list(out)[:3 * k]
-    return [(PROGRAM_OPS[vals[3 * i]], vals[3 * i + 1], vals[3 * i + 2]) for i in range(k)]
+    return [("F" if vals[3 * i] == 0 else "B", vals[3 * i + 1], vals[3 * i + 2]) for i in range(k)]
 
 
 class OrderHash:

@@ -66,16 +66,39 @@ class _FlatOptimizer(torch.optim.Optimizer):
     # -------------------------------------------------------------- clipping
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
-        """Global-norm clipping fused into the next step (device-side coefficient, no host sync)."""
+        """GLOBAL-norm clipping fused into the next step (device-side coefficient, no host sync).
+
+        The squared norm of this rank's flat gradients is summed over the groups the engine
+        names (``norm_reduction``): the pipeline group (stages hold disjoint parameters; a
+        tied parameter counts on its first owner only) and the tensor-parallel group
+        (shards count on every rank, replicated parameters on TP rank 0 only), so every rank
+        applies the coefficient torch.nn.utils.clip_grad_norm_ would on the whole model."""
         if self.space is None:
             self._bind_local()
         if self._reduced_by_engine():
             self.grad_source.finalize_grads()
         flats = [self._grads(bk) for bk in self.space.buckets]
         self._grads_cached = flats
-        out = ops.grad_norm(flats, max_norm=max_norm)
-        self._dscale = out[1:2]
-        return out[0]
+        groups, skip = ([], [])
+        if self.grad_source is not None and hasattr(self.grad_source, "norm_reduction"):
+            groups, skip = self.grad_source.norm_reduction()
+        if not groups and not skip:
+            out = ops.grad_norm(flats, max_norm=max_norm)
+            self._dscale = out[1:2]
+            return out[0]
+        sq = ops.grad_norm(flats, max_norm=0.0)[0:1].double().square()
+        for p in skip:
+            bk, off, _ = self.space.param_info[id(p)]
+            i = self.space.buckets.index(bk)
+            sq -= flats[i][off:off + p.numel()].double().square().sum()
+        sq = sq.float()
+        from .. import comm
+
+        for g in groups:
+            comm.all_reduce(sq, "sum", group=g)
+        norm = sq.clamp_min(0).sqrt()
+        self._dscale = (max_norm / (norm + 1e-6)).clamp(max=1.0)
+        return norm[0]
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -85,10 +108,23 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 loss = closure()
         if self.space is None:
             self._bind_local()
+        late = set()
+        gs = self.grad_source
         if self._reduced_by_engine():
-            self.grad_source.finalize_grads()
+            if hasattr(gs, "tied_buckets") and getattr(self, "_grads_cached", None) is None:
+                # update every other bucket while the cross-stage tied-gradient sum runs
+                gs.finalize_grads(wait_tied=False)
+                late = gs.tied_buckets()
+            else:
+                gs.finalize_grads()
         cached = getattr(self, "_grads_cached", None)
-        for i, bk in enumerate(self.space.buckets):
+        order = [i for i, bk in enumerate(self.space.buckets) if bk.index not in late] + \
+                [i for i, bk in enumerate(self.space.buckets) if bk.index in late]
+        for i in order:
+            bk = self.space.buckets[i]
+            if late and bk.index in late:
+                gs.finalize_grads()
+                late = set()
             g = cached[i] if cached is not None else self._grads(bk)
             group = self.param_groups[bk.group_id]
             self.bucket_steps[bk.index] += 1

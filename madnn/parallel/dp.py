@@ -102,6 +102,7 @@ class DataParallel(nn.Module):
             # high priority so the pack + RCCL enqueue is not starved by backward kernels
             self.comm_stream = torch.cuda.Stream(device=dev, priority=-1)
         self._sync_enabled = True
+        self.defer_flush = False
         self._in_backward = False
         self._needs_finalize = False
         self._steps = 0
@@ -186,6 +187,14 @@ class DataParallel(nn.Module):
     def _on_backward_end(self):
         self._in_backward = False
         self._backwards += 1
+        if not self.defer_flush:
+            self.flush()
+
+    def flush(self):
+        """End of the gradient-producing backward(s): launch the buckets whose parameters got
+        no gradient and mark the step for finalisation.  Runs from the autograd end callback,
+        or -- with ``defer_flush`` (the pipeline engine, whose chunks finish their last
+        microbatch at different times) -- explicitly after the LAST backward."""
         if self.is_cuda:
             self._ev["bwd_end"] = torch.cuda.Event(enable_timing=True)
             self._ev["bwd_end"].record()

@@ -1,26 +1,29 @@
-"""Pipeline-parallel engine (GPipe / 1F1B) and hybrid DP x PP over RCCL.
+"""Pipeline-parallel engine (GPipe / 1F1B / interleaved 1F1B) and hybrid DP x PP over RCCL.
 
 Not in the reference ("Pipeline parallel — No"); BASELINE
 configs 3 and 4 require it.  Design for one MI355X node:
 
 * one process per GPU; rank -> (dp, pp) coordinates from ``runtime.Mesh``;
-  the planner's stage boundaries cut the traced spine into per-rank stage
-  modules (layers on the META device are materialised only on their own
-  rank, so an 8B model never exists whole in host memory);
-* the per-stage instruction list — forward/backward AND its send/recv steps —
-  comes from the C++ scheduler (``madnn_pipeline_program``); steady-state
-  1F1B pairs (send activation / receive gradient) are issued as ONE
-  ``batch_isend_irecv`` group so adjacent stages never both block in a send;
-* activations travel as bf16 over the xGMI link between adjacent stages
-  (every pair of GPUs is one hop on the MI355X mesh); shapes are negotiated
-  once per input signature;
-* gradients of each stage are reduced over its DP group by the bucketed
-  ``DataParallel`` reducer, only during the LAST microbatch's backward
-  (``no_sync`` before), so the all-reduce overlaps that backward and travels
-  on links disjoint from the PP hops;
-* parameters shared by two stages (GPT-2's tied ``wte``/``lm_head``) get
-  their gradients summed between the owning stages before the optimizer
-  step, and are broadcast once at build time.
+  the planner's stage boundaries cut the traced spine into per-rank chunks
+  (layers on the META device are materialised only on their own rank, so an
+  8B model never exists whole in host memory);
+* the per-rank COMPUTE order comes from the C++ scheduler
+  (``madnn_pipeline_order``): GPipe, 1F1B, or interleaved 1F1B where every rank
+  holds V chunks (virtual stages c*S + rank), shrinking the bubble from
+  (S-1)/(M+S-1) toward (S-1)/(V*M+S-1);
+* communication is derived from that order over one-directional FIFO
+  channels, each its own process group (own RCCL communicator and stream):
+  activations r -> r+1 (ring edge S-1 -> 0 between chunks), gradients back.
+  Every receive of a step is posted up front and consumed with a stream wait,
+  sends are never waited on before the step ends, so the xGMI transfers run
+  underneath compute (``simulate_schedule`` proves each channel's receive
+  order equals its send order, which is what makes that legal);
+* gradients of each rank are reduced over its DP group by the bucketed
+  ``DataParallel`` reducer during each chunk's LAST microbatch backward
+  (``no_sync`` before) on links disjoint from the PP hops;
+* parameters shared by two ranks (GPT-2's tied ``wte``/``lm_head``) have
+  their gradients summed between the owners asynchronously right after the
+  last backward; the optimizer updates every other bucket first.
 """
 from __future__ import annotations
 
@@ -62,12 +65,22 @@ class StageModule(nn.Module):
 def materialize_(module: nn.Module, device, init_fn: Optional[Callable] = None, optimizer=None) -> bool:
     """Allocate META parameters/buffers of ``module`` on ``device`` and initialise them.
 
-    ``to_empty`` creates new Parameter objects; an ``optimizer`` built over the meta
-    parameters is re-pointed at them (matched by parameter name)."""
+    ``to_empty`` creates a new Parameter per module slot, which would UNTIE shared weights
+    (GPT-2's wte / lm_head); slots that shared one Parameter share the new one again.  An
+    ``optimizer`` built over the meta parameters is re-pointed at them (matched by name)."""
     if not any(t.is_meta for t in list(module.parameters()) + list(module.buffers())):
         return False
     old = {id(p): n for n, p in module.named_parameters(remove_duplicate=False)}
+    slots: Dict[int, list] = {}
+    for m in module.modules():
+        for pn, p in m._parameters.items():
+            if p is not None:
+                slots.setdefault(id(p), []).append((m, pn))
     module.to_empty(device=device)
+    for lst in slots.values():
+        keep = lst[0][0]._parameters[lst[0][1]]
+        for m, pn in lst[1:]:
+            m._parameters[pn] = keep
     with torch.no_grad():
         for m in module.modules():
             if init_fn is not None:
@@ -136,94 +149,223 @@ def restrict_optimizer(opt, params: List[nn.Parameter]):
     return type(opt)(groups, **opt.defaults)
 
 
-class P2P:
-    """Point-to-point transport between adjacent stages (global ranks)."""
+# ----------------------------------------------------------------------------
+# schedule analysis (pure Python; also used by the planner to price the bubble)
+# ----------------------------------------------------------------------------
+def virtual_stage(chunk: int, stage: int, nstages: int) -> int:
+    """Chunk ``chunk`` of pipeline rank ``stage`` is virtual stage chunk*S + stage."""
+    return chunk * nstages + stage
 
-    def __init__(self, prev: Optional[int], nxt: Optional[int], group, device):
-        self.prev, self.next, self.group, self.device = prev, nxt, group, device
-        self.pending = []
-        # RCCL moves device tensors directly over xGMI; a gloo group (CPU tier, or several
-        # ranks sharing one GPU in tests) stages device tensors through host memory.
+
+def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_fwd: float = 1.0,
+                      t_bwd: float = 2.0, t_p2p: float = 0.0) -> dict:
+    """Execute every rank's compute order (``native_runtime.pipeline_order``) against
+    one-directional FIFO channels with non-blocking sends, as the engine does.
+
+    Raises RuntimeError if the schedule deadlocks or a channel's receive order differs from
+    its send order (the property that lets the engine post receives ahead of time).  Returns
+    ``{"makespan", "bubble", "peak_inflight"}`` for per-chunk forward/backward costs
+    ``t_fwd``/``t_bwd`` and a per-message latency ``t_p2p``; ``bubble`` is the idle fraction
+    of the busiest rank (the analytic (S-1)/(M+S-1) for 1F1B, less when interleaved)."""
+    S, M, V = nstages, nmicro, nchunks
+    SV = S * V
+    orders = [native_runtime.pipeline_order(kind, s, S, M, V) for s in range(S)]
+    done: Dict[tuple, float] = {}          # (op, vs, m) -> finish time
+    sent: Dict[tuple, list] = {}           # channel -> list of messages in send order
+    recv_seq: Dict[tuple, list] = {}       # channel -> list of messages in consume order
+    pos = [0] * S
+    free = [0.0] * S
+    busy = [0.0] * S
+    live = [0] * S
+    peak = [0] * S
+
+    def chan(kind_, src_vs, dst_vs):
+        return (kind_, src_vs % S, dst_vs % S)
+
+    total = sum(len(o) for o in orders)
+    finished = 0
+    while finished < total:
+        progressed = False
+        for s in range(S):
+            while pos[s] < len(orders[s]):
+                op, c, m = orders[s][pos[s]]
+                vs = c * S + s
+                if op == "F":
+                    dep = ("F", vs - 1, m) if vs > 0 else None
+                else:
+                    dep = ("B", vs + 1, m) if vs < SV - 1 else ("F", vs, m)
+                if dep is not None and dep not in done:
+                    break
+                ready = done[dep] + (t_p2p if dep[1] != vs else 0.0) if dep is not None else 0.0
+                start = max(free[s], ready)
+                dur = t_fwd if op == "F" else t_bwd
+                free[s] = start + dur
+                busy[s] += dur
+                done[(op, vs, m)] = free[s]
+                if op == "F":
+                    live[s] += 1
+                    peak[s] = max(peak[s], live[s])
+                    if vs > 0:
+                        recv_seq.setdefault(chan("act", vs - 1, vs), []).append((vs, m))
+                    if vs < SV - 1:
+                        sent.setdefault(chan("act", vs, vs + 1), []).append((vs + 1, m))
+                else:
+                    live[s] -= 1
+                    if vs < SV - 1:
+                        recv_seq.setdefault(chan("grad", vs + 1, vs), []).append((vs, m))
+                    if vs > 0:
+                        sent.setdefault(chan("grad", vs, vs - 1), []).append((vs - 1, m))
+                pos[s] += 1
+                finished += 1
+                progressed = True
+        if not progressed:
+            stuck = {s: orders[s][pos[s]] for s in range(S) if pos[s] < len(orders[s])}
+            raise RuntimeError(f"pipeline schedule {kind} S={S} M={M} V={V} deadlocks at {stuck}")
+    for ch, msgs in sent.items():
+        if recv_seq.get(ch, []) != msgs:
+            raise RuntimeError(f"channel {ch}: receive order differs from send order")
+    makespan = max(free)
+    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan, "peak_inflight": peak}
+
+
+# ----------------------------------------------------------------------------
+# transport
+# ----------------------------------------------------------------------------
+class _Pending:
+    """A posted receive; ``get()`` orders the consumer after it (RCCL: a stream wait, no
+    host block) and returns the tensor on the compute device."""
+
+    __slots__ = ("work", "buf", "device", "staged")
+
+    def __init__(self, work, buf, device, staged):
+        self.work, self.buf, self.device, self.staged = work, buf, device, staged
+
+    def get(self) -> torch.Tensor:
+        self.work.wait()
+        return self.buf.to(self.device, non_blocking=False) if self.staged else self.buf
+
+
+class Channel:
+    """One-directional point-to-point FIFO between two pipeline ranks.
+
+    Each direction of each pipeline edge gets its OWN process group, hence its own RCCL
+    communicator and internal HIP stream, so a channel only ever carries messages one way
+    and in one order: receives can be posted ahead of time (the transfer then runs as soon
+    as the peer's send is enqueued, overlapping this rank's compute) and sends are never
+    waited on before the end of the step.  On a gloo group HIP tensors are staged through
+    host memory (tests run several ranks on one GPU that way; RCCL refuses that)."""
+
+    def __init__(self, group, src: int, dst: int, device, name: str = ""):
+        self.group, self.src, self.dst, self.name = group, src, dst, name
+        self.device = torch.device(device)
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
-        self.host_staged = backend == "gloo" and torch.device(device).type == "cuda"
-        self.buf_device = torch.device("cpu") if self.host_staged else torch.device(device)
+        self.staged = backend == "gloo" and self.device.type == "cuda"
+        self.buf_device = torch.device("cpu") if self.staged else self.device
+        self._sends = []
+        self.bytes = 0
+        self.messages = 0
 
-    def _run(self, ops):
-        if not ops:
-            return
-        reqs = dist.batch_isend_irecv(ops)
-        for r in reqs:
-            r.wait()
+    def send(self, t: torch.Tensor) -> None:
+        t = t.detach().contiguous()
+        if self.staged:
+            t = t.cpu()
+        comm._record("send", self.group, t)
+        self._sends.append((dist.isend(t, self.dst, group=self.group), t))
+        self.bytes += t.numel() * t.element_size()
+        self.messages += 1
 
-    def exchange(self, send_t=None, send_to=None, recv_shape=None, recv_dtype=None, recv_from=None):
-        ops = []
-        out = None
-        if send_t is not None and send_to is not None:
-            send_t = send_t.contiguous()
-            if self.host_staged:
-                send_t = send_t.cpu()
-            ops.append(dist.P2POp(dist.isend, send_t, send_to, self.group))
-            self.pending.append(send_t)
-        if recv_shape is not None and recv_from is not None:
-            out = torch.empty(recv_shape, dtype=recv_dtype, device=self.buf_device)
-            ops.append(dist.P2POp(dist.irecv, out, recv_from, self.group))
-        self._run(ops)
-        if out is not None and self.host_staged:
-            out = out.to(self.device)
-        return out
+    def post_recv(self, shape, dtype) -> _Pending:
+        buf = torch.empty(shape, dtype=dtype, device=self.buf_device)
+        comm._record("recv", self.group, buf)
+        return _Pending(dist.irecv(buf, self.src, group=self.group), buf, self.device, self.staged)
 
-    def send_meta(self, t: torch.Tensor, to: int):
-        hdr = torch.zeros(10, dtype=torch.int64, device=self.buf_device)
+    def send_meta(self, t: torch.Tensor) -> None:
+        hdr = torch.zeros(10, dtype=torch.int64)
         hdr[0] = t.dim()
         hdr[1] = _DT_CODE[t.dtype]
         hdr[2:2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
-        self._run([dist.P2POp(dist.isend, hdr, to, self.group)])
+        self.send(hdr.to(self.buf_device))
 
-    def recv_meta(self, frm: int):
-        hdr = torch.empty(10, dtype=torch.int64, device=self.buf_device)
-        self._run([dist.P2POp(dist.irecv, hdr, frm, self.group)])
-        h = hdr.tolist()
+    def recv_meta(self):
+        h = self.post_recv((10,), torch.int64).get().tolist()
         return tuple(int(v) for v in h[2:2 + h[0]]), _CODE_DT[h[1]]
 
-    def flush(self):
-        self.pending.clear()
+    def drain(self) -> None:
+        """Wait for (RCCL: order the current stream after) every send of this step."""
+        for w, _ in self._sends:
+            w.wait()
+        self._sends.clear()
+
+
+# ----------------------------------------------------------------------------
+# engine
+# ----------------------------------------------------------------------------
+class PipelineStage(nn.Module):
+    """The model chunks one pipeline rank holds (one per virtual stage)."""
+
+    def __init__(self, chunks: List[StageModule]):
+        super().__init__()
+        self.chunks = nn.ModuleList(chunks)
+
+    def forward(self, x, chunk: int = 0):
+        return self.chunks[chunk](x)
 
 
 class PipelineEngine:
-    """Runs one pipeline stage of a (dp x pp) mesh; ``train_step`` = fwd + bwd of all microbatches."""
+    """Runs one pipeline rank of a (dp x pp) mesh; ``train_step`` = fwd + bwd of all microbatches.
 
-    def __init__(self, stage_module: StageModule, *, stage: int, nstages: int, groups: rt.ProcessGroups,
+    The compute order comes from the C++ scheduler (GPipe, 1F1B or interleaved 1F1B with V
+    chunks per rank); all communication is derived from it: the activation input of every
+    non-first virtual stage arrives on the ``act`` channel from the previous rank (the ring
+    edge S-1 -> 0 between chunks), gradients flow back on the ``grad`` channels.  In steady
+    state every receive of the step is posted up front (shapes are known from the first step
+    of an input signature, which exchanges headers just in time), so each transfer overlaps
+    the compute that precedes its consumer; sends are fire-and-forget until the step ends."""
+
+    def __init__(self, stage_module: PipelineStage, *, stage: int, nstages: int, groups: rt.ProcessGroups,
                  microbatches: int, schedule: str, loss_fn: Callable, dp_engine: DataParallel,
-                 cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=()):
+                 cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=(),
+                 channels: Optional[Dict[str, Channel]] = None, p2p_groups=()):
         self.module = stage_module
+        self.chunks = list(stage_module.chunks)
+        self.V = len(self.chunks)
         self.stage, self.nstages = stage, nstages
         self.groups = groups
         self.M = microbatches
         self.schedule = schedule
         self.loss_fn = loss_fn
         self.dp = dp_engine
+        self.dp.defer_flush = True          # the engine launches the leftover buckets after the LAST backward
         self.sync = "grads"
         self.cast_dtype = cast_dtype
-        self.tied = tied                      # [(param, group)] on this rank
+        self.tied = tied                      # [(param, group, first owner's global rank)] on this rank
         self.param_names = param_names
         self.buffer_refs = list(buffer_refs)   # (original name, owner module, local name)
+        self.channels = channels or {}
+        self.order = native_runtime.pipeline_order(schedule, stage, nstages, microbatches, self.V)
+        S, SV = nstages, nstages * self.V
+        self._vs = [virtual_stage(c, stage, S) for c in range(self.V)]
+        self.holds_first = 0 in self._vs
+        self.holds_last = (SV - 1) in self._vs
         dev = rt.device()
-        prev = groups.pp_ranks[stage - 1] if stage > 0 else None
-        nxt = groups.pp_ranks[stage + 1] if stage < nstages - 1 else None
-        self.p2p = P2P(prev, nxt, groups.pp_group, dev)
-        self.program = native_runtime.pipeline_program(schedule, stage, nstages, microbatches)
-        # A collective over every group first: RCCL communicators exist before the first
-        # batched send/recv, which must not be a group's first operation.
+        # A collective over every group first: each RCCL communicator exists before its first
+        # point-to-point operation.
         if dist.is_initialized():
             probe = torch.zeros(1, device=dev)
-            for g in (groups.pp_group, groups.dp_group):
+            seen = set()
+            for g in [groups.pp_group, groups.dp_group] + list(p2p_groups):
+                if id(g) not in seen:
+                    seen.add(id(g))
+                    comm.all_reduce(probe, "sum", group=g)
+            for _, g, _ in tied:
                 comm.all_reduce(probe, "sum", group=g)
-            for _, g in tied:
-                comm.all_reduce(probe, "sum", group=g)
-        self._sig = None
-        self._in_meta = None     # (shape, dtype) of the activation this stage receives
-        self._out_meta = None    # (shape, dtype) of the activation this stage sends
+        self._sig = _UNSET
+        self._in_meta: Dict[int, tuple] = {}    # chunk -> (shape, dtype) of its received activation
+        self._out_meta: Dict[int, tuple] = {}   # chunk -> (shape, dtype) of its sent activation
+        self._tied_works = []
+        self._needs_tied = False
         self.last_loss = None
+        self.stats = {"steps": 0, "prefetched_recvs": 0}
 
     @property
     def is_first(self):
@@ -233,155 +375,211 @@ class PipelineEngine:
     def is_last(self):
         return self.stage == self.nstages - 1
 
+    # ------------------------------------------------------------ channels
+    def _act_in(self, c: int) -> Channel:
+        return self.channels["act_in" if self.stage > 0 else "act_in_wrap"]
+
+    def _act_out(self, c: int) -> Channel:
+        return self.channels["act_out" if self.stage < self.nstages - 1 else "act_out_wrap"]
+
+    def _grad_in(self, c: int) -> Channel:
+        return self.channels["grad_in" if self.stage < self.nstages - 1 else "grad_in_wrap"]
+
+    def _grad_out(self, c: int) -> Channel:
+        return self.channels["grad_out" if self.stage > 0 else "grad_out_wrap"]
+
+    def _prepost(self):
+        """Post every receive of the step, per channel in consumption order."""
+        S, SV = self.nstages, self.nstages * self.V
+        q = {}
+        for op, c, m in self.order:
+            vs = self._vs[c]
+            if op == "F" and vs > 0:
+                q[("act", c, m)] = self._act_in(c).post_recv(*self._in_meta[c])
+            elif op == "B" and vs < SV - 1:
+                q[("grad", c, m)] = self._grad_in(c).post_recv(*self._out_meta[c])
+        self.stats["prefetched_recvs"] += len(q)
+        return q
+
     # ------------------------------------------------------------ training
-    def train_step(self, inputs: torch.Tensor, targets: Optional[torch.Tensor] = None):
-        """Forward + backward of every microbatch of this stage; returns the mean loss on the last stage."""
+    def train_step(self, inputs: Optional[torch.Tensor], targets: Optional[torch.Tensor] = None):
+        """Forward + backward of every microbatch on this rank; returns the mean loss on the
+        rank that holds the last virtual stage (None elsewhere)."""
         self.module.train()
-        M = self.M
-        xs = list(inputs.chunk(M)) if self.is_first else [None] * M
-        ts = list(targets.chunk(M)) if (self.is_last and targets is not None) else [None] * M
-        if len(xs) != M or len(ts) != M:
-            raise ValueError(f"batch of {inputs.shape[0]} does not split into {M} microbatches")
-        sig = (tuple(inputs.shape), inputs.dtype)
+        M, S, SV = self.M, self.nstages, self.nstages * self.V
+        if self.holds_first:
+            xs = list(inputs.chunk(M))
+            if len(xs) != M:
+                raise ValueError(f"batch of {inputs.shape[0]} does not split into {M} microbatches")
+        if self.holds_last:
+            if targets is None:
+                raise ValueError("the last pipeline stage needs targets")
+            ts = list(targets.chunk(M))
+            if len(ts) != M:
+                raise ValueError(f"targets of {targets.shape[0]} do not split into {M} microbatches")
+        # every rank of a pipeline must see the same batch SHAPE each step (ranks without the
+        # first/last chunk may pass None): the header exchange is keyed on it
+        ref = inputs if inputs is not None else targets
+        sig = (tuple(ref.shape), ref.dtype) if ref is not None else "static"
         new_sig = sig != self._sig
-        self._sig = sig
-        acts_in: Dict[int, torch.Tensor] = {}
-        acts_out: Dict[int, torch.Tensor] = {}
-        losses: Dict[int, torch.Tensor] = {}
-        grads_in: Dict[int, torch.Tensor] = {}
-        total = torch.zeros((), device=rt.device(), dtype=torch.float32) if self.is_last else None
-        pr, nx = self.p2p.prev, self.p2p.next
-
-        def recv_fwd(m):
-            if self.is_first:
-                x = _cast_inputs(xs[m], self.cast_dtype, False)
-            else:
-                if m == 0 and new_sig:
-                    self._in_meta = self.p2p.recv_meta(pr)
-                shape, dt = self._in_meta
-                x = self.p2p.exchange(recv_shape=shape, recv_dtype=dt, recv_from=pr)
-                x.requires_grad_(x.is_floating_point())
-            acts_in[m] = x
-
-        def fwd(m):
-            y = self.module(acts_in[m])
-            if self.is_last:
-                loss = self.loss_fn(y, ts[m]) / M
-                losses[m] = loss
-                total.add_(loss.detach().float())
-            else:
-                acts_out[m] = y
-                if m == 0 and new_sig:
-                    self._out_meta = (tuple(y.shape), y.dtype)
-
-        def send_fwd(m):
-            if self.is_last:
-                return
-            y = acts_out[m]
-            if m == 0 and new_sig:
-                self.p2p.send_meta(y, nx)
-            self.p2p.exchange(send_t=y.detach(), send_to=nx)
-
-        def recv_bwd(m):
-            if self.is_last:
-                return
-            shape, dt = self._out_meta
-            grads_in[m] = self.p2p.exchange(recv_shape=shape, recv_dtype=dt, recv_from=nx)
-
-        def bwd(m):
-            last_mb = m == M - 1
-            ctx = self.dp.no_sync() if not last_mb else _null()
-            with ctx:
-                if self.is_last:
-                    losses.pop(m).backward()
+        if self._needs_tied:  # a previous step's gradients were never consumed: drop its tied sums
+            self._wait_tied()
+        pend = {} if new_sig else self._prepost()
+        acts_in: Dict[tuple, torch.Tensor] = {}
+        acts_out: Dict[tuple, torch.Tensor] = {}
+        losses: Dict[tuple, torch.Tensor] = {}
+        total = torch.zeros((), device=rt.device(), dtype=torch.float32) if self.holds_last else None
+        met_in, met_out = set(), set()
+        for op, c, m in self.order:
+            vs = self._vs[c]
+            if op == "F":
+                if vs == 0:
+                    x = _cast_inputs(xs[m], self.cast_dtype, False)
                 else:
-                    torch.autograd.backward(acts_out.pop(m), grad_tensors=grads_in.pop(m))
-
-        def send_bwd(m):
-            x = acts_in.pop(m)
-            if self.is_first:
-                return
-            g = x.grad if x.grad is not None else torch.zeros_like(x)
-            self.p2p.exchange(send_t=g, send_to=pr)
-
-        for op, a, b in self.program:
-            if op == "RECV_FWD":
-                recv_fwd(a)
-            elif op == "FWD":
-                fwd(a)
-            elif op == "SEND_FWD":
-                send_fwd(a)
-            elif op == "RECV_BWD":
-                recv_bwd(a)
-            elif op == "BWD":
-                bwd(a)
-            elif op == "SEND_BWD":
-                send_bwd(a)
-            elif op == "SEND_FWD_RECV_BWD":
-                if self.is_last:
-                    continue
-                y = acts_out[a]
-                shape, dt = self._out_meta
-                grads_in[b] = self.p2p.exchange(send_t=y.detach(), send_to=nx, recv_shape=shape, recv_dtype=dt,
-                                                recv_from=nx)
-            elif op == "SEND_BWD_RECV_FWD":
-                x = acts_in.pop(a)
-                if self.is_first:
-                    recv_fwd(b)
-                    continue
-                g = x.grad if x.grad is not None else torch.zeros_like(x)
-                shape, dt = self._in_meta
-                nxt_x = self.p2p.exchange(send_t=g, send_to=pr, recv_shape=shape, recv_dtype=dt, recv_from=pr)
-                nxt_x.requires_grad_(nxt_x.is_floating_point())
-                acts_in[b] = nxt_x
-        self.p2p.flush()
+                    if new_sig:
+                        ch = self._act_in(c)
+                        if c not in met_in:
+                            self._in_meta[c] = ch.recv_meta()
+                            met_in.add(c)
+                        x = ch.post_recv(*self._in_meta[c]).get()
+                    else:
+                        x = pend.pop(("act", c, m)).get()
+                    x.requires_grad_(x.is_floating_point())
+                acts_in[(c, m)] = x
+                y = self.chunks[c](x)
+                if vs == SV - 1:
+                    loss = self.loss_fn(y, ts[m]) / M
+                    losses[(c, m)] = loss
+                    total.add_(loss.detach().float())
+                else:
+                    acts_out[(c, m)] = y
+                    ch = self._act_out(c)
+                    if new_sig and c not in met_out:
+                        self._out_meta[c] = (tuple(y.shape), y.dtype)
+                        ch.send_meta(y)
+                        met_out.add(c)
+                    ch.send(y)
+            else:
+                ctx = self.dp.no_sync() if m != M - 1 else _null()  # reduce during each chunk's last backward
+                with ctx:
+                    if vs == SV - 1:
+                        losses.pop((c, m)).backward()
+                    else:
+                        g = (self._grad_in(c).post_recv(*self._out_meta[c]) if new_sig
+                             else pend.pop(("grad", c, m))).get()
+                        torch.autograd.backward(acts_out.pop((c, m)), grad_tensors=g)
+                x = acts_in.pop((c, m))
+                if vs > 0:
+                    self._grad_out(c).send(x.grad if x.grad is not None else torch.zeros_like(x))
+        self._sig = sig
+        self.dp.flush()                      # buckets of params that got no gradient, backward-end event
+        self._launch_tied()
+        for ch in self.channels.values():
+            ch.drain()
+        self.stats["steps"] += 1
         self.last_loss = total
         return total
 
+    # -------------------------------------------------- tied parameters (N8)
+    def _launch_tied(self):
+        """Sum the gradients of parameters shared across pipeline ranks (GPT-2's wte/lm_head)
+        asynchronously, right after their stage-local DP reduction was issued; the optimizer
+        updates the other buckets first and waits for these last (``bucket_order``)."""
+        self._tied_works = []
+        if not self.tied:
+            return
+        space = self.dp.space
+        cs = self.dp.comm_stream
+        for p, group, _src in self.tied:
+            bk, off, _ = space.param_info[id(p)]
+            buf = space.grad_buffer(bk)[off:off + p.numel()]
+            if cs is not None:
+                with torch.cuda.stream(cs):
+                    if bk.work is not None:
+                        bk.work.wait()
+                    self._tied_works.append(comm.all_reduce(buf, "sum", group=group, async_op=True))
+            else:
+                if bk.work is not None:
+                    bk.work.wait()
+                self._tied_works.append(comm.all_reduce(buf, "sum", group=group, async_op=True))
+        self._needs_tied = True
+
+    def _wait_tied(self):
+        cs = self.dp.comm_stream
+        for w in self._tied_works:
+            if w is None:
+                continue
+            if cs is not None:
+                with torch.cuda.stream(cs):
+                    w.wait()
+            else:
+                w.wait()
+        if cs is not None and self._tied_works:
+            torch.cuda.current_stream().wait_stream(cs)
+        self._tied_works = []
+        self._needs_tied = False
+
     # -------------------------------------------------- optimizer protocol
-    def finalize_grads(self):
+    def finalize_grads(self, wait_tied: bool = True):
+        """Idempotent: the stage-local DP reduction, then the cross-stage tied-gradient sum.
+        Called by clip_grad_norm_ AND step; the tied sum is applied exactly once per step."""
         self.dp.finalize_grads()
-        for p, group in self.tied:
-            bk, off, _ = self.dp.space.param_info[id(p)]
-            buf = self.dp.space.grad_buffer(bk)
-            comm.all_reduce(buf[off:off + p.numel()], "sum", group=group)
+        if wait_tied and self._needs_tied:
+            self._wait_tied()
+
+    def tied_buckets(self) -> set:
+        """Buckets holding a tied parameter: the optimizer updates them last, after the others
+        (whose gradients are final as soon as the DP reduction is), hiding the tied sum."""
+        return {self.dp.space.param_info[id(p)][0].index for p, _, _ in self.tied}
+
+    def norm_reduction(self):
+        """(groups to sum squared gradient norms over, params to leave out of this rank's sum):
+        pipeline ranks hold disjoint parameters except tied ones, counted on their first owner."""
+        skip = [p for p, _g, src in self.tied if src != rt.get_rank()]
+        return ([self.groups.pp_group] if self.nstages > 1 else []), skip
 
     def after_step(self):
         self.dp.after_step()
 
     def comm_metrics(self) -> dict:
-        """DP all-reduce numbers of this stage plus the schedule's analytic bubble fraction
-        ((S-1)/(M+S-1) for GPipe and 1F1B with S stages and M microbatches)."""
+        """DP all-reduce numbers of this stage, P2P bytes, plus the schedule's bubble fraction
+        (simulated for the configured schedule; (S-1)/(M+S-1) for GPipe/1F1B)."""
         out = self.dp.comm_metrics()
-        out["bubble_fraction"] = (self.nstages - 1) / (self.M + self.nstages - 1)
+        out["bubble_fraction"] = pipeline_bubble(self.schedule, self.nstages, self.M, self.V)
+        out["p2p_bytes"] = sum(ch.bytes for ch in self.channels.values())
         return out
 
     # ------------------------------------------------------------ inference
     @torch.no_grad()
-    def forward_step(self, inputs: torch.Tensor) -> Optional[torch.Tensor]:
-        """Pipelined forward only (GPipe order); returns the full output on the last stage."""
+    def forward_step(self, inputs: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """Pipelined forward only, microbatch-major then chunk order (every channel FIFO);
+        returns the full output on the rank holding the last virtual stage."""
         self.module.eval()
-        M = self.M
-        xs = list(inputs.chunk(M)) if self.is_first else [None] * M
+        M, SV = self.M, self.nstages * self.V
+        xs = list(inputs.chunk(M)) if self.holds_first else [None] * M
         outs = []
-        pr, nx = self.p2p.prev, self.p2p.next
         for m in range(M):
-            if self.is_first:
-                x = _cast_inputs(xs[m], self.cast_dtype, False)
-            else:
-                shape, dt = self.p2p.recv_meta(pr)
-                x = self.p2p.exchange(recv_shape=shape, recv_dtype=dt, recv_from=pr)
-            y = self.module(x)
-            if self.is_last:
-                outs.append(y)
-            else:
-                self.p2p.send_meta(y, nx)
-                self.p2p.exchange(send_t=y, send_to=nx)
-        self.p2p.flush()
+            for c in range(self.V):
+                vs = self._vs[c]
+                if vs == 0:
+                    x = _cast_inputs(xs[m], self.cast_dtype, False)
+                else:
+                    ch = self._act_in(c)
+                    shape, dt = ch.recv_meta()
+                    x = ch.post_recv(shape, dt).get()
+                y = self.chunks[c](x)
+                if vs == SV - 1:
+                    outs.append(y)
+                else:
+                    ch = self._act_out(c)
+                    ch.send_meta(y)
+                    ch.send(y)
+        for ch in self.channels.values():
+            ch.drain()
         return torch.cat(outs) if outs else None
 
     def state_dict(self):
-        """This stage's parameters under their ORIGINAL model names."""
+        """This rank's parameters under their ORIGINAL model names."""
         out = {}
         for p in self.module.parameters():
             name = self.param_names.get(id(p))
@@ -394,6 +592,20 @@ class PipelineEngine:
             yield name, owner.get_buffer(local)
 
 
+_BUBBLE_CACHE: Dict[tuple, float] = {}
+
+
+def pipeline_bubble(schedule: str, nstages: int, nmicro: int, nchunks: int = 1) -> float:
+    """Idle fraction of a schedule (backward = 2x forward), from :func:`simulate_schedule`."""
+    key = (schedule, nstages, nmicro, nchunks)
+    if key not in _BUBBLE_CACHE:
+        if nstages <= 1:
+            _BUBBLE_CACHE[key] = 0.0
+        else:
+            _BUBBLE_CACHE[key] = simulate_schedule(schedule, nstages, nmicro, nchunks)["bubble"]
+    return _BUBBLE_CACHE[key]
+
+
 class _null:
     def __enter__(self):
         return self
@@ -402,21 +614,60 @@ class _null:
         return False
 
 
+_UNSET = object()
+
+
+def _chunk_layer_ranges(plan, stage: int, nstages: int, V: int):
+    """(lo, hi) spine-layer ranges of this rank's chunks: chunk c = virtual stage c*S + stage."""
+    return [(plan.bounds[virtual_stage(c, stage, nstages)], plan.bounds[virtual_stage(c, stage, nstages) + 1])
+            for c in range(V)]
+
+
 def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Optional[Callable] = None):
     """Cut ``model`` along ``plan`` and return ``(PipelineEngine, stage_optimizer)`` for this rank."""
     from ..api import _is_fused, build_space, prepare_model
 
     rt.init(timeout_s=cfg.timeout_s)
     world = rt.get_world_size()
-    mesh = rt.Mesh(dp=plan.dp, pp=plan.pp, tp=1)
+    S = plan.pp
+    V = max(int(getattr(plan, "virtual", 1) or 1), 1)
+    schedule = getattr(plan, "schedule", None) or cfg.schedule
+    if V > 1:
+        schedule = "interleaved"
+    elif schedule == "interleaved":
+        schedule = "1f1b"
+    if len(plan.bounds) != S * V + 1:
+        raise ValueError(f"plan has {len(plan.bounds) - 1} pipeline chunks, expected {S} x {V}")
+    mesh = rt.Mesh(dp=plan.dp, pp=S, tp=1)
     if mesh.size != world:
-        raise ValueError(f"plan {plan.dp}x{plan.pp} does not match world size {world}")
+        raise ValueError(f"plan {plan.dp}x{S} does not match world size {world}")
     groups = rt.ProcessGroups(mesh)
     stage = groups.pp_idx
-    lo, hi = plan.bounds[stage], plan.bounds[stage + 1]
-    layers = plan.spine.layers[lo:hi]
-    pmap, bmap = original_names(model, layers)
-    stage_mod = StageModule(layers, plan.checkpoint[lo:hi])
+    ranges = _chunk_layer_ranges(plan, stage, S, V)
+    all_layers = plan.spine.layers
+
+    # tied parameters, from ORIGINAL parameter identities (before this rank materialises its
+    # chunks, which re-creates the local tensors): which pipeline ranks hold each shared one
+    pid_name = {}
+    for n, p in model.named_parameters(remove_duplicate=False):
+        pid_name.setdefault(id(p), n)
+    owners: Dict[str, List[int]] = {}
+    for vs in range(S * V):
+        for layer in all_layers[plan.bounds[vs]:plan.bounds[vs + 1]]:
+            for p in layer.parameters():
+                name = pid_name.get(id(p))
+                if name is None:
+                    continue
+                lst = owners.setdefault(name, [])
+                if vs % S not in lst:
+                    lst.append(vs % S)
+    tied_sets = [(n, sorted(sts)) for n, sts in owners.items() if len(sts) > 1]
+
+    layers_per_chunk = [all_layers[lo:hi] for lo, hi in ranges]
+    flat_layers = [l for ls in layers_per_chunk for l in ls]
+    pmap, bmap = original_names(model, flat_layers)
+    chunks = [StageModule(ls, plan.checkpoint[lo:hi]) for ls, (lo, hi) in zip(layers_per_chunk, ranges)]
+    stage_mod = PipelineStage(chunks)
     dev = rt.device()
     init_fn = getattr(model, "init_weights", None)
     materialize_(stage_mod, dev, init_fn)
@@ -429,27 +680,50 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     if loss_fn is None:
         raise ValueError("pipeline parallelism needs loss_fn= (or model.loss_fn)")
 
-    # tied parameters: which stages hold each shared parameter
-    owners: Dict[int, List[int]] = {}
-    objs = {}
-    for s in range(plan.pp):
-        for layer in plan.spine.layers[plan.bounds[s]:plan.bounds[s + 1]]:
-            for p in layer.parameters():
-                lst = owners.setdefault(id(p), [])
-                if s not in lst:
-                    lst.append(s)
-                objs[id(p)] = p
-    tied_sets = [(pid, sts) for pid, sts in owners.items() if len(sts) > 1]
+    names, buffer_refs = stage_names(flat_layers, pmap, bmap)
+    by_name = {n: p for p in stage_mod.parameters() for n in [names.get(id(p))] if n is not None}
     tied_local = []
-    for pid, sts in tied_sets:  # every rank creates every group, same order
+    for name, sts in tied_sets:  # every rank creates every group, same order
         for d in range(plan.dp):
             ranks = [mesh.rank_of(d, s, 0) for s in sts]
             grp = dist.new_group(ranks) if dist.is_initialized() else None
             if rt.get_rank() in ranks:
-                tied_local.append((objs[pid], grp, ranks[0]))
+                tied_local.append((by_name[name], grp, ranks[0]))
+
+    # one-directional FIFO channels: a process group per direction per pipeline edge kind
+    channels: Dict[str, Channel] = {}
+    p2p_groups = []  # every channel group this rank belongs to (also those it sends nothing on)
+    kinds = ["act", "grad"] + (["act_wrap", "grad_wrap"] if V > 1 else [])
+    for kind in kinds:
+        for d in range(plan.dp):
+            ranks = [mesh.rank_of(d, s, 0) for s in range(S)]
+            grp = dist.new_group(ranks) if dist.is_initialized() else None
+            if rt.get_rank() not in ranks:
+                continue
+            p2p_groups.append(grp)
+            me = ranks[stage]
+            if kind == "act":
+                if stage > 0:
+                    channels["act_in"] = Channel(grp, ranks[stage - 1], me, dev, "act_in")
+                if stage < S - 1:
+                    channels["act_out"] = Channel(grp, me, ranks[stage + 1], dev, "act_out")
+            elif kind == "grad":
+                if stage < S - 1:
+                    channels["grad_in"] = Channel(grp, ranks[stage + 1], me, dev, "grad_in")
+                if stage > 0:
+                    channels["grad_out"] = Channel(grp, me, ranks[stage - 1], dev, "grad_out")
+            elif kind == "act_wrap":
+                if stage == 0:
+                    channels["act_in_wrap"] = Channel(grp, ranks[S - 1], me, dev, "act_in_wrap")
+                if stage == S - 1:
+                    channels["act_out_wrap"] = Channel(grp, me, ranks[0], dev, "act_out_wrap")
+            else:
+                if stage == S - 1:
+                    channels["grad_in_wrap"] = Channel(grp, ranks[0], me, dev, "grad_in_wrap")
+                if stage == 0:
+                    channels["grad_out_wrap"] = Channel(grp, me, ranks[S - 1], dev, "grad_out_wrap")
 
     dtype, dtype_of, cl = prepare_model(stage_mod, cfg, dev)
-    names, buffer_refs = stage_names(layers, pmap, bmap)
     stage_params = [p for p in stage_mod.parameters() if p.requires_grad]
     if optimizer is not None:
         optimizer = restrict_optimizer(optimizer, stage_params)
@@ -464,16 +738,16 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     dp_engine = DataParallel(stage_mod, space, group=groups.dp_group, src_rank=groups.dp_ranks[0], sync="grads",
                              overlap=cfg.overlap, cast_dtype=dtype, channels_last=cl, unpack_grads=False,
                              broadcast_buffers=cfg.broadcast_buffers, find_unused=True, sync_comm=cfg.sync_comm)
-    engine = PipelineEngine(stage_mod, stage=stage, nstages=plan.pp, groups=groups, microbatches=plan.microbatches,
-                            schedule=cfg.schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
-                            tied=[(p, g) for p, g, _ in tied_local], param_names=names,
-                            buffer_refs=buffer_refs)
+    engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
+                            schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
+                            tied=tied_local, param_names=names, buffer_refs=buffer_refs, channels=channels,
+                            p2p_groups=p2p_groups)
     engine.plan = plan
     if optimizer is not None:
         if not _is_fused(optimizer):
             raise TypeError("pipeline engine needs a madnn fused optimizer (FusedSGD / FusedAdam)")
         optimizer.bind(space)
         optimizer.grad_source = engine
-    get_logger().info("madnn pp: stage %d/%d layers [%d, %d) dp=%d microbatches=%d schedule=%s tied=%d",
-                      stage, plan.pp, lo, hi, plan.dp, plan.microbatches, cfg.schedule, len(tied_local))
+    get_logger().info("madnn pp: rank %d/%d chunks %s dp=%d microbatches=%d schedule=%s tied=%d", stage, S,
+                      ranges, plan.dp, plan.microbatches, schedule, len(tied_local))
     return engine, optimizer

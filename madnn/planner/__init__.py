@@ -1,4 +1,4 @@
-"""Auto-partitioner: trace -> cost -> place (DP, PP or DP x PP) for one node.
+"""Auto-partitioner: trace -> cost -> place (DP, PP, DP x PP or DP x TP) for one node.
 
 North-star requirement: walk an arbitrary ``nn.Module``,
 cost each layer, and place it across the GPUs of one node as data- or
@@ -6,25 +6,37 @@ pipeline-parallel stages sized for 288 GB of HBM3E per GPU.  The reference's
 closest analog is the sync-period heuristic (datamodule.lua:68-78) and the
 dead ``comm_speed`` probe (datamodule.lua:280-303).
 
-Step-time model for ``W = dp x pp`` GPUs, global batch B, M microbatches:
+Costs: per-layer analytic FLOPs/bytes on the meta device (``cost.estimate``),
+replaced by HIP-event measurements of every distinct layer when a GPU is
+present (``cost.measure_layers``).  Machine numbers (xGMI all-reduce / P2P
+bandwidth, HBM, GEMM rate) come from the calibrated hardware profile
+(``madnn.planner.calibrate``) when one exists, else the datasheet defaults.
 
-* DP   (pp = 1): compute(B/dp) + exposed all-reduce, where the bucketed
-  all-reduce overlaps backward so only the last bucket (and whatever exceeds
-  the backward time) is exposed;
-* PP   (dp = 1): (M + pp - 1)/M x max_stage(B) + per-microbatch P2P of the
-  boundary activations and gradients;
-* DPxPP: the PP expression with B/dp per replica, plus the stage-local
-  all-reduce over dp (on links disjoint from the PP hops).
+Step-time model for ``W = dp x pp x tp`` GPUs, global batch B, M microbatches:
 
-Memory per GPU: parameter/optimizer bytes of its stage (madnn layout, 16-20
-B/param) + saved activations (1F1B keeps ``pp - s`` microbatches in flight on
-stage s; with activation checkpointing only boundary tensors + one layer).
-A candidate that does not fit ``hbm_gb x mem_headroom`` first tries
-checkpointing, then is dropped.  Stage boundaries come from the C++
-min-max-bottleneck partitioner (``madnn_partition``).
+* DP: compute(B/dp) + the part of the bucketed all-reduce that the backward
+  does not hide -- a bucket-by-bucket timeline: buckets fill in backward
+  order, each is reduced when its last gradient lands, one after another on
+  the comm stream; exposed = reductions still running after backward ends;
+* PP (GPipe / 1F1B / interleaved with V chunks per rank):
+  M x max-rank-time-per-microbatch / (1 - bubble), where the bubble is the
+  idle fraction of the simulated schedule, plus the fill/drain P2P latency
+  (steady-state transfers run under compute); with dp > 1 the stage-local
+  all-reduce overlaps only the last microbatch's backward (same timeline);
+* TP (row-parallel large Linears, ``strategy="tp"``): the sharded GEMM share of
+  compute divided by T, plus the per-layer activation all-reduce and
+  input-gradient all-gather on the critical path.
+
+Memory per GPU: parameter/optimizer bytes of its layers (madnn layout)
++ saved activations of the microbatches in flight (simulated per schedule;
+with activation checkpointing only boundary tensors + one layer).  A candidate
+that does not fit ``hbm_gb x mem_headroom`` is dropped unless nothing fits.
+Stage boundaries come from the C++ min-max-bottleneck partitioner
+(``madnn_partition``).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -33,37 +45,48 @@ from torch import nn
 
 from ..config import Config, torch_dtype
 from ..ops import native_runtime
-from .cost import LayerCost, divisors, estimate, stage_estimate
+from ..utils.logging import get_logger
+from .cost import LayerCost, divisors, estimate, measure_layers, stage_estimate
 from .hw import Machine, load
 from .trace import Spine, find_block_list, trace
 
 
 @dataclass
 class Plan:
-    strategy: str                      # dp | pp | dp_pp
+    strategy: str                      # dp | pp | dp_pp | tp
     dp: int
     pp: int
-    bounds: List[int]                  # stage boundaries over spine layers (len pp+1)
+    bounds: List[int]                  # chunk boundaries over spine layers (len pp*virtual+1)
     microbatches: int
     checkpoint: List[bool]             # per spine layer
     est_step_s: float
-    est_mem_gb: List[float]            # per stage, per GPU
+    est_mem_gb: List[float]            # per pipeline rank, per GPU
     spine: Optional[Spine] = None
     costs: Optional[List[LayerCost]] = None
     candidates: list = field(default_factory=list)
     global_batch: int = 0
+    schedule: str = "1f1b"
+    virtual: int = 1
+    tp: int = 1
+    measured: bool = False
 
     def describe(self) -> str:
         ck = sum(self.checkpoint)
-        return (f"{self.strategy} dp={self.dp} pp={self.pp} stages={self.bounds} microbatches={self.microbatches} "
-                f"ckpt_layers={ck}/{len(self.checkpoint)} est_step={self.est_step_s * 1e3:.1f}ms "
-                f"mem/GPU={max(self.est_mem_gb):.1f}GB")
+        sched = f" schedule={self.schedule}" + (f"x{self.virtual}" if self.virtual > 1 else "") if self.pp > 1 else ""
+        return (f"{self.strategy} dp={self.dp} pp={self.pp} tp={self.tp}{sched} stages={self.bounds} "
+                f"microbatches={self.microbatches} ckpt_layers={ck}/{len(self.checkpoint)} "
+                f"est_step={self.est_step_s * 1e3:.1f}ms mem/GPU={max(self.est_mem_gb):.1f}GB "
+                f"costs={'measured' if self.measured else 'analytic'}")
 
     def table(self) -> str:
-        rows = ["| strategy | dp | pp | M | ckpt | est step (ms) | max mem/GPU (GB) | fits |", "|---|---|---|---|---|---|---|---|"]
-        for c in self.candidates:
-            rows.append(f"| {c['strategy']} | {c['dp']} | {c['pp']} | {c['M']} | {c['ckpt']} | "
-                        f"{c['step_s'] * 1e3:.2f} | {c['mem_gb']:.1f} | {c['fits']} |")
+        rows = ["| strategy | dp | pp | tp | sched | M | ckpt | compute (ms) | exposed comm (ms) | bubble | "
+                "est step (ms) | max mem/GPU (GB) | fits |",
+                "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+        for c in sorted(self.candidates, key=lambda c: c["step_s"]):
+            rows.append(f"| {c['strategy']} | {c['dp']} | {c['pp']} | {c.get('tp', 1)} | {c.get('schedule', '-')} | "
+                        f"{c['M']} | {c['ckpt']} | {c.get('compute_s', 0) * 1e3:.2f} | "
+                        f"{c.get('comm_s', 0) * 1e3:.2f} | {c.get('bubble', 0):.3f} | {c['step_s'] * 1e3:.2f} | "
+                        f"{c['mem_gb']:.1f} | {c['fits']} |")
         return "\n".join(rows)
 
 
@@ -71,7 +94,8 @@ def infer_example_input(model: nn.Module, batch: int = 1) -> torch.Tensor:
     """A representative input when the caller gives none (zoo configs, first layer shapes)."""
     cfg = getattr(model, "config", None)
     if cfg is not None:
-        seq = getattr(cfg, "n_positions", None) or getattr(cfg, "max_position", None) or 512
+        seq = getattr(cfg, "n_positions", None) or getattr(cfg, "max_position", None) or \
+            getattr(cfg, "max_position_embeddings", None) or 512
         seq = min(seq, 2048)
         return torch.zeros(batch, seq, dtype=torch.long)
     for m in model.modules():
@@ -91,15 +115,58 @@ def _opt_kind(optimizer) -> str:
     return "adam" if "adam" in name else "sgd"
 
 
+def _reduce_bytes(cfg: Config) -> int:
+    return 4 if cfg.reduce_dtype in ("float32", "fp32") else 2
+
+
+def _want_measure(cfg: Config) -> bool:
+    v = cfg.extra.get("measure", os.environ.get("MADNN_PLAN_MEASURE", "auto"))
+    if isinstance(v, str):
+        v = v.lower()
+        if v == "auto":
+            return torch.cuda.is_available()
+        return v in ("1", "true", "yes", "on")
+    return bool(v)
+
+
 def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optional[torch.Tensor] = None,
-               optimizer=None, global_batch: Optional[int] = None, machine: Optional[Machine] = None) -> Plan:
+               optimizer=None, global_batch: Optional[int] = None, machine: Optional[Machine] = None,
+               costs: Optional[List[LayerCost]] = None) -> Plan:
+    """Trace, cost (measured on the GPU when available) and choose the placement with the
+    lowest modelled step time that fits in HBM.  ``global_batch``: samples per optimizer step
+    over the whole job (default ``cfg.extra['global_batch']``, else the example input's
+    batch per GPU x ``world``)."""
     hw = machine or load()
     spine = trace(model)
+    explicit_input = example_input is not None
     if example_input is None:
         example_input = infer_example_input(model)
     dtype = torch_dtype(cfg.dtype)
-    costs = estimate(spine, example_input, dtype=dtype, machine=hw)
-    B = global_batch or cfg.extra.get("global_batch") or max(example_input.shape[0], 1) * world
+    measured = False
+    if costs is None:
+        costs = estimate(spine, example_input, dtype=dtype, machine=hw)
+        import torch.distributed as dist
+
+        multi = dist.is_initialized() and dist.get_world_size() > 1
+        if _want_measure(cfg) and (not multi or dist.get_rank() == 0):
+            try:
+                mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input)
+                costs = measure_layers(spine, example_input, costs, batch=mb, dtype=dtype)
+            except Exception as e:  # noqa: BLE001 - the analytic model still plans
+                get_logger().warning("madnn planner: layer measurement failed (%s); using analytic costs", e)
+        if multi:
+            # every rank must choose the SAME placement: rank 0's (measured) costs are the plan input
+            obj = [[(c.fwd_s, c.bwd_s, c.measured) for c in costs]]
+            dist.broadcast_object_list(obj, src=0)
+            for c, (f, b, m) in zip(costs, obj[0]):
+                c.fwd_s, c.bwd_s, c.measured = f, b, m
+    measured = all(c.measured for c in costs)
+    B = global_batch or cfg.extra.get("global_batch")
+    if not B:
+        if not explicit_input:
+            get_logger().warning("madnn planner: no example_input / global_batch given; assuming %d sample(s) per "
+                                 "GPU for microbatch and activation sizing", example_input.shape[0])
+        B = max(example_input.shape[0], 1) * world
     opt = _opt_kind(optimizer)
     cap = hw.hbm_gb * cfg.mem_headroom * 1e9
     L = len(spine)
@@ -115,19 +182,41 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
             c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode)
             if c is not None:
                 cands.append(c)
+    if forced in ("auto", "tp") and world > 1:
+        for tp in divisors(world):
+            if tp == 1 or (forced == "tp" and cfg.tp_size > 1 and tp != cfg.tp_size):
+                continue
+            c = _tp_candidate(spine, costs, world // tp, tp, B, cfg, hw, opt, cap, tuple(example_input.shape[1:]),
+                              example_input.dtype)
+            if c is not None:
+                cands.append(c)
     if not cands:
         raise RuntimeError(f"madnn planner: no feasible placement for world={world}, strategy={forced}")
     feasible = [c for c in cands if c["fits"]] or cands
-    best = min(feasible, key=lambda c: (c["step_s"], c["pp"], c["ckpt"]))
-    strategy = "dp" if best["pp"] == 1 else ("pp" if best["dp"] == 1 else "dp_pp")
+    best = min(feasible, key=lambda c: (c["step_s"], c["pp"], c.get("tp", 1), c["ckpt"]))
     ck = [best["ckpt"] and _ckpt_eligible(spine, i) for i in range(L)]
-    return Plan(strategy, best["dp"], best["pp"], best["bounds"], best["M"], ck, best["step_s"], best["mem_list"],
-                spine, costs, cands, B)
+    plan = Plan(best["strategy"], best["dp"], best["pp"], best["bounds"], best["M"], ck, best["step_s"],
+                best["mem_list"], spine, costs, cands, B, schedule=best.get("schedule", "1f1b"),
+                virtual=best.get("V", 1), tp=best.get("tp", 1), measured=measured)
+    log = get_logger()
+    log.info("madnn plan: %s", plan.describe())
+    log.info("madnn plan candidates (world=%d, global batch %d):\n%s", world, B, plan.table())
+    return plan
+
+
+def _default_measure_batch(example_input: torch.Tensor) -> int:
+    """Per-layer timing batch: enough work per launch for realistic kernel efficiency."""
+    per = int(torch.tensor(example_input.shape[1:]).prod()) if example_input.dim() > 1 else 1
+    if example_input.dtype in (torch.long, torch.int32):  # token ids: ~4k tokens
+        return max(1, min(16, 4096 // max(per, 1)))
+    return 32 if example_input.dim() == 4 else 64
 
 
 def _allowed(forced: str, pp: int, dp: int, world: int, pp_stages) -> bool:
     if forced == "dp":
         return pp == 1
+    if forced == "tp":
+        return False
     if forced == "pp":
         return pp == (pp_stages or world) and pp > 1 or world == 1
     if forced == "dp_pp":
@@ -142,45 +231,181 @@ def _ckpt_eligible(spine: Spine, i: int) -> bool:
     return 0 < i < len(spine) - 1 or len(spine) == 1
 
 
+def dp_exposed_s(bwd_times: List[float], grad_bytes: List[float], dp: int, hw: Machine, bucket_bytes: float) -> float:
+    """Communication left exposed after backward by the overlapped bucketed all-reduce.
+
+    ``bwd_times``/``grad_bytes`` per layer in FORWARD order (seconds for this rank's batch,
+    bytes of its gradients in the reduce dtype).  Backward visits layers in reverse; a
+    bucket (filled in that order up to ``bucket_bytes``) becomes ready when the backward of
+    its last layer ends, and buckets are reduced one after another on the comm stream."""
+    if dp <= 1:
+        return 0.0
+    t = 0.0
+    ready = []
+    cur = 0.0
+    for bt, gb in zip(reversed(bwd_times), reversed(grad_bytes)):
+        t += bt
+        cur += gb
+        if cur >= bucket_bytes:
+            ready.append((t, cur))
+            cur = 0.0
+    if cur > 0:
+        ready.append((t, cur))
+    end = 0.0
+    for rt_, nb in ready:
+        end = max(end, rt_) + hw.allreduce_s(nb, dp)
+    return max(0.0, end - t)
+
+
+def _chunk_ranks(pp: int, V: int):
+    return [[c * pp + r for c in range(V)] for r in range(pp)]
+
+
 def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt):
+    from ..parallel.pp import pipeline_bubble, simulate_schedule
+
     L = len(costs)
     per_replica = max(B // dp, 1)
-    M = 1 if pp == 1 else (cfg.microbatches or min(max(4 * pp, pp), per_replica))
-    M = max(1, min(M, per_replica))
+    V = 1
+    schedule = cfg.schedule if pp > 1 else "none"
+    if pp == 1:
+        M = 1
+    else:
+        M = cfg.microbatches or min(4 * pp, per_replica)
+        M = max(1, min(M, per_replica))
+        if schedule == "interleaved":
+            V = max(int(cfg.virtual_stages or 2), 1)
+            while V > 1 and pp * V > L:
+                V -= 1
+            M = M // pp * pp
+            if V == 1 or M < pp:
+                V, schedule = 1, "1f1b"
+                M = max(1, min(cfg.microbatches or min(4 * pp, per_replica), per_replica))
     mb = per_replica / M
-    times = [c.time_s * (1.0 + (1.0 / 3.0 if ckpt else 0.0)) for c in costs]
+    rfac = 1.0 + (1.0 / 3.0 if ckpt else 0.0)
+    nst = pp * V
     mems = [stage_estimate(costs, i, i + 1, opt, ckpt).param_bytes + stage_estimate(costs, i, i + 1, opt, ckpt)
             .act_bytes_per_sample * mb * (pp if pp > 1 else 1) for i in range(L)]
+    times = [c.time_s * rfac for c in costs]
     try:
-        bounds, _ = native_runtime.partition(times, pp, mems, cap if cap > 0 else 0.0)
+        bounds, _ = native_runtime.partition(times, nst, mems, cap / V if cap > 0 else 0.0)
     except ValueError:
-        bounds, _ = native_runtime.partition(times, pp)
-    stage_t, mem_list = [], []
-    for s in range(pp):
-        lo, hi = bounds[s], bounds[s + 1]
-        est = stage_estimate(costs, lo, hi, opt, ckpt)
-        stage_t.append(est.time_per_sample_s * mb)
-        inflight = (pp - s) if cfg.schedule == "1f1b" else M
-        inflight = min(inflight, M)
-        act = est.act_bytes_per_sample * mb * inflight
-        mem_list.append((est.param_bytes + act) / 1e9)
-    bottleneck = max(stage_t)
-    if pp == 1:
-        compute = bottleneck
-        grad_bytes = sum(c.params for c in costs) * 4.0  # fp32 reduce buffers
-        ar = hw.allreduce_s(grad_bytes, dp)
-        exposed = max(ar - 0.8 * compute * (2.0 / 3.0), ar * 0.1)
-        step = compute + exposed
+        bounds, _ = native_runtime.partition(times, nst)
+    chunk_est = [stage_estimate(costs, bounds[v], bounds[v + 1], opt, ckpt) for v in range(nst)]
+    ranks = _chunk_ranks(pp, V)
+    rank_t = [sum(chunk_est[v].time_per_sample_s for v in vs) * mb for vs in ranks]
+    if pp > 1:
+        inflight = simulate_schedule(schedule, pp, M, V)["peak_inflight"] if schedule != "none" else [1] * pp
+        if schedule == "gpipe":
+            inflight = [M * V] * pp
     else:
-        p2p = max(costs[bounds[s + 1] - 1].out_bytes * mb for s in range(pp - 1))
-        step = (M + pp - 1) * bottleneck + 2 * (M + pp - 1) * hw.p2p_s(p2p)
-        if dp > 1:
-            stage_params = max(stage_estimate(costs, bounds[s], bounds[s + 1], opt).params for s in range(pp))
-            step += 0.3 * hw.allreduce_s(stage_params * 4.0, dp)
+        inflight = [1]
+    mem_list = []
+    for r, vs in enumerate(ranks):
+        pbytes = sum(chunk_est[v].param_bytes for v in vs)
+        act_per_chunk = sum(chunk_est[v].act_bytes_per_sample for v in vs) / len(vs) * mb
+        mem_list.append((pbytes + act_per_chunk * inflight[r]) / 1e9)
+    bucket_bytes = cfg.bucket_mb * 2**20
+    rb = _reduce_bytes(cfg)
+    if pp == 1:
+        compute = rank_t[0]
+        bubble = 0.0
+        bwd = [c.bwd_s * rfac * per_replica for c in costs]
+        comm_s = dp_exposed_s(bwd, [c.params * rb for c in costs], dp, hw, bucket_bytes)
+        step = compute + comm_s
+    else:
+        bubble = pipeline_bubble(schedule, pp, M, V)
+        compute = M * max(rank_t)
+        p2p = max((costs[bounds[v + 1] - 1].out_bytes * mb for v in range(nst - 1)), default=0.0)
+        comm_s = 2 * (nst - 1) * hw.p2p_s(p2p)  # fill + drain; steady-state hops run under compute
+        if dp > 1:  # stage-local reduction overlaps the last microbatch's backward only
+            worst = 0.0
+            for vs in ranks:
+                idx = [i for v in vs for i in range(bounds[v], bounds[v + 1])]
+                bwd = [costs[i].bwd_s * rfac * mb for i in idx]
+                worst = max(worst, dp_exposed_s(bwd, [costs[i].params * rb for i in idx], dp, hw, bucket_bytes))
+            comm_s += worst
+        step = compute / max(1.0 - bubble, 1e-3) + comm_s
     fits = max(mem_list) * 1e9 <= cap
-    return {"strategy": "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp"), "dp": dp, "pp": pp, "M": M,
-            "ckpt": ckpt, "bounds": bounds, "step_s": step, "mem_gb": max(mem_list), "mem_list": mem_list,
-            "fits": fits}
+    strategy = "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp")
+    return {"strategy": strategy, "dp": dp, "pp": pp, "tp": 1, "M": M, "V": V, "schedule": schedule,
+            "ckpt": ckpt, "bounds": bounds, "step_s": step, "compute_s": compute, "comm_s": comm_s,
+            "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits}
 
 
-__all__ = ["Plan", "plan_model", "trace", "estimate", "infer_example_input", "find_block_list"]
+def _tp_linears(layer: nn.Module, tp: int, min_params: int, in_shape, in_dtype):
+    """(in, out, tokens per sample) of the Linears ``strategy="tp"`` would shard inside
+    ``layer``; tokens come from a META-device forward with hooks on those Linears."""
+    mods = [m for m in layer.modules()
+            if type(m) is nn.Linear and m.weight.numel() >= min_params and m.in_features % tp == 0]
+    if not mods:
+        return []
+    toks = {}
+    hooks = [m.register_forward_hook(lambda mod, inp, out: toks.__setitem__(
+        id(mod), int(inp[0].numel() // max(inp[0].shape[-1], 1)))) for m in mods]
+    try:
+        from torch.func import functional_call
+
+        from .cost import _FlashSDPA, _meta_state
+
+        x = torch.empty((1,) + tuple(in_shape), dtype=in_dtype, device="meta")
+        with torch.no_grad(), _FlashSDPA():
+            functional_call(layer, _meta_state(layer, None), (x,))
+    except Exception:  # noqa: BLE001 - an un-runnable layer: assume one token per sample
+        pass
+    finally:
+        for h in hooks:
+            h.remove()
+    # a Linear applied functionally (madnn's fused ops.linear) fires no hook: tokens per sample
+    # are then the leading dims of the layer input ([S, H] -> S)
+    fallback = 1
+    for d in tuple(in_shape)[:-1]:
+        fallback *= int(d)
+    return [(m.in_features, m.out_features, toks.get(id(m), fallback)) for m in mods]
+
+
+def _tp_candidate(spine: Spine, costs, dp, tp, B, cfg, hw: Machine, opt, cap, example_shape=(), example_dtype=None):
+    """dp x tp with row-parallel sharding of the large Linears (``parallel.tp.shard_linears``):
+    their GEMM time divides by tp; each adds an output all-reduce (forward) and an input-grad
+    all-gather (backward) over the TP group on the critical path."""
+    min_params = int(cfg.extra.get("tp_min_params", 1 << 20))
+    per_replica = max(B // dp, 1)
+    compute = 0.0
+    comm = 0.0
+    sharded_params = 0
+    total_params = sum(c.params for c in costs)
+    link_bw = hw.link_gbps * 1e9 * max(min(hw.links, tp - 1), 1) * hw.allreduce_eff
+    for i, (layer, c) in enumerate(zip(spine.layers, costs)):
+        if i > 0:
+            in_shape, in_dtype = costs[i - 1].out_shape, costs[i - 1].out_dtype or torch.float32
+        else:
+            in_shape, in_dtype = tuple(example_shape), example_dtype
+        lin = _tp_linears(layer, tp, min_params, in_shape, in_dtype)
+        gflops = sum(2.0 * a * b * t for a, b, t in lin)
+        g = min(gflops / c.flops, 1.0) if c.flops > 0 else 0.0
+        compute += c.time_s * per_replica * ((1 - g) + g / tp)
+        for a, b, tokens in lin:
+            sharded_params += a * b
+            nb_out = tokens * b * 2.0 * per_replica
+            nb_in = tokens * a * 2.0 * per_replica
+            comm += 2.0 * (tp - 1) / tp * nb_out / link_bw + (tp - 1) / tp * nb_in / link_bw \
+                + 2 * hw.collective_latency_us * 1e-6
+    if sharded_params == 0:
+        return None
+    local_params = total_params - sharded_params + sharded_params / tp
+    from .cost import param_state_bytes
+
+    act = sum(c.act_bytes for c in costs) * per_replica
+    mem = (param_state_bytes(local_params, opt) + act) / 1e9
+    grad_dp = 0.0
+    if dp > 1:
+        bwd = [c.bwd_s * per_replica for c in costs]
+        grad_dp = dp_exposed_s(bwd, [c.params * _reduce_bytes(cfg) / tp for c in costs], dp, hw,
+                               cfg.bucket_mb * 2**20)
+    step = compute + comm + grad_dp
+    return {"strategy": "tp", "dp": dp, "pp": 1, "tp": tp, "M": 1, "V": 1, "schedule": "none", "ckpt": False,
+            "bounds": [0, len(costs)], "step_s": step, "compute_s": compute, "comm_s": comm + grad_dp,
+            "bubble": 0.0, "mem_gb": mem, "mem_list": [mem], "fits": mem * 1e9 <= cap}
+
+
+__all__ = ["Plan", "plan_model", "trace", "estimate", "infer_example_input", "find_block_list", "dp_exposed_s"]

@@ -184,6 +184,101 @@ def measure(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], i
     return costs
 
 
+def layer_signature(layer: nn.Module) -> tuple:
+    """Layers with equal signatures (type + parameter shapes/dtypes) cost the same: the
+    repeated blocks of a transformer are measured once."""
+    return (type(layer).__name__,
+            tuple((n, tuple(p.shape), str(p.dtype)) for n, p in layer.named_parameters(remove_duplicate=False)))
+
+
+def _replica(layer: nn.Module, device, dtype):
+    """A private, initialised copy of ``layer`` on ``device`` in madnn's compute layout
+    (compute-dtype weights, fp32 norm parameters, channels_last convolutions)."""
+    import copy
+
+    from ..api import _has_conv, _norm_param_ids
+
+    rep = copy.deepcopy(layer)
+    if any(t.is_meta for t in list(rep.parameters()) + list(rep.buffers())):
+        from ..parallel.pp import materialize_
+
+        materialize_(rep, device)
+    rep.to(device)
+    keep = _norm_param_ids(rep)
+    with torch.no_grad():
+        for p in rep.parameters():
+            if p.is_floating_point() and id(p) not in keep and dtype is not None:
+                p.data = p.data.to(dtype)
+    cl = device.type == "cuda" and _has_conv(rep)
+    if cl:
+        rep.to(memory_format=torch.channels_last)
+    rep.train()
+    return rep, cl
+
+
+def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: Optional[int] = None,
+                   dtype: Optional[torch.dtype] = torch.bfloat16, iters: int = 3,
+                   device: Optional[torch.device] = None) -> List[LayerCost]:
+    """Replace the analytic times of ``costs`` with HIP-event timings on this GPU.
+
+    Every DISTINCT layer (:func:`layer_signature` + input shape) is copied once onto the
+    device -- a meta-device layer is materialised -- and its forward and forward+backward
+    are timed at ``batch`` samples (default: the example input's batch), so a 24-block
+    transformer costs three measurements and an 8B model never needs to exist whole.  The
+    input of layer i is a random tensor of layer i-1's analytic output shape.  Returns
+    ``costs`` unchanged without a GPU.  This is the working version of the reference's
+    dead ``comm_speed`` probe (datamodule.lua:280-303)."""
+    if not torch.cuda.is_available():
+        return costs
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    b = int(batch or max(example_input.shape[0], 1))
+    cache = {}
+    for i, (layer, c) in enumerate(zip(spine.layers, costs)):
+        if i == 0:
+            in_key = ("input", tuple(example_input.shape[1:]), str(example_input.dtype))
+        else:
+            in_key = (tuple(costs[i - 1].out_shape), str(costs[i - 1].out_dtype))
+        key = (layer_signature(layer), in_key)
+        if key not in cache:
+            rep, cl = _replica(layer, dev, dtype)
+            if i == 0:
+                idx = torch.arange(b) % max(example_input.shape[0], 1)
+                x = example_input[idx].to(dev)
+                if x.is_floating_point():
+                    x = x.to(dtype or x.dtype)
+            else:
+                odt = costs[i - 1].out_dtype or dtype
+                if odt is not None and not odt.is_floating_point:
+                    x = torch.zeros((b,) + tuple(costs[i - 1].out_shape), dtype=odt, device=dev)
+                else:
+                    x = torch.randn((b,) + tuple(costs[i - 1].out_shape), dtype=odt, device=dev)
+            if cl and x.dim() == 4:
+                x = x.contiguous(memory_format=torch.channels_last)
+            xin = x.detach().requires_grad_(x.is_floating_point())
+            for _ in range(2):
+                y = rep(xin)
+                if y.requires_grad:
+                    y.backward(torch.ones_like(y))
+            start, mid, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            fw = bw = 0.0
+            for _ in range(iters):
+                start.record()
+                y = rep(xin)
+                mid.record()
+                if y.requires_grad:
+                    y.backward(torch.ones_like(y))
+                end.record()
+                end.synchronize()
+                fw += start.elapsed_time(mid)
+                bw += mid.elapsed_time(end)
+            cache[key] = (fw / iters / 1e3 / b, bw / iters / 1e3 / b)
+            del rep, xin, y
+        c.fwd_s, c.bwd_s = cache[key]
+        c.measured = True
+    torch.cuda.empty_cache()
+    return costs
+
+
 def param_state_bytes(params: int, optimizer: str = "adam", compute_bytes: int = 2) -> float:
     """Bytes per parameter in madnn's layout: bf16 model + bf16 grad + fp32 master
     + fp32 flat reduce buffer + optimizer state (SGD momentum 4 B, Adam 8 B)."""

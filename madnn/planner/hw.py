@@ -1,11 +1,13 @@
 """MI355X machine model used by the cost model.
 
-Defaults are the measured / guide numbers for one MI355X (gfx950) and its
-xGMI mesh (MI355X_MICROARCH.md: 6.3 TB/s achievable HBM3E, ~2.5 PF dense
-bf16 MFMA; task spec: 7 xGMI links x ~153 GB/s per GPU).  ``load()`` overlays
-a JSON file written by ``madnn.comm.bench`` / ``madnn.planner.calibrate``
-(env ``MADNN_HW_PROFILE``) so the planner prices collectives with numbers
-measured on the actual node rather than datasheet values.
+Defaults are the guide numbers for one MI355X (gfx950) and its xGMI mesh
+(MI355X_MICROARCH.md: 6.3 TB/s achievable HBM3E, ~2.5 PF dense bf16 MFMA; task
+spec: 7 xGMI links x ~153 GB/s per GPU).  ``load()`` overlays, in order of
+precedence, the JSON profile named by ``MADNN_HW_PROFILE``, the node's own
+profile written by ``madnn.planner.calibrate`` (``~/.cache/madnn/hw_profile.json``),
+or the profile shipped in-tree (``madnn/tuning/hw_mi355x.json``, measured on an
+MI355X box with ``calibrate``), so the planner prices compute and collectives
+with measured numbers rather than datasheet values.
 """
 from __future__ import annotations
 
@@ -27,6 +29,8 @@ class Machine:
     p2p_gbps: float = 60.0           # achievable point-to-point over one link (send/recv)
     collective_latency_us: float = 25.0
     kernel_launch_us: float = 4.0
+    calibrated: str = ""             # when / at what world size the profile was measured ("" = datasheet)
+    source: str = "defaults"
 
     def allreduce_s(self, nbytes: float, world: int) -> float:
         """Ring all-reduce time: 2(W-1)/W * bytes over the per-GPU xGMI bandwidth RCCL spreads on.
@@ -44,23 +48,43 @@ class Machine:
 
 
 _CACHE = {}
+SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "hw_mi355x.json")
+
+
+def default_profile_path() -> str:
+    return os.path.join(os.path.expanduser("~"), ".cache", "madnn", "hw_profile.json")
+
+
+def profile_candidates():
+    return [p for p in (os.environ.get("MADNN_HW_PROFILE"), default_profile_path(), SHIPPED) if p]
+
+
+def invalidate() -> None:
+    _CACHE.clear()
 
 
 def load() -> Machine:
-    path = os.environ.get("MADNN_HW_PROFILE")
-    key = path or ""
+    """The machine model: the first existing profile of :func:`profile_candidates` over the
+    defaults.  A single-GPU profile leaves the link numbers at their defaults; one measured
+    with several ranks overrides them too."""
+    paths = profile_candidates()
+    key = tuple(paths)
     if key in _CACHE:
         return _CACHE[key]
     m = Machine()
-    if path and os.path.exists(path):
-        with open(path) as f:
-            for k, v in json.load(f).items():
-                if hasattr(m, k):
-                    setattr(m, k, type(getattr(m, k))(v))
+    for path in paths:
+        if os.path.exists(path):
+            with open(path) as f:
+                for k, v in json.load(f).items():
+                    if hasattr(m, k) and k != "source":
+                        setattr(m, k, type(getattr(m, k))(v))
+            m.source = path
+            break
     _CACHE[key] = m
     return m
 
 
 def dump(m: Machine, path: str) -> None:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
     with open(path, "w") as f:
         json.dump(asdict(m), f, indent=2)

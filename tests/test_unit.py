@@ -88,33 +88,39 @@ def test_plan_buckets_alignment_and_cap():
     assert bs == [64, 112, 16]
 
 
-@pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
-@pytest.mark.parametrize("S,M", [(2, 4), (4, 4), (4, 8), (3, 2)])
-def test_pipeline_programs_consistent(kind, S, M):
-    progs = [nr.pipeline_program(kind, s, S, M) for s in range(S)]
-    for s, prog in enumerate(progs):
-        f = [a for op, a, _ in prog if op == "FWD"]
-        b = [a for op, a, _ in prog if op == "BWD"]
-        assert sorted(f) == list(range(M)) and sorted(b) == list(range(M))
-        for m in range(M):  # a microbatch's backward follows its forward
-            assert [op for op, a, _ in prog].index("FWD") <= [i for i, (op, a, _) in enumerate(prog)
-                                                               if op == "BWD" and a == m][0]
-    # sends of stage s and receives of stage s+1 pair up in the same order
-    for s in range(S - 1):
-        sends = [a for op, a, b in progs[s] if op in ("SEND_FWD", "SEND_FWD_RECV_BWD")]
-        recvs = [a for op, a, b in progs[s + 1] if op == "RECV_FWD"] + \
-                [b for op, a, b in progs[s + 1] if op == "SEND_BWD_RECV_FWD"]
-        assert sorted(sends) == sorted(recvs) == list(range(M))
-    if kind == "1f1b":  # in-flight activations bounded by S - s
-        for s, prog in enumerate(progs):
-            live = peak = 0
-            for op, a, b in prog:
-                if op == "FWD":
-                    live += 1
-                    peak = max(peak, live)
-                elif op == "BWD":
-                    live -= 1
-            assert peak <= min(S - s, M)
+@pytest.mark.parametrize("kind,V", [("gpipe", 1), ("1f1b", 1), ("interleaved", 2), ("interleaved", 3)])
+@pytest.mark.parametrize("S,M", [(2, 4), (4, 4), (4, 8), (3, 6), (2, 2)])
+def test_pipeline_orders_deadlock_free_and_fifo(kind, V, S, M):
+    """Every rank's compute order against one-directional FIFO channels with non-blocking
+    sends: no deadlock, each channel received in send order (what lets the engine post all
+    receives up front), every (chunk, microbatch) forward and backward exactly once."""
+    from madnn.parallel.pp import simulate_schedule
+
+    for s in range(S):
+        order = nr.pipeline_order(kind, s, S, M, V)
+        for op in ("F", "B"):
+            assert sorted((c, m) for o, c, m in order if o == op) == [(c, m) for c in range(V) for m in range(M)]
+    r = simulate_schedule(kind, S, M, V)
+    if kind == "1f1b":
+        assert r["peak_inflight"] == [min(S - s, M) for s in range(S)]
+        assert r["bubble"] == pytest.approx((S - 1) / (M + S - 1), abs=1e-9)
+
+
+def test_interleaving_shrinks_the_bubble():
+    from madnn.parallel.pp import pipeline_bubble
+
+    b1 = pipeline_bubble("1f1b", 4, 16, 1)
+    b2 = pipeline_bubble("interleaved", 4, 16, 2)
+    b3 = pipeline_bubble("interleaved", 4, 16, 3)
+    assert b1 == pytest.approx(3 / 19)
+    assert b3 < b2 < b1 and b2 < 0.6 * b1
+
+
+def test_pipeline_order_rejects_bad_interleave():
+    with pytest.raises(ValueError):
+        nr.pipeline_order("interleaved", 0, 4, 6, 2)  # M % S != 0
+    with pytest.raises(ValueError):
+        nr.pipeline_order("1f1b", 0, 4, 8, 2)
 
 
 def test_order_hash():
@@ -239,11 +245,105 @@ def test_planner_choices():
         m = Llama(llama_config("llama3-8b"))
     ex = torch.zeros(1, 4096, dtype=torch.long)
     p = plan_model(m, Config.from_env(strategy="auto", global_batch=64), 8, example_input=ex)
-    assert p.dp * p.pp == 8 and max(p.est_mem_gb) <= 288 * 0.85
+    assert p.dp * p.pp * p.tp == 8 and max(p.est_mem_gb) <= 288 * 0.85
     p = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, global_batch=64), 4, example_input=ex)
     assert (p.dp, p.pp) == (1, 4) and p.bounds[0] == 0 and p.bounds[-1] == 34
     p = plan_model(m, Config.from_env(strategy="dp_pp", pp_stages=2, global_batch=64), 8, example_input=ex)
     assert (p.dp, p.pp) == (4, 2)
+
+
+def test_planner_ws8_table_covers_all_strategies():
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.planner import plan_model
+
+    with torch.device("meta"):
+        m = GPT2(gpt2_config("gpt2-medium"))
+    ex = torch.zeros(1, 1024, dtype=torch.long)
+    p = plan_model(m, Config.from_env(strategy="auto", global_batch=128), 8, example_input=ex)
+    kinds = {c["strategy"] for c in p.candidates}
+    assert kinds >= {"dp", "pp", "dp_pp", "tp"}, kinds
+    assert "| tp |" in p.table() and "| dp_pp |" in p.table()
+    assert not p.measured  # no GPU here: analytic costs
+
+
+def test_planner_interleaved_plan_shape():
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.planner import plan_model
+
+    with torch.device("meta"):
+        m = GPT2(gpt2_config("gpt2-medium"))
+    ex = torch.zeros(1, 1024, dtype=torch.long)
+    p = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, schedule="interleaved", global_batch=64), 4,
+                   example_input=ex)
+    assert p.virtual == 2 and p.schedule == "interleaved" and len(p.bounds) == 4 * 2 + 1
+    assert p.microbatches % 4 == 0
+    q = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, global_batch=64), 4, example_input=ex)
+    # same work, smaller bubble
+    assert p.est_step_s < q.est_step_s
+
+
+def test_measured_costs_change_the_placement():
+    """The planner consumes measured layer times: with GPT-2 medium at 8 GPUs, analytic costs
+    and costs that make compute 100x cheaper (comm-dominated) must not pick the same layout,
+    and skewed per-layer measurements move the pipeline stage boundaries."""
+    import copy
+
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.planner import estimate, plan_model, trace
+
+    with torch.device("meta"):
+        m = GPT2(gpt2_config("gpt2-medium"))
+    ex = torch.zeros(1, 1024, dtype=torch.long)
+    cfg = Config.from_env(strategy="auto", global_batch=16)
+    base = estimate(trace(m), ex)
+    p0 = plan_model(m, cfg, 8, example_input=ex, costs=copy.deepcopy(base))
+    fast = copy.deepcopy(base)
+    for c in fast:
+        c.fwd_s, c.bwd_s, c.measured = c.fwd_s / 100, c.bwd_s / 100, True
+    p1 = plan_model(m, cfg, 8, example_input=ex, costs=fast)
+    assert p1.measured and not p0.measured
+    assert (p0.strategy, p0.dp, p0.pp, p0.tp) != (p1.strategy, p1.dp, p1.pp, p1.tp)
+    cfg_pp = Config.from_env(strategy="pp", pp_stages=4, global_batch=64)
+    q0 = plan_model(m, cfg_pp, 4, example_input=ex, costs=copy.deepcopy(base))
+    skew = copy.deepcopy(base)
+    for c in skew[1:6]:  # the first blocks measure 3x slower than the model says
+        c.fwd_s, c.bwd_s, c.measured = c.fwd_s * 3, c.bwd_s * 3, True
+    q1 = plan_model(m, cfg_pp, 4, example_input=ex, costs=skew)
+    assert q1.bounds != q0.bounds and q1.bounds[1] < q0.bounds[1]
+
+
+def test_dp_exposed_timeline():
+    from madnn.planner import dp_exposed_s
+    from madnn.planner.hw import Machine
+
+    hw = Machine()
+    mb = 64 * 2**20
+    ar = hw.allreduce_s(mb, 8)
+    # all gradients land at the very end (one layer): the whole reduction is exposed
+    assert dp_exposed_s([1e-3], [mb], 8, hw, mb) == pytest.approx(ar)
+    # ten equal layers, one bucket each, backward much longer than a reduction: only the last
+    exp = dp_exposed_s([10 * ar] * 10, [mb] * 10, 8, hw, mb)
+    assert exp == pytest.approx(ar)
+    # comm-bound: reductions queue up behind each other
+    exp = dp_exposed_s([ar / 10] * 10, [mb] * 10, 8, hw, mb)
+    assert exp == pytest.approx(10 * ar - 9 * ar / 10, rel=1e-6)
+    assert dp_exposed_s([1.0], [mb], 1, hw, mb) == 0.0
+
+
+def test_hw_profile_precedence(tmp_path, monkeypatch):
+    import json as _json
+
+    from madnn.planner import hw
+
+    prof = tmp_path / "p.json"
+    prof.write_text(_json.dumps({"hbm_tbps": 4.2, "bf16_tflops": 901.0, "calibrated": "test"}))
+    monkeypatch.setenv("MADNN_HW_PROFILE", str(prof))
+    hw.invalidate()
+    m = hw.load()
+    assert m.hbm_tbps == 4.2 and m.bf16_tflops == 901.0 and m.source == str(prof)
+    monkeypatch.delenv("MADNN_HW_PROFILE")
+    hw.invalidate()
+    assert hw.load().source in (hw.default_profile_path(), hw.SHIPPED, "defaults")
 
 
 # ---------------------------------------------------------------- nn modules
