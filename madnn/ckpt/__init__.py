@@ -40,7 +40,8 @@ def _st():
 
 
 def _named_state(engine) -> Dict[str, torch.Tensor]:
-    """name -> fp32 value of every parameter this rank owns, plus buffers."""
+    """name -> fp32 FULL value of every parameter this rank holds, plus buffers.  Collective
+    for tensor-parallel shards (gathered over their TP group, with or without a DP space)."""
     from ..parallel.dp import DataParallel
     from ..parallel.pp import PipelineEngine
 
@@ -61,30 +62,74 @@ def _named_state(engine) -> Dict[str, torch.Tensor]:
             out.setdefault("__aliases__", {})[name] = seen[id(p)]
             continue
         seen[id(p)] = name
-        if space is not None and id(p) in space.param_info:
-            out[name] = space.master_view(p).detach().float().cpu().contiguous()
-        else:
-            out[name] = _full_param(module, name, p).detach().float().cpu().contiguous()
+        v = space.master_view(p) if space is not None and id(p) in space.param_info else p
+        out[name] = _full_value(module, name, v.detach().float()).cpu().contiguous()
     for name, b in module.named_buffers():
         out[name] = b.detach().cpu().clone()
     return out
 
 
-def _full_param(module, name, p):
-    """Gather TP-sharded weights back to their full shape."""
-    from ..parallel.tp import ColumnParallelLinear, RowParallelLinear, _gather_last, _world
+def _tp_owner(module, name):
+    """(owner layer, attribute, shard dim) for a parameter sharded by tensor parallelism, else None."""
+    from ..parallel.tp import ColumnParallelLinear, RowParallelLinear, _world
 
     owner_name, _, attr = name.rpartition(".")
-    owner = module.get_submodule(owner_name) if owner_name else module
+    try:
+        owner = module.get_submodule(owner_name) if owner_name else module
+    except AttributeError:
+        return None
     if isinstance(owner, RowParallelLinear) and attr == "weight" and _world(owner.group) > 1:
-        return _gather_last(p.detach(), owner.group)
+        return owner, attr, 1
     if isinstance(owner, ColumnParallelLinear) and _world(owner.group) > 1:
-        t = p.detach()
-        return _gather_last(t.t().contiguous(), owner.group).t() if attr == "weight" else _gather_last(t, owner.group)
-    return p
+        return owner, attr, 0
+    return None
+
+
+def _full_value(module, name, t: torch.Tensor) -> torch.Tensor:
+    """Gather a TP shard (any tensor shaped like the local parameter: value or optimizer state)
+    to the full parameter shape; other tensors pass through."""
+    own = _tp_owner(module, name)
+    if own is None:
+        return t
+    owner, _attr, dim = own
+    from .. import comm
+    from ..parallel.tp import _world
+
+    w = _world(owner.group)
+    t = t.contiguous()
+    buf = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    if dim == 0:
+        comm.all_gather_into(buf, t, group=owner.group)
+        return buf
+    tt = t.t().contiguous()  # row-parallel weight [out, in/W]: gather the in-dim as rows
+    buf = torch.empty((w * tt.shape[0], tt.shape[1]), dtype=t.dtype, device=t.device)
+    comm.all_gather_into(buf, tt, group=owner.group)
+    return buf.t().contiguous()
+
+
+def _local_value(module, name, full: torch.Tensor, local_shape) -> torch.Tensor:
+    """This rank's shard of a FULL tensor (inverse of :func:`_full_value`)."""
+    own = _tp_owner(module, name)
+    if own is None or tuple(full.shape) == tuple(local_shape):
+        return full
+    owner, _attr, dim = own
+    from ..parallel.tp import _rank
+
+    k = local_shape[dim]
+    r = _rank(owner.group)
+    return full.narrow(dim, r * k, k)
+
+
+def _full_param(module, name, p):
+    """Gather TP-sharded weights back to their full shape."""
+    return _full_value(module, name, p.detach())
 
 
 def _optim_state(engine, optimizer) -> Dict[str, Dict[str, torch.Tensor]]:
+    """Per-parameter optimizer state under the parameters' names, TP shards gathered to the
+    full shape (collective: every rank calls it with the same parameter order)."""
+    from ..parallel.dp import DataParallel
+
     if optimizer is None:
         return {}
     sd = optimizer.state_dict()
@@ -95,13 +140,20 @@ def _optim_state(engine, optimizer) -> Dict[str, Dict[str, torch.Tensor]]:
             idx2p[k] = p
             k += 1
     names = _param_names(engine)
+    module = engine.module if isinstance(engine, DataParallel) else engine
     out = {}
-    for i, st in sd["state"].items():
+    for i in sorted(sd["state"], key=int):
+        st = sd["state"][i]
         p = idx2p.get(int(i))
         if p is None or id(p) not in names:
             continue
-        out[names[id(p)]] = {kk: (v.detach().cpu() if isinstance(v, torch.Tensor) else torch.tensor(v))
-                             for kk, v in st.items()}
+        name = names[id(p)]
+        ent = {}
+        for kk, v in st.items():
+            if isinstance(v, torch.Tensor) and tuple(v.shape) == tuple(p.shape) and isinstance(module, nn.Module):
+                v = _full_value(module, name, v.to(p.device))
+            ent[kk] = v.detach().cpu() if isinstance(v, torch.Tensor) else torch.tensor(v)
+        out[name] = ent
     return out
 
 
@@ -225,11 +277,11 @@ def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
         for n, p in params.items():
             if n not in full:
                 continue
-            v = full[n]
+            v = _local_value(module, n, full[n], tuple(p.shape))
             if space is not None and id(p) in space.param_info:
                 space.master_view(p).copy_(v.to(space.master_view(p).device))
             else:
-                _load_param(module, n, p, v)
+                p.copy_(v.to(p.device))
         if space is not None:
             space.sync_model_from_master()
         bufs = dict(engine.named_buffers()) if isinstance(engine, PipelineEngine) else dict(module.named_buffers())
@@ -245,7 +297,9 @@ def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
             for p in g["params"]:
                 n = names.get(id(p))
                 if n in ost:
-                    new_state[k] = ost[n]
+                    new_state[k] = {kk: (_local_value(module, n, v, tuple(p.shape))
+                                         if isinstance(v, torch.Tensor) and v.dim() == p.dim() and v.dim() > 0 else v)
+                                    for kk, v in ost[n].items()}
                 k += 1
         sd["state"] = new_state
         optimizer.load_state_dict(sd)
@@ -258,19 +312,3 @@ def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
         if "cuda" in rng and torch.cuda.is_available():
             torch.cuda.set_rng_state(rng["cuda"])
     return meta
-
-
-def _load_param(module, name, p, v):
-    from ..parallel.tp import ColumnParallelLinear, RowParallelLinear
-
-    owner_name, _, attr = name.rpartition(".")
-    owner = module.get_submodule(owner_name) if owner_name else module
-    if isinstance(owner, (RowParallelLinear, ColumnParallelLinear)) and tuple(v.shape) != tuple(p.shape):
-        if attr == "weight":
-            owner.load_full(v.to(p.device), None)
-        else:
-            r = torch.distributed.get_rank(owner.group) if torch.distributed.is_initialized() else 0
-            k = p.numel()
-            p.copy_(v[r * k:(r + 1) * k].to(p.device))
-        return
-    p.copy_(v.to(p.device))

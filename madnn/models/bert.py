@@ -77,6 +77,9 @@ class BertLayer(nn.Module):
         self.ffn_norm = FusedLayerNorm(cfg.hidden, eps=cfg.layer_norm_eps)
         self.drop = nn.Dropout(cfg.dropout)
 
+    def tensor_parallel_pairs(self):
+        return [(("fc1",), "fc2")]
+
     def forward(self, x):
         y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
         z, _ = self.ffn_norm(self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y)))), residual=y)

@@ -73,6 +73,9 @@ class GPT2MLP(nn.Module):
     def forward(self, x):
         return self.drop(linear(self.c_proj, linear(self.c_fc, x, gelu=True)))
 
+    def tensor_parallel_pairs(self):
+        return [(("c_fc",), "c_proj")]
+
 
 class GPT2Block(nn.Module):
     def __init__(self, cfg: GPT2Config):

@@ -26,6 +26,10 @@ class MLP(nn.Module):
     def forward(self, x):
         return self.fc2(self.act(self.fc1(x.flatten(1))))
 
+    def tensor_parallel_pairs(self):
+        """fc1 column-parallel -> elementwise act -> fc2 row-parallel (one all-reduce)."""
+        return [(("fc1",), "fc2")]
+
 
 class CifarConvNet(nn.Module):
     def __init__(self, num_classes: int = 10, dropout: float = 0.5):

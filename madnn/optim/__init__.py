@@ -35,6 +35,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self.bucket_steps: Dict[int, int] = {}
         self._dscale: Optional[torch.Tensor] = None
         self._pending_load = None
+        self.norm_spec = None              # (groups, skip params) for clipping when no engine provides it
 
     # ----------------------------------------------------------------- binding
     def bind(self, space: FlatParamSpace):
@@ -79,7 +80,7 @@ class _FlatOptimizer(torch.optim.Optimizer):
             self.grad_source.finalize_grads()
         flats = [self._grads(bk) for bk in self.space.buckets]
         self._grads_cached = flats
-        groups, skip = ([], [])
+        groups, skip = self.norm_spec or ([], [])
         if self.grad_source is not None and hasattr(self.grad_source, "norm_reduction"):
             groups, skip = self.grad_source.norm_reduction()
         if not groups and not skip:

@@ -270,6 +270,11 @@ class DataParallel(nn.Module):
                 out["busbw_gbps"] = 2.0 * (self.world - 1) / self.world * nbytes / (ms * 1e-3) / 1e9
         return out
 
+    def norm_reduction(self):
+        """Gradient-norm reduction spec for clipping: replicas hold identical reduced gradients
+        (nothing to sum); a tensor-parallel inner layout sets ``_norm_spec``."""
+        return getattr(self, "_norm_spec", ([], []))
+
     def after_step(self):
         """Called by the fused optimizer after each step: the sync="params" period, then the
         robustness hooks (fault injection, collective-order check)."""

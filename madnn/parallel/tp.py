@@ -271,21 +271,112 @@ class MPBaseReshape(_Reshape):
 # --------------------------------------------------------------------------
 # strategy="tp": shard the large Linear layers of an arbitrary model
 # --------------------------------------------------------------------------
-def shard_linears(model: nn.Module, group=None, min_params: int = 1 << 20) -> int:
-    """Replace every ``nn.Linear`` with >= ``min_params`` weights and a TP-divisible input dim by a
-    row-parallel copy holding this rank's shard (weights taken from the original layer)."""
+_ELEMENTWISE = (nn.ReLU, nn.GELU, nn.Tanh, nn.SiLU, nn.Sigmoid, nn.Dropout, nn.Identity, nn.LeakyReLU, nn.ELU)
+
+
+def _eligible(m: nn.Module, w: int, min_params: int, dim: str) -> bool:
+    if type(m) is not nn.Linear or m.weight.numel() < min_params:
+        return False
+    return (m.in_features if dim == "in" else m.out_features) % w == 0
+
+
+def _column(child: nn.Linear, group, gather_output: bool) -> "ColumnParallelLinear":
+    new = ColumnParallelLinear(child.in_features, child.out_features, bias=child.bias is not None,
+                               gather_output=gather_output, group=group, device=child.weight.device,
+                               dtype=child.weight.dtype)
+    new.load_full(child.weight.detach(), child.bias.detach() if child.bias is not None else None)
+    return new
+
+
+def _row(child: nn.Linear, group, input_is_parallel: bool) -> "RowParallelLinear":
+    new = RowParallelLinear(child.in_features, child.out_features, bias=child.bias is not None,
+                            input_is_parallel=input_is_parallel, group=group, device=child.weight.device,
+                            dtype=child.weight.dtype)
+    new.load_full(child.weight.detach(), child.bias.detach() if child.bias is not None else None)
+    return new
+
+
+def _pairs_of(module: nn.Module):
+    """Column -> row pairs of a module: declared by ``tensor_parallel_pairs()`` (madnn's MLPs:
+    ``[(("c_fc",), "c_proj")]``, gated MLPs ``[(("gate_proj", "up_proj"), "down_proj")]``), or
+    found in an ``nn.Sequential`` as Linear, elementwise activations, Linear."""
+    if hasattr(module, "tensor_parallel_pairs"):
+        return [(tuple(cols), row) for cols, row in module.tensor_parallel_pairs()]
+    pairs = []
+    if isinstance(module, nn.Sequential):
+        names = [n for n, _ in module.named_children()]
+        mods = [m for _, m in module.named_children()]
+        i = 0
+        while i < len(mods):
+            if type(mods[i]) is nn.Linear:
+                j = i + 1
+                while j < len(mods) and isinstance(mods[j], _ELEMENTWISE):
+                    j += 1
+                if j < len(mods) and type(mods[j]) is nn.Linear and j > i:
+                    pairs.append(((names[i],), names[j]))
+                    i = j + 1
+                    continue
+            i += 1
+    return pairs
+
+
+def shard_linears(model: nn.Module, group=None, min_params: int = 1 << 20, _tied=None) -> int:
+    """Shard the large Linears of ``model`` over ``group`` (returns how many were replaced).
+
+    Column -> row PAIRS (:func:`_pairs_of`) become the Megatron pattern: the column-parallel
+    layer keeps its output sharded (no gather), the elementwise activation runs on the shard,
+    the row-parallel layer consumes the shard directly -- ONE all-reduce per pair forward
+    (and one in backward, for the replicated input), no activation gather/scatter.  Every
+    other eligible Linear becomes row-parallel on its own (scatter its input, all-reduce its
+    output).  Weights are taken from the original layers.  A Linear whose weight is TIED to
+    another module (GPT-2's lm_head = wte) stays replicated, keeping the tie."""
     w = _world(group)
+    if _tied is None:
+        cnt = {}
+        for _, p in model.named_parameters(remove_duplicate=False):
+            cnt[id(p)] = cnt.get(id(p), 0) + 1
+        _tied = {k for k, v in cnt.items() if v > 1}
     n = 0
+    paired = set()
+    for cols, row in _pairs_of(model):
+        cm = [getattr(model, c, None) for c in cols]
+        rm = getattr(model, row, None)
+        if rm is None or any(c is None for c in cm):
+            continue
+        if any(id(x.weight) in _tied for x in cm + [rm] if hasattr(x, "weight")):
+            continue
+        if all(_eligible(c, w, 0, "out") for c in cm) and _eligible(rm, w, 0, "in") and \
+                sum(c.weight.numel() for c in cm) + rm.weight.numel() >= min_params:
+            for name, c in zip(cols, cm):
+                setattr(model, name, _column(c, group, gather_output=False))
+                paired.add(name)
+            setattr(model, row, _row(rm, group, input_is_parallel=True))
+            paired.add(row)
+            n += len(cols) + 1
     for name, child in list(model.named_children()):
-        if type(child) is nn.Linear and child.weight.numel() >= min_params and child.in_features % w == 0:
-            new = RowParallelLinear(child.in_features, child.out_features, bias=child.bias is not None,
-                                    group=group, device=child.weight.device, dtype=child.weight.dtype)
-            new.load_full(child.weight.detach(), child.bias.detach() if child.bias is not None else None)
-            setattr(model, name, new)
+        if name in paired:
+            continue
+        if _eligible(child, w, min_params, "in") and id(child.weight) not in _tied:
+            setattr(model, name, _row(child, group, input_is_parallel=False))
             n += 1
         else:
-            n += shard_linears(child, group, min_params)
+            n += shard_linears(child, group, min_params, _tied)
     return n
+
+
+def tp_norm_spec(model: nn.Module, group):
+    """(groups, params to skip) for global-norm clipping under TP: shards are disjoint across
+    the TP group (sum everything), replicated parameters count on TP rank 0 only."""
+    if _world(group) == 1:
+        return [], []
+    sharded = set()
+    for m in model.modules():
+        if isinstance(m, ColumnParallelLinear):
+            sharded.update(id(p) for p in m.parameters(recurse=False))
+        elif isinstance(m, RowParallelLinear):
+            sharded.add(id(m.weight))
+    skip = [] if _rank(group) == 0 else [p for p in model.parameters() if p.requires_grad and id(p) not in sharded]
+    return [group], skip
 
 
 def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
@@ -333,6 +424,9 @@ def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
         engine, optimizer = _distribute_dp(model, optimizer, cfg, dev, group=groups.dp_group,
                                            src_rank=groups.dp_ranks[0])
         engine.groups = groups
+        engine._norm_spec = tp_norm_spec(model, groups.tp_group)
         return engine, optimizer
     model.groups = groups
+    if optimizer is not None and hasattr(optimizer, "norm_spec"):
+        optimizer.norm_spec = tp_norm_spec(model, groups.tp_group)
     return model, optimizer

@@ -5,7 +5,14 @@ For every RCCL kernel: which HIP queue/stream it ran on and how much of its life
 overlapped kernels on OTHER streams (the backward's compute kernels).  Evidence for
 "RCCL all-reduce on the comm stream interleaved with backward kernels".
 
-usage: comm_overlap.py <kernel_trace.csv> [--out file.md] [--max-rows 40]
+usage: comm_overlap.py <kernel_trace.csv> [--rccl-api rccl_api_trace.csv] [--step-kernel REGEX]
+                        [--out file.md] [--max-rows 40]
+
+With ``--rccl-api`` (rocprofv3 ``--rccl-trace``) it also places every ncclAllReduce CALL
+inside its training step: which host thread issued it (the autograd engine thread = from a
+gradient hook, mid-backward) and how much of that step's compute-stream kernel time still
+ran after the call (work the reduction can overlap).  At world size 1 RCCL launches no
+kernel for an in-place all-reduce, so the API trace is the evidence there.
 """
 import argparse
 import csv
@@ -27,6 +34,9 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--out", default=None)
     ap.add_argument("--max-rows", type=int, default=40)
+    ap.add_argument("--rccl-api", default=None)
+    ap.add_argument("--step-kernel", default=r"adam_kernel|sgd_kernel",
+                    help="kernel name regex marking each step's optimizer (step boundary)")
     a = ap.parse_args()
     rows = []
     for r in csv.DictReader(open(a.csv)):
@@ -83,10 +93,47 @@ def main():
         ex = ex if len(ex) < 50 else ex[:47] + "..."
         n = n if len(n) < 50 else n[:47] + "..."
         lines.append(f"| {(s - t0) / 1e6:.3f} | {d / 1e3:.1f} | {q} | {u / 1e3:.1f} | {k} | `{ex}` | `{n}` |")
+    if a.rccl_api:
+        lines += _api_section(a, rows)
     txt = "\n".join(lines) + "\n"
     print(txt)
     if a.out:
         open(a.out, "w").write(txt)
+
+
+def _api_section(a, rows):
+    calls = []
+    for r in csv.DictReader(open(a.rccl_api)):
+        calls.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"], r["Thread_Id"]))
+    main_tid = min((c[3] for c in calls), key=lambda t: int(t)) if calls else None
+    ar = sorted(c for c in calls if c[2] in ("ncclAllReduce", "ncclReduceScatter", "ncclAllGather"))
+    step_pat = re.compile(a.step_kernel)
+    # step boundaries: first optimizer kernel after a gap of non-optimizer kernels
+    bounds, prev_opt = [], False
+    for s_, e_, q, n in rows:
+        is_opt = bool(step_pat.search(n))
+        if is_opt and not prev_opt:
+            bounds.append(s_)
+        prev_opt = is_opt
+    comp = [(s_, e_) for s_, e_, q, n in rows if q == "0" and not RCCL.search(n)]
+    out = ["", "## RCCL calls inside the training steps (rccl API trace)", "",
+           f"collective calls: {len(ar)}; issuing threads: "
+           + ", ".join(f"{t} ({'main' if t == main_tid else 'autograd/hook'}): {sum(1 for c in ar if c[3] == t)}"
+                       for t in sorted({c[3] for c in ar}))]
+    rows_md = ["", "| step | calls | from hook thread | median compute after call (ms) | step compute (ms) |",
+               "|---|---|---|---|---|"]
+    lo = 0
+    for k, b in enumerate(bounds):
+        sc = [c for c in ar if lo <= c[0] < b]
+        if sc:
+            win = [(s_, e_) for s_, e_ in comp if lo <= s_ < b]
+            tot = sum(e_ - s_ for s_, e_ in win)
+            after = sorted(sum(e_ - max(s_, c[0]) for s_, e_ in win if e_ > c[0]) for c in sc)
+            med = after[len(after) // 2]
+            hook = sum(1 for c in sc if c[3] != main_tid)
+            rows_md.append(f"| {k} | {len(sc)} | {hook} | {med / 1e6:.2f} | {tot / 1e6:.2f} |")
+        lo = b
+    return out + rows_md
 
 
 if __name__ == "__main__":

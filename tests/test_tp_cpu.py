@@ -122,9 +122,11 @@ def _w_strategy_tp(rank, world):
     ref.load_state_dict(m.state_dict())
     opt = FusedSGD(m.parameters(), lr=0.1)
     m, opt = madnn.distribute(m, opt, strategy="tp", tp_min_params=1000)
-    from madnn.nn import RowParallelLinear
+    from madnn.nn import ColumnParallelLinear, RowParallelLinear
 
-    assert isinstance(m.fc1, RowParallelLinear) and isinstance(m.fc2, RowParallelLinear)
+    # Megatron pairing: fc1 column-parallel (output stays sharded), fc2 row-parallel
+    assert isinstance(m.fc1, ColumnParallelLinear) and not m.fc1.gather_output
+    assert isinstance(m.fc2, RowParallelLinear) and m.fc2.input_is_parallel
     ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
     x, y = torch.randn(6, 64), torch.randint(0, 10, (6,))
     for _ in range(2):
@@ -170,3 +172,64 @@ def _w_dp_tp(rank, world):
 
 def test_dp2_x_tp2():
     run_dist(_w_dp_tp, 4)
+
+
+def _w_tp_gpt_clip_ckpt(rank, world, path):
+    """dp2 x tp2 GPT-2 tiny: paired MLPs + row-parallel projections, global-norm clipping, and a
+    checkpoint that holds FULL tensors (params and Adam state), consolidates into the plain
+    model and resumes to the same trajectory (TP shards used to be saved as shards)."""
+    import copy
+
+    import madnn
+    from madnn import ckpt
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.nn import ColumnParallelLinear, RowParallelLinear
+    from madnn.optim import FusedAdam
+
+    def make():
+        torch.manual_seed(0)
+        m = GPT2(gpt2_config("gpt2-tiny", n_layer=2))
+        return m, FusedAdam(m.parameters(), lr=1e-2)
+
+    m, opt = make()
+    ref = copy.deepcopy(m)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.0)
+    eng, opt = madnn.distribute(m, opt, strategy="tp", tp_size=2, tp_min_params=4096)
+    mlp = eng.module.h[0].mlp
+    assert isinstance(mlp.c_fc, ColumnParallelLinear) and isinstance(mlp.c_proj, RowParallelLinear)
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(0, 512, (4, 16), generator=g)
+    d = eng.groups.dp_idx
+    mine = ids[d * 2:(d + 1) * 2]
+
+    def step(e, o, r=None, ro=None):
+        e.module.loss_fn(e(mine), mine).backward()
+        n = o.clip_grad_norm_(0.5)
+        o.step()
+        if r is not None:
+            r.loss_fn(r(ids), ids).backward()
+            rn = torch.nn.utils.clip_grad_norm_(r.parameters(), 0.5)
+            torch.testing.assert_close(n, rn.detach(), atol=1e-5, rtol=1e-4)
+            ro.step()
+            ro.zero_grad()
+
+    for _ in range(2):
+        step(eng, opt, ref, ropt)
+    ckpt.save(path, eng, opt, step=2)
+    full = ckpt.consolidate(path)
+    plain, _ = make()
+    plain.load_state_dict(full, strict=True)  # full shapes, loads into the plain model
+    for n_, p in ref.named_parameters():
+        torch.testing.assert_close(full[n_], p.detach().float(), atol=3e-4, rtol=3e-4, msg=lambda m, n_=n_: f"{n_}: {m}")
+    step(eng, opt)
+    want = {n_: p.detach().clone() for n_, p in eng.module.named_parameters()}
+    m2, opt2 = make()
+    eng2, opt2 = madnn.distribute(m2, opt2, strategy="tp", tp_size=2, tp_min_params=4096)
+    ckpt.load(path, eng2, opt2)
+    step(eng2, opt2)
+    for n_, p in eng2.module.named_parameters():
+        torch.testing.assert_close(p.detach(), want[n_], atol=1e-6, rtol=1e-6, msg=n_)
+
+
+def test_dp2_x_tp2_gpt_clip_and_checkpoint(tmp_path):
+    run_dist(_w_tp_gpt_clip_ckpt, 4, str(tmp_path / "ck"))
