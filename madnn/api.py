@@ -85,7 +85,8 @@ def build_space(model: nn.Module, optimizer, cfg: Config, device, dtype_of, chan
     else:
         groups = [[p for p in model.parameters() if p.requires_grad]]
     return FlatParamSpace(groups, dtype_of=dtype_of, bucket_cap_mb=cfg.bucket_mb,
-                          reduce_dtype=torch_dtype(cfg.reduce_dtype), device=device,
+                          reduce_dtype=None if cfg.reduce_dtype == "auto" else torch_dtype(cfg.reduce_dtype),
+                          device=device,
                           channels_last_of=(lambda p: channels_last and p.dim() == 4))
 
 
@@ -105,6 +106,12 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
     rt.init(timeout_s=cfg.timeout_s)
     apply_debug_flags(cfg)
     device = rt.device()
+    if cfg.fused_kernels == "on" or (cfg.fused_kernels == "auto" and device.type == "cuda"):
+        from .nn.swap import use_madnn_kernels
+
+        swapped = use_madnn_kernels(model)
+        if swapped:
+            get_logger().info("madnn: hand-written kernels swapped in: %s", swapped)
     strat = cfg.strategy
     plan = None
     if strat in ("auto", "pp", "dp_pp"):
@@ -206,13 +213,14 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
     engine = DataParallel(model, space, group=group, src_rank=src_rank, sync=cfg.sync, sync_every=sync_every,
                           overlap=cfg.overlap, cast_dtype=dtype, channels_last=cl, unpack_grads=not fused,
                           broadcast_buffers=cfg.broadcast_buffers, find_unused=cfg.find_unused,
-                          sync_comm=cfg.sync_comm)
+                          sync_comm=cfg.sync_comm, rebuild_buckets=cfg.rebuild_buckets and fused)
     engine.loss_fn = loss_fn or getattr(model, "loss_fn", None)
     engine.plan = plan
     if optimizer is not None:
         if fused:
             optimizer.bind(space)
             optimizer.grad_source = engine
+            engine.optimizer = optimizer
         else:
             if cfg.sync == "grads":
                 optimizer.register_step_pre_hook(lambda *a, **k: engine.finalize_grads())

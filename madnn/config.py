@@ -39,13 +39,15 @@ class Config:
     sync_every: Optional[int] = None     # period K for sync="params" (None => reference heuristic)
     bucket_mb: float = 64.0              # gradient bucket cap (MB of reduce dtype)
     overlap: bool = True                 # overlap bucket all-reduce with backward on a comm stream
-    reduce_dtype: str = "float32"        # dtype of the gradient all-reduce buffers
+    reduce_dtype: str = "auto"           # gradient all-reduce dtype: auto = each bucket's own (bf16 / fp32 norms)
+    rebuild_buckets: bool = True         # re-lay buckets in the OBSERVED gradient order after step 1
     broadcast_buffers: bool = True       # broadcast module buffers (BN stats) at wrap time
     find_unused: bool = True             # flush buckets holding params that got no grad
     # mixed precision
     dtype: str = "bfloat16"              # compute/parameter dtype of the wrapped model
     keep_fp32_norms: bool = True         # BatchNorm/LayerNorm params stay fp32
     channels_last: Optional[bool] = None  # None => auto (conv nets)
+    fused_kernels: str = "auto"          # swap madnn kernels into the model: auto (on GPU) | on | off
     # pipeline parallel
     pp_stages: Optional[int] = None
     microbatches: Optional[int] = None

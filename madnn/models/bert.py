@@ -95,7 +95,7 @@ class BertMLMHead(nn.Module):
         self.decoder.weight = word.weight  # tied
 
     def forward(self, x):
-        return self.decoder(self.norm(F.gelu(self.dense(x))))
+        return linear(self.decoder, self.norm(F.gelu(linear(self.dense, x))))
 
 
 class BertForPreTraining(nn.Module):

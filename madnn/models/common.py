@@ -35,14 +35,16 @@ def mlm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None) -> 
     return ops.cross_entropy(logits, targets, shift=False, vocab=vocab, ignore_index=-100)
 
 
-def linear(mod: nn.Module, x: torch.Tensor, gelu: bool = False) -> torch.Tensor:
-    """``mod(x)`` (then tanh-GELU if asked).  A plain biased ``nn.Linear`` runs through
-    ``ops.linear``, whose backward produces the bias gradient (and the GELU backward) in one
-    K11 pass; any other module (e.g. a tensor-parallel replacement) is called as is."""
-    if ops.FUSED_LINEAR and type(mod) is nn.Linear and mod.bias is not None:
-        return ops.linear(x, mod.weight, mod.bias, gelu=gelu)
+def linear(mod: nn.Module, x: torch.Tensor, gelu: bool = False, residual: torch.Tensor = None) -> torch.Tensor:
+    """``mod(x)`` (then tanh-GELU if asked).  A plain ``nn.Linear`` runs through ``ops.linear``,
+    whose backward produces the bias gradient (and the GELU backward) in one K11 pass and writes
+    the weight gradient straight into the data-parallel bucket; any other module (e.g. a
+    tensor-parallel replacement) is called as is."""
+    if ops.FUSED_LINEAR and type(mod) is nn.Linear:
+        return ops.linear(x, mod.weight, mod.bias, gelu=gelu, residual=residual)
     y = mod(x)
-    return F.gelu(y, approximate="tanh") if gelu else y
+    y = F.gelu(y, approximate="tanh") if gelu else y
+    return y + residual if residual is not None else y
 
 
 class SelfAttention(nn.Module):

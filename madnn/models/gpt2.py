@@ -70,8 +70,12 @@ class GPT2MLP(nn.Module):
         self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
         self.drop = nn.Dropout(cfg.dropout)
 
-    def forward(self, x):
-        return self.drop(linear(self.c_proj, linear(self.c_fc, x, gelu=True)))
+    def forward(self, x, residual=None):
+        """MLP(x) (+ ``residual``, added in c_proj's GEMM epilogue when dropout is off)."""
+        if residual is not None and (self.drop.p == 0.0 or not self.training):
+            return linear(self.c_proj, linear(self.c_fc, x, gelu=True), residual=residual)
+        y = self.drop(linear(self.c_proj, linear(self.c_fc, x, gelu=True)))
+        return y + residual if residual is not None else y
 
     def tensor_parallel_pairs(self):
         return [(("c_fc",), "c_proj")]
@@ -89,7 +93,7 @@ class GPT2Block(nn.Module):
     def forward(self, x):
         a = self.drop(self.attn(self.ln_1(x)))
         y, h = self.ln_2(a, residual=x)      # h = x + a, y = LN(h): one kernel
-        return h + self.mlp(y)
+        return self.mlp(y, residual=h)        # h + MLP(y): the add rides in c_proj's GEMM epilogue
 
 
 class GPT2Head(nn.Module):
@@ -100,7 +104,7 @@ class GPT2Head(nn.Module):
         self.lm_head.weight = wte.weight      # tied
 
     def forward(self, x):
-        return self.lm_head(self.ln_f(x))
+        return linear(self.lm_head, self.ln_f(x))
 
 
 class GPT2(nn.Module):

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ..nn.norm import FusedRMSNorm
-from .common import init_module_, RotaryEmbedding, SelfAttention, causal_lm_loss, init_normal_
+from .common import init_module_, RotaryEmbedding, SelfAttention, causal_lm_loss, init_normal_, linear
 
 
 @dataclass
@@ -62,8 +62,8 @@ class LlamaMLP(nn.Module):
         self.down = nn.Linear(cfg.intermediate, cfg.hidden, bias=False)
 
     def forward(self, x):
-        g, u = self.gate_up(x).split(self.inter, dim=-1)
-        return self.down(F.silu(g) * u)
+        g, u = linear(self.gate_up, x).split(self.inter, dim=-1)
+        return linear(self.down, F.silu(g) * u)
 
 
 class LlamaBlock(nn.Module):
@@ -87,7 +87,7 @@ class LlamaHead(nn.Module):
         self.lm_head = nn.Linear(cfg.hidden, cfg.vocab_size, bias=False)
 
     def forward(self, x):
-        return self.lm_head(self.norm(x))
+        return linear(self.lm_head, self.norm(x))
 
 
 class Llama(nn.Module):

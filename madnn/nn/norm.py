@@ -4,7 +4,8 @@ Drop-in for ``nn.LayerNorm`` (same parameter names ``weight``/``bias``, so
 state dicts interchange).  On HIP tensors they call ``madnn.ops.layer_norm`` /
 ``rms_norm`` (one fused kernel each way, optional fused residual add); on CPU
 the eager reference.  ``swap_layernorms(model)`` replaces every eligible
-``nn.LayerNorm`` of an arbitrary model in place (the planner does this).
+``nn.LayerNorm`` of an arbitrary model in place; ``distribute()`` does this (and
+more) through :func:`madnn.nn.swap.use_madnn_kernels`.
 """
 from __future__ import annotations
 

@@ -641,20 +641,85 @@ def bias_grad(dy: torch.Tensor, pre: Optional[torch.Tensor] = None, bias_dtype: 
     return db, (dp.view(dy.shape) if pre is not None else None)
 
 
+def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """Where ``weight``'s gradient should be WRITTEN: a fresh view of its slot in the data-parallel
+    reducer's flat gradient bucket when (a) the parameter lives in a FlatParamSpace with sinks
+    enabled, (b) its bucket reduces in the parameter's dtype and (c) no gradient was accumulated
+    yet this step (``weight.grad is None``).  A layer that computes its weight gradient with a
+    GEMM writes it there (``torch.mm(..., out=sink)``) and returns the view; autograd adopts it
+    as ``p.grad`` without a copy and the reducer skips the K4 pack for it."""
+    space = getattr(weight, "_madnn_space", None)
+    if space is None or weight.grad is not None:
+        return None
+    return space.grad_slot(weight)
+
+
+LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)
+_LT_FAILED = {}   # (gelu, residual) -> the error that disabled that epilogue kind
+_LT_KIND = {"gelu": os.environ.get("MADNN_LT_GELU", "1") != "0", "res": os.environ.get("MADNN_LT_RES", "1") != "0"}
+
+
+def _lt_ok(x: torch.Tensor, weight: torch.Tensor, gelu: bool = False, residual: bool = False) -> bool:
+    if gelu and not _LT_KIND["gelu"] or residual and not _LT_KIND["res"]:
+        return False
+    return (LT_EPILOGUE and (bool(gelu), bool(residual)) not in _LT_FAILED and x.dtype == torch.bfloat16
+            and weight.dtype == torch.bfloat16 and x.is_cuda and weight.is_contiguous())
+
+
+def _lt_linear(x2, weight, bias, residual, gelu):
+    """(y, pre) from one hipBLASLt call with the bias / GELU(+aux) / residual epilogue, or None
+    if hipBLASLt refuses it (then that epilogue kind uses the unfused path for good)."""
+    try:
+        y, pre = _need_native("lt_linear").lt_linear(x2, weight, bias, residual, bool(gelu), bool(gelu))
+        return y, (pre if gelu else None)
+    except RuntimeError as e:  # noqa: PERF203 - once per kind
+        _LT_FAILED[(bool(gelu), residual is not None)] = e
+        import sys
+
+        print(f"[madnn] hipBLASLt epilogue (gelu={gelu}, residual={residual is not None}) disabled: {e}",
+              file=sys.stderr)
+        return None
+
+
 class _LinearFn(torch.autograd.Function):
-    """y = act(x W^T + b) with act in {identity, tanh-GELU}; the backward's bias gradient (and the
-    GELU backward) come from one K11 pass, the two GEMMs stay on hipBLASLt."""
+    """y = act(x W^T + b) (+ residual) with act in {identity, tanh-GELU}.
+
+    Forward: one hipBLASLt GEMM whose epilogue adds the bias, applies the GELU (keeping the
+    pre-activation as its AUX output for the backward) and adds the residual stream -- no
+    standalone elementwise passes.  Backward: the bias gradient (and the GELU backward) come from
+    one K11 pass, the two GEMMs stay on hipBLASLt, and the weight-gradient GEMM writes straight
+    into the reducer's bucket when the weight has a :func:`grad_sink`; the residual's gradient is
+    the output gradient itself (no copy)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, gelu):
-        pre = F.linear(x, weight, bias)
+    def forward(ctx, x, weight, bias, gelu, residual):
         ctx.gelu = gelu
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.param = weight  # the Parameter itself (for its grad sink); not modified before backward
+        ctx.has_res = residual is not None
+        out = None
+        if (gelu or residual is not None) and _lt_ok(x, weight, gelu, residual is not None):
+            x2 = x.reshape(-1, x.shape[-1])
+            if not x2.is_contiguous():
+                x2 = x2.contiguous()
+            r2 = residual.reshape(-1, weight.shape[0]).contiguous() if residual is not None else None
+            out = _lt_linear(x2, weight, bias if bias is None or bias.is_contiguous() else bias.contiguous(), r2, gelu)
+        if out is not None:
+            y, pre = out
+            y = y.view(*x.shape[:-1], weight.shape[0])
+            if gelu:
+                ctx.save_for_backward(x, weight, pre.view_as(y))
+            else:
+                ctx.save_for_backward(x, weight)
+            return y
+        pre = F.linear(x, weight, bias)
         if gelu:
             ctx.save_for_backward(x, weight, pre)
-            return F.gelu(pre, approximate="tanh")
-        ctx.save_for_backward(x, weight)
-        return pre
+            y = F.gelu(pre, approximate="tanh")
+        else:
+            ctx.save_for_backward(x, weight)
+            y = pre
+        return y + residual if residual is not None else y
 
     @staticmethod
     def backward(ctx, g):
@@ -674,14 +739,35 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = (g2 @ weight).view(*x.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = (g2.t() @ x.reshape(-1, x.shape[-1])).to(weight.dtype)
-        return dx, dw, db, None
+            x2 = x.reshape(-1, x.shape[-1])
+            sink = grad_sink(ctx.param)
+            if sink is not None and sink.dtype == g2.dtype == x2.dtype and sink.is_contiguous():
+                torch.mm(g2.t(), x2, out=sink)
+                dw = sink
+            else:
+                dw = (g2.t() @ x2).to(weight.dtype)
+        ctx.param = None
+        return dx, dw, db, None, (g if ctx.has_res else None)
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False):
-    """``F.linear`` (optionally followed by tanh-GELU) whose backward fuses the bias gradient (K11).
-    Falls back to eager ops on CPU tensors."""
-    if not _is_dev(x) or weight.shape[0] % 8 or not torch.is_grad_enabled():
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
+           force_fn: bool = False, residual: Optional[torch.Tensor] = None):
+    """``act(F.linear(x, weight, bias)) + residual`` with act in {identity, tanh-GELU}: one
+    epilogue-fused hipBLASLt GEMM forward; backward fuses the bias gradient (K11) and writes the
+    weight gradient into the reducer bucket (:func:`grad_sink`).  Eager ops on CPU tensors
+    (``force_fn`` runs the autograd Function anyway: tests of the sink path)."""
+    if residual is not None and residual.shape[:-1] != x.shape[:-1]:
+        raise ValueError("linear: residual must have the output's shape")
+    if not torch.is_grad_enabled() or (not force_fn and (not _is_dev(x) or weight.shape[0] % 8)):
+        if not torch.is_grad_enabled() and _is_dev(x) and (gelu or residual is not None) \
+                and _lt_ok(x, weight, gelu, residual is not None) \
+                and weight.shape[0] % 8 == 0:
+            x2 = x.reshape(-1, x.shape[-1]).contiguous()
+            r2 = residual.reshape(-1, weight.shape[0]).contiguous() if residual is not None else None
+            out = _lt_linear(x2, weight, bias, r2, gelu)
+            if out is not None:
+                return out[0].view(*x.shape[:-1], weight.shape[0])
         y = F.linear(x, weight, bias)
-        return F.gelu(y, approximate="tanh") if gelu else y
-    return _LinearFn.apply(x, weight, bias, gelu)
+        y = F.gelu(y, approximate="tanh") if gelu else y
+        return y + residual if residual is not None else y
+    return _LinearFn.apply(x, weight, bias, gelu, residual)

@@ -35,7 +35,7 @@ MANIFEST = HERE / "_madnn_build_manifest.json"
 
 ARCH = os.environ.get("MADNN_OFFLOAD_ARCH", "gfx950")
 KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "pool.hip", "attn.hip", "conv.hip",
-                  "stem.hip", "bias.hip", "binding.cpp"]
+                  "stem.hip", "bias.hip", "binding.cpp", "lt.cpp"]
 RUNTIME_SOURCES = ["runtime.cpp"]
 # per-source extra flags: MFMA kernels keep their accumulators in the (unified) VGPR file
 # instead of AGPRs, which removes a v_accvgpr_read/write around every softmax element
@@ -148,7 +148,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     if changed or not KERNELS_SO.exists():
         objs = [str(BUILD / (s + ".o")) for s in KERNEL_SOURCES]
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", str(KERNELS_SO),
-               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt",
                f"-Wl,-rpath,{tlib}"]
         if verbose:
             print(" ".join(cmd), flush=True)

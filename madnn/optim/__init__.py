@@ -49,6 +49,25 @@ class _FlatOptimizer(torch.optim.Optimizer):
             sd, self._pending_load = self._pending_load, None
             self.load_state_dict(sd)
 
+    @torch.no_grad()
+    def migrate(self, old: dict):
+        """Follow a ``FlatParamSpace.relayout``: move every parameter's optimizer state from its
+        old bucket slot (``old[id(p)] = (bucket, offset)``) to its new one."""
+        old_state, old_steps = self.flat_state, self.bucket_steps
+        self.flat_state, self.bucket_steps = {}, {}
+        for bk in self.space.buckets:
+            st = {n: torch.zeros_like(bk.master) for n in self._state_names if
+                  any(n in v for v in old_state.values())}
+            steps = 0
+            for p, off in zip(bk.params, bk.offsets):
+                obk, ooff = old[id(p)]
+                steps = max(steps, old_steps.get(obk.index, 0))
+                for n, t in st.items():
+                    if n in old_state.get(obk.index, {}):
+                        t[off:off + p.numel()].copy_(old_state[obk.index][n][ooff:ooff + p.numel()])
+            self.flat_state[bk.index] = st
+            self.bucket_steps[bk.index] = steps
+
     def _bind_local(self):
         groups = [g["params"] for g in self.param_groups]
         dev = groups[0][0].device

@@ -82,7 +82,7 @@ class DataParallel(nn.Module):
                  sync: str = "grads", sync_every: int = 1, overlap: bool = True,
                  cast_dtype: Optional[torch.dtype] = None, channels_last: bool = False,
                  unpack_grads: bool = False, broadcast_buffers: bool = True, find_unused: bool = True,
-                 sync_comm: bool = False):
+                 sync_comm: bool = False, grad_sinks: bool = True, rebuild_buckets: bool = True):
         super().__init__()
         self.module = module
         self.space = space
@@ -115,8 +115,16 @@ class DataParallel(nn.Module):
         self._last_ev = None
         self._step_bytes = 0
         self.broadcast_state(broadcast_buffers)
+        self.grad_sinks = 0
+        self.optimizer = None                 # fused optimizer bound to ``space`` (set by distribute)
+        self.rebuild_buckets = rebuild_buckets
+        self._observe = [] if (sync == "grads" and rebuild_buckets) else None
+        self.rebuilt = False
         if sync == "grads":
             self._install_hooks()
+            if not unpack_grads and grad_sinks:
+                # fused optimizer reads the buckets: layers may write weight grads straight in
+                self.grad_sinks = space.enable_grad_sinks()
 
     # ---------------------------------------------------------------- setup
     @torch.no_grad()
@@ -144,6 +152,8 @@ class DataParallel(nn.Module):
         def hook(_p):
             if not self._sync_enabled:
                 return
+            if self._observe is not None:
+                self._observe.append(id(_p))
             if not self._in_backward:
                 self._in_backward = True
                 if self._needs_finalize:
@@ -162,7 +172,9 @@ class DataParallel(nn.Module):
 
     # ------------------------------------------------------------ reduction
     def _launch(self, bk: FlatBucket):
-        scale = 1.0 / self.world
+        # pack with no scale: gradients written in place by their layers (grad sinks) cannot take
+        # one, so the 1/W average rides in RCCL's in-kernel AVG reduction (a plain sum at W = 1)
+        scale, op = 1.0, ("avg" if self.world > 1 else "sum")
         if self.comm_stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(bk.model.device))
@@ -175,10 +187,10 @@ class DataParallel(nn.Module):
                     if p.grad is not None:
                         p.grad.record_stream(self.comm_stream)
                 buf = self.space.pack_grads(bk, scale)
-                bk.work = comm.all_reduce(buf, "sum", group=self.group, async_op=True)
+                bk.work = comm.all_reduce(buf, op, group=self.group, async_op=True)
         else:
             buf = self.space.pack_grads(bk, scale)
-            bk.work = comm.all_reduce(buf, "sum", group=self.group, async_op=True)
+            bk.work = comm.all_reduce(buf, op, group=self.group, async_op=True)
         bk.launched = True
         self.stats["buckets_launched"] += 1
         self.stats["bytes_reduced"] += buf.numel() * buf.element_size()
@@ -279,9 +291,31 @@ class DataParallel(nn.Module):
         """Called by the fused optimizer after each step: the sync="params" period, then the
         robustness hooks (fault injection, collective-order check)."""
         self._steps += 1
+        if self._observe is not None:
+            self._maybe_relayout()
         if self.sync == "params" and self._steps % self.sync_every == 0:
             self.average_parameters()
         robustness_tick(self._steps, self.group)
+
+    def _maybe_relayout(self):
+        """After the first step: if the buckets did not fill in the order backward produced
+        gradients, re-lay them in the observed order (every rank observes the same autograd
+        order, so layouts stay identical across replicas)."""
+        seen = self._observe
+        self._observe = None
+        if not seen or self.space.layout_is_contiguous(seen):
+            return
+        if self.optimizer is None and self.unpack_grads is False:
+            return  # a flat state we cannot migrate
+        old = self.space.relayout(seen)
+        if self.optimizer is not None:
+            self.optimizer.migrate(old)
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+        self._install_hooks()
+        self.rebuilt = True
+        get_logger().info("madnn dp: re-laid %d buckets in the observed gradient order", len(self.space.buckets))
 
     @torch.no_grad()
     def average_parameters(self):
@@ -352,5 +386,5 @@ class DataParallel(nn.Module):
 def log_plan(engine: DataParallel):
     log = get_logger()
     for bk in engine.space.buckets:
-        log.info("bucket %d: %s x %d params, %.1f MB", bk.index, bk.dtype, len(bk.params),
-                 bk.numel * torch.tensor([], dtype=engine.space.reduce_dtype).element_size() / 2**20)
+        log.info("bucket %d: %s x %d params, %.1f MB (reduce %s)", bk.index, bk.dtype, len(bk.params),
+                 bk.numel * torch.tensor([], dtype=bk.grad_dtype).element_size() / 2**20, bk.grad_dtype)

@@ -359,6 +359,7 @@ class PipelineEngine:
                     comm.all_reduce(probe, "sum", group=g)
             for _, g, _ in tied:
                 comm.all_reduce(probe, "sum", group=g)
+            self._warm_channels()
         self._sig = _UNSET
         self._in_meta: Dict[int, tuple] = {}    # chunk -> (shape, dtype) of its received activation
         self._out_meta: Dict[int, tuple] = {}   # chunk -> (shape, dtype) of its sent activation
@@ -376,6 +377,38 @@ class PipelineEngine:
         return self.stage == self.nstages - 1
 
     # ------------------------------------------------------------ channels
+    def _warm_channels(self):
+        """Create every channel's point-to-point communicator before the first step.
+
+        RCCL builds a two-rank communicator on a pair's first send/recv and that build is a
+        blocking rendezvous of the two ranks.  Doing it lazily inside the schedule would turn
+        the first message of every channel into a synchronous handshake (the schedule is only
+        proven deadlock-free for non-blocking sends); here every rank walks the pipeline edges
+        in one global order -- channel kind, then edge index, the ring edge S-1 -> 0 last --
+        so the handshakes form a chain that always completes."""
+        order = ["act_out", "act_in", "grad_out", "grad_in", "act_out_wrap", "act_in_wrap", "grad_out_wrap",
+                 "grad_in_wrap"]
+        S = self.nstages
+
+        def edge(name):  # (kind, edge index) of this rank's end of the channel
+            kind = name.replace("_in", "").replace("_out", "")
+            if kind == "act":
+                return kind, (self.stage if name == "act_out" else self.stage - 1)
+            if kind == "grad":
+                return kind, (self.stage - 1 if name == "grad_out" else self.stage)
+            return kind, S - 1
+        ranked = sorted(self.channels, key=lambda n: (["act", "grad", "act_wrap", "grad_wrap"].index(edge(n)[0]),
+                                                      edge(n)[1], order.index(n)))
+        for name in ranked:
+            ch = self.channels[name]
+            t = torch.zeros(1, device=ch.buf_device)
+            if name.endswith("_out") or name.endswith("_out_wrap"):
+                dist.isend(t, ch.dst, group=ch.group).wait()
+            else:
+                dist.irecv(t, ch.src, group=ch.group).wait()
+        if self.channels and torch.cuda.is_available() and rt.device().type == "cuda":
+            torch.cuda.synchronize()
+
     def _act_in(self, c: int) -> Channel:
         return self.channels["act_in" if self.stage > 0 else "act_in_wrap"]
 
@@ -737,7 +770,8 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
         space.sync_model_from_master()
     dp_engine = DataParallel(stage_mod, space, group=groups.dp_group, src_rank=groups.dp_ranks[0], sync="grads",
                              overlap=cfg.overlap, cast_dtype=dtype, channels_last=cl, unpack_grads=False,
-                             broadcast_buffers=cfg.broadcast_buffers, find_unused=True, sync_comm=cfg.sync_comm)
+                             broadcast_buffers=cfg.broadcast_buffers, find_unused=True, sync_comm=cfg.sync_comm,
+                             rebuild_buckets=cfg.rebuild_buckets and optimizer is not None)
     engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
                             schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
                             tied=tied_local, param_names=names, buffer_refs=buffer_refs, channels=channels,
@@ -748,6 +782,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
             raise TypeError("pipeline engine needs a madnn fused optimizer (FusedSGD / FusedAdam)")
         optimizer.bind(space)
         optimizer.grad_source = engine
+        dp_engine.optimizer = optimizer
     get_logger().info("madnn pp: rank %d/%d chunks %s dp=%d microbatches=%d schedule=%s tied=%d", stage, S,
                       ranges, plan.dp, plan.microbatches, schedule, len(tied_local))
     return engine, optimizer

@@ -254,3 +254,76 @@ def _metrics_worker(rank, world, path):
 
 def test_step_metrics_jsonl(tmp_path):
     run_dist(_metrics_worker, 2, str(tmp_path / "metrics.jsonl"))
+
+
+# ------------------------------------------------------- bucket layout / grad sinks
+class _Crossed(torch.nn.Module):
+    """Registration order differs from backward order: ``late`` is registered first but is used
+    LAST in forward (so its gradient arrives first), ``early`` the other way round."""
+
+    def __init__(self):
+        super().__init__()
+        self.late = torch.nn.Linear(16, 4)
+        self.mid = torch.nn.Linear(16, 16)
+        self.early = torch.nn.Linear(8, 16)
+
+    def forward(self, x):
+        return self.late(torch.relu(self.mid(torch.relu(self.early(x)))))
+
+
+def _w_relayout(rank, world):
+    import madnn
+    from madnn.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = _Crossed()
+    ref = copy.deepcopy(m)
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9)
+    # tiny buckets: one or two parameters each, so the order matters
+    dm, opt = madnn.distribute(m, opt, strategy="dp", bucket_mb=300 * 4 / 2**20)
+    nb = len(dm.space.buckets)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(1)
+    for step in range(3):
+        x, y = torch.randn(4 * world, 8, generator=g), torch.randint(0, 4, (4 * world,), generator=g)
+        F.cross_entropy(dm(x[4 * rank:4 * rank + 4]), y[4 * rank:4 * rank + 4]).backward()
+        opt.step()
+        F.cross_entropy(ref(x), y).backward()
+        ropt.step()
+        ropt.zero_grad()
+        if step == 0:
+            assert dm.rebuilt, "buckets should follow the observed gradient order after step 1"
+            assert dm.space.layout_is_contiguous([id(p) for p in (m.late.bias, m.late.weight, m.mid.bias,
+                                                                  m.mid.weight, m.early.bias, m.early.weight)])
+    assert len(dm.space.buckets) == nb
+    for p, q in zip(m.parameters(), ref.parameters()):  # values and momentum migrated exactly
+        torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_buckets_relaid_in_observed_order():
+    run_dist(_w_relayout, 2)
+
+
+def test_grad_sink_writes_in_place_cpu():
+    """ops.linear's backward writes the weight gradient straight into the bucket slot and
+    autograd adopts that view as p.grad (no copy); the reducer then skips it when packing."""
+    from madnn import ops
+    from madnn.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(16, 8)
+    ref = copy.deepcopy(lin)
+    space = FlatParamSpace([list(lin.parameters())], dtype_of=lambda p: torch.float32, bucket_cap_mb=1.0)
+    assert space.enable_grad_sinks() == 2
+    x = torch.randn(5, 16)
+    ops.linear(x, lin.weight, lin.bias, force_fn=True).square().sum().backward()
+    ref(x).square().sum().backward()
+    bk, off, _ = space.param_info[id(lin.weight)]
+    assert lin.weight.grad.data_ptr() == bk.grad.data_ptr() + off * 4, "weight grad was copied"
+    torch.testing.assert_close(lin.weight.grad, ref.weight.grad)
+    ts, offs, missing = space.bucket_grads(bk)
+    assert all(t is not lin.weight.grad for t in ts) and id(lin.weight) not in [id(t) for t in ts]
+    assert space.packed_fraction(bk) < 0.1  # only the bias (K11 column sum) is packed
+    # a second accumulation (no_sync microbatch) adds in place into the same slot
+    ops.linear(x, lin.weight, lin.bias, force_fn=True).square().sum().backward()
+    torch.testing.assert_close(lin.weight.grad, 2 * ref.weight.grad)

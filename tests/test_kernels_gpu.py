@@ -359,3 +359,39 @@ def test_fused_linear_matches_eager(cuda, gelu):
     for a, r in ((x.grad, xr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
         assert a.dtype == torch.bfloat16
         torch.testing.assert_close(a.float(), r, atol=3e-2 * r.abs().max().item(), rtol=3e-2)
+
+
+# ------------------------------------------------------- hipBLASLt epilogue Linear
+@pytest.mark.parametrize("gelu,res,bias", [(True, False, True), (False, True, True), (True, True, False),
+                                           (False, True, False)])
+@pytest.mark.parametrize("M,K,N", [(512, 256, 1024), (333, 128, 64)])
+def test_lt_linear_epilogues_match_fp32(cuda, gelu, res, bias, M, K, N):
+    """One hipBLASLt GEMM with the bias / tanh-GELU (+ pre-activation AUX) / residual epilogue vs
+    the fp32 composition; backward through ops.linear vs autograd of the fp32 reference."""
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * K ** -0.5).requires_grad_()
+    b = (torch.randn(N, device=cuda, dtype=torch.bfloat16) * 0.1).requires_grad_() if bias else None
+    r = torch.randn(M, N, device=cuda, dtype=torch.bfloat16, requires_grad=True) if res else None
+    y = madnn.ops.linear(x, w, b, gelu=gelu, residual=r)
+    if (gelu, res) in madnn.ops._LT_FAILED:
+        pytest.skip(f"hipBLASLt offers no epilogue for this kind on this box: {madnn.ops._LT_FAILED[(gelu, res)]}")
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    bf = b.detach().float().requires_grad_() if bias else None
+    rf = r.detach().float().requires_grad_() if res else None
+    yf = torch.nn.functional.linear(xf, wf, bf)
+    yf = torch.nn.functional.gelu(yf, approximate="tanh") if gelu else yf
+    yf = yf + rf if res else yf
+    assert _rel(y, yf) < 1e-2
+    g = torch.randn_like(yf)
+    y.backward(g.to(y.dtype))
+    yf.backward(g)
+    assert _rel(x.grad, xf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2
+    if bias:
+        assert _rel(b.grad, bf.grad) < 2e-2
+    if res:
+        assert _rel(r.grad, rf.grad) < 1e-2
+
+
+def _rel(a, b):
+    return float((a.detach().float() - b.detach().float()).norm() / b.detach().float().norm().clamp_min(1e-12))

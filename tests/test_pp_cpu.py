@@ -130,3 +130,42 @@ def test_pp_clip_grad_norm_is_global_and_tied_counted_once():
 
 def test_dp_pp_interleaved_2x2():
     run_dist(_w_pp, 4, "gpt", "interleaved", 2, 2, 2, None, 2)
+
+
+def _w_meta_tied(rank, world):
+    """A META-device GPT-2 (weights never on the host) cut into 2 stages: each rank materialises
+    its own stage, the tied wte / lm_head is found by NAME (ids change on
+    materialisation), broadcast from the first owner and summed across the owners every step."""
+    import torch.distributed as dist
+
+    import madnn
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.optim import FusedAdam
+
+    torch.manual_seed(0)
+    with torch.device("meta"):
+        model = GPT2(gpt2_config("gpt2-tiny", n_layer=4))
+    opt = FusedAdam(model.parameters(), lr=1e-2)
+    eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=2, microbatches=2, checkpointing="none",
+                                example_input=torch.zeros(1, 16, dtype=torch.long), global_batch=4)
+    assert len(eng.tied) == 1, "tied wte/lm_head must be detected on BOTH end stages"
+    ids = torch.randint(0, 512, (4, 16), generator=torch.Generator().manual_seed(2))
+
+    def tied_value():
+        p = eng.tied[0][0]
+        v = eng.dp.space.master_view(p).detach().clone()
+        other = v.clone()
+        dist.broadcast(other, src=0)
+        return v, other
+
+    v, other = tied_value()
+    torch.testing.assert_close(v, other, rtol=0, atol=0)
+    for _ in range(2):
+        eng.train_step(ids, ids)
+        opt.step()
+    v, other = tied_value()
+    torch.testing.assert_close(v, other, rtol=0, atol=0)  # same summed gradient -> same update
+
+
+def test_pp_meta_model_tied_weights_by_name():
+    run_dist(_w_meta_tied, 2)

@@ -205,10 +205,15 @@ def test_fx_spine_composes_to_model():
     from madnn.models import resnet18
     from madnn.planner.trace import run_spine, trace
 
+    from madnn.planner.trace import _fx_split
+
     m = resnet18(num_classes=7).eval()
-    sp = trace(m)
-    assert sp.source == "fx" and len(sp) > 5
     x = torch.randn(2, 3, 64, 64)
+    sp = _fx_split(m)  # the fx path on its own (ResNet also declares its spine)
+    assert sp.source == "fx" and len(sp) > 5
+    torch.testing.assert_close(run_spine(sp, x), m(x))
+    sp = trace(m)
+    assert sp.source == "declared" and len(sp) == 2 + 8
     torch.testing.assert_close(run_spine(sp, x), m(x))
 
 
