@@ -33,12 +33,15 @@ def main():
     assert madnn.ops.load_kernels()
     ops = torch.ops.madnn
     res = {"probe": [], "timing_us": {}}
-    for (M, K, N) in [(16384, 1024, 4096), (16384, 4096, 1024), (512, 64, 256)]:
+    dummy = torch.empty(16384 * 4096, device="cuda", dtype=torch.bfloat16)
+    for (M, K, N) in [(16384, 1024, 4096), (16384, 4096, 1024)]:
         for name, e in EPI.items():
             for bc in (-1, 0, 2):
                 for ac in (-1, 0, 2):
-                    n = int(ops.lt_probe(M, N, K, e, bc, ac, False))
-                    res["probe"].append({"M": M, "K": K, "N": N, "epi": name, "bias": bc, "aux": ac, "algos": n})
+                    for ptr in (0, dummy.data_ptr()):
+                        n = int(ops.lt_probe(M, N, K, e, bc, ac, False, ptr))
+                        res["probe"].append({"M": M, "K": K, "N": N, "epi": name, "bias": bc, "aux": ac,
+                                             "ptr": bool(ptr), "algos": n})
     M, K, N = 16384, 1024, 4096
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.03
@@ -54,7 +57,7 @@ def main():
             t[nm] = timeit(lambda: ops.lt_linear(x, w, b, kw["residual"], kw["gelu"], kw["gelu"]))
         except RuntimeError as e:
             t[nm] = str(e)[:160]
-    ok = [p for p in res["probe"] if p["algos"] > 0 and "GELU" in p["epi"]]
+    ok = [p for p in res["probe"] if p["algos"] > 0 and "AUX" in p["epi"]]
     print(json.dumps({"gelu_supported": ok[:12], "timing_us": t}, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)

@@ -62,7 +62,7 @@ std::map<Key, Plan> g_plans;
 std::mutex g_mu;
 
 Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEpilogue_t epi, hipDataType dt,
-               hipDataType bias_dt, bool has_c, size_t ws_cap) {
+               hipDataType bias_dt, bool has_c, size_t ws_cap, const void* bias_ptr, void* aux_ptr) {
   Key key{M, N, K, (int)epi, (int)dt, (int)bias_dt, (int)has_c, 0, ws_cap};
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_plans.find(key);
@@ -76,10 +76,15 @@ Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEp
   if (epi != HIPBLASLT_EPILOGUE_DEFAULT && epi != HIPBLASLT_EPILOGUE_GELU && epi != HIPBLASLT_EPILOGUE_GELU_AUX) {
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bias_dt, sizeof(bias_dt)));
   }
+  if (bias_ptr != nullptr) {  // set before the heuristic: solution selection looks at it
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias_ptr, sizeof(bias_ptr)));
+  }
   if (epi == HIPBLASLT_EPILOGUE_GELU_AUX_BIAS || epi == HIPBLASLT_EPILOGUE_GELU_AUX) {
     int64_t ld = N;
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld)));
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &dt, sizeof(dt)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux_ptr,
+                                             sizeof(aux_ptr)));
   }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt, K, N, K));  // W: K x N col-major, op T
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, dt, K, M, K));  // X: K x M col-major
@@ -129,15 +134,16 @@ std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tens
   hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
   const size_t ws_cap = at::cuda::getCUDABlasLtWorkspaceSize();
   void* ws = at::cuda::getCUDABlasLtWorkspace();
-  Plan& p = get_plan(h, M, N, K, epi, dt, bdt, has_res, ws_cap);
   at::Tensor y = at::empty({M, N}, x.options());
   at::Tensor pre;
+  if (gelu && want_pre) pre = at::empty({M, N}, x.options());
+  Plan& p = get_plan(h, M, N, K, epi, dt, bdt, has_res, ws_cap, has_bias ? bias->data_ptr() : nullptr,
+                     pre.defined() ? pre.data_ptr() : nullptr);
   if (has_bias) {
     const void* bp = bias->data_ptr();
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
   }
   if (gelu && want_pre) {
-    pre = at::empty({M, N}, x.options());
     void* ap = pre.data_ptr();
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &ap, sizeof(ap)));
   }
@@ -151,7 +157,8 @@ std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tens
 
 // How many algorithms hipBLASLt's heuristic offers for an epilogue / type combination
 // (0 = unsupported); dtype codes: 0 bf16, 1 fp16, 2 fp32, -1 = leave the attribute unset.
-int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code, int64_t aux_code, bool has_c) {
+int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code, int64_t aux_code, bool has_c,
+                 int64_t dummy_ptr) {
   auto code = [](int64_t c) { return c == 0 ? HIP_R_16BF : (c == 1 ? HIP_R_16F : HIP_R_32F); };
   hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
   hipblasLtMatmulDesc_t desc;
@@ -163,15 +170,18 @@ int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code
   LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e)));
+  void* dp = reinterpret_cast<void*>(dummy_ptr);
   if (bias_code >= 0) {
     hipDataType bdt = code(bias_code);
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bdt, sizeof(bdt)));
+    if (dp) LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &dp, sizeof(dp)));
   }
   if (aux_code >= 0) {
     hipDataType adt = code(aux_code);
     int64_t ld = N;
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ld, sizeof(ld)));
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &adt, sizeof(adt)));
+    if (dp) LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &dp, sizeof(dp)));
   }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&a, dt, K, N, K));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&b, dt, K, M, K));
@@ -198,10 +208,11 @@ int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code
 
 TORCH_LIBRARY_FRAGMENT(madnn, m) {
   m.def("lt_linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu, bool want_pre) -> (Tensor, Tensor)");
-  m.def("lt_probe(int M, int N, int K, int epi, int bias_code, int aux_code, bool has_c) -> int");
+  // no tensor arguments -> nothing to dispatch on: a catch-all kernel
+  m.def("lt_probe(int M, int N, int K, int epi, int bias_code, int aux_code, bool has_c, int dummy_ptr) -> int",
+        TORCH_FN(lt_probe));
 }
 
 TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("lt_linear", lt_linear);
-  m.impl("lt_probe", TORCH_FN(lt_probe));
 }
