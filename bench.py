@@ -10,9 +10,12 @@ Default (the driver's contract) measures BOTH halves of the metric in one run:
   channels_last, FusedSGD (momentum 0.9, wd 5e-5) on the hand-written gfx950 kernel,
   bucketed RCCL all-reduce overlapped with backward; 512 images per GPU (weak scaling);
 * ``gpt2_pp``: GPT-2 medium (seq 1024, bf16, FusedAdam), pipeline parallel over
-  RCCL P2P -- ``pp2`` at 2 GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1
-  GPU (a pipeline needs two stages); 16 sequences per GPU (weak scaling), 4-sequence
-  microbatches.
+  RCCL P2P with the interleaved 1F1B schedule (2 model chunks per rank) -- ``pp2`` at 2
+  GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1 GPU (a pipeline needs two
+  stages); 32 sequences per GPU (weak scaling), 16-sequence microbatches.  The sizes come
+  from a 1-GPU sweep (profiles/r2_gpt2m_dp1_batch_sweep.jsonl): GEMM efficiency keeps
+  rising with the rows per GEMM (4 / 8 / 16 / 32 / 64 sequences: 194k / 235k / 277k /
+  308k / 326k tok/s), and interleaving keeps the bubble small at 8 microbatches.
 
 Synthetic data and random init (no network on the box).  ``--model resnet50`` /
 ``--model gpt2-medium`` run one half only.  Without a launcher environment the
@@ -48,12 +51,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="all", choices=["all", "resnet50", "gpt2-medium"])
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
-    ap.add_argument("--gpt2-batch-per-gpu", type=int, default=16, help="GPT-2 sequences per GPU (global = this x N)")
+    ap.add_argument("--gpt2-batch-per-gpu", type=int, default=32, help="GPT-2 sequences per GPU (global = this x N)")
     ap.add_argument("--gpt2-config", default="gpt2-medium", help="GPT-2 size (gpt2-tiny for CPU harness tests)")
-    ap.add_argument("--gpt2-mb", type=int, default=4, help="GPT-2 sequences per pipeline microbatch")
+    ap.add_argument("--gpt2-mb", type=int, default=16, help="GPT-2 sequences per pipeline microbatch")
     ap.add_argument("--gpt2-steps", type=int, default=None, help="GPT-2 timed steps (default: --steps)")
     ap.add_argument("--gpt2-warmup", type=int, default=None, help="GPT-2 warmup steps (default: --warmup)")
-    ap.add_argument("--schedule", default=None, help="pipeline schedule override (gpipe | 1f1b | interleaved)")
+    ap.add_argument("--schedule", default="interleaved", help="pipeline schedule (gpipe | 1f1b | interleaved)")
     ap.add_argument("--no-pg", action="store_true", help="no world-1 process group when run without a launcher")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
@@ -156,8 +159,11 @@ def bench_gpt2(args, world, rank):
     model = GPT2(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
     kw = {}
-    if args.schedule:
-        kw["schedule"] = args.schedule
+    if args.schedule and stages > 1:
+        sched = args.schedule
+        if sched == "interleaved" and (micro or 1) % stages:
+            sched = "1f1b"  # interleaving needs microbatches % stages == 0
+        kw["schedule"] = sched
     engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if stages > 1 else None,
                                    microbatches=micro, checkpointing="none", global_batch=gbatch,
                                    example_input=torch.zeros(1, args.seq_len, dtype=torch.long), **kw)
@@ -188,6 +194,7 @@ def bench_gpt2(args, world, rank):
     info = {"model": args.gpt2_config, "global_batch": gbatch, "per_gpu_batch": args.gpt2_batch_per_gpu,
             "seq_len": args.seq_len, "parallelism": par, "microbatches": micro if stages > 1 else 1,
             "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
+            "virtual_stages": getattr(engine, "V", None) if stages > 1 else None,
             "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "loss_last_stage": lv}
     return dt, steps, gbatch, info
 

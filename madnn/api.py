@@ -84,7 +84,13 @@ def build_space(model: nn.Module, optimizer, cfg: Config, device, dtype_of, chan
         groups = [g["params"] for g in optimizer.param_groups]
     else:
         groups = [[p for p in model.parameters() if p.requires_grad]]
-    return FlatParamSpace(groups, dtype_of=dtype_of, bucket_cap_mb=cfg.bucket_mb,
+    mb = cfg.bucket_mb
+    if not mb:
+        from .config import auto_bucket_mb
+
+        rb = 4 if cfg.reduce_dtype in ("float32", "fp32") else 2
+        mb = auto_bucket_mb(sum(p.numel() for g in groups for p in g if p.requires_grad) * rb)
+    return FlatParamSpace(groups, dtype_of=dtype_of, bucket_cap_mb=mb,
                           reduce_dtype=None if cfg.reduce_dtype == "auto" else torch_dtype(cfg.reduce_dtype),
                           device=device,
                           channels_last_of=(lambda p: channels_last and p.dim() == 4))

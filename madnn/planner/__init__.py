@@ -119,6 +119,12 @@ def _reduce_bytes(cfg: Config) -> int:
     return 4 if cfg.reduce_dtype in ("float32", "fp32") else 2
 
 
+def _bucket_bytes(cfg: Config, costs, rb: int) -> float:
+    from ..config import auto_bucket_mb
+
+    return (cfg.bucket_mb or auto_bucket_mb(sum(c.params for c in costs) * rb)) * 2**20
+
+
 def _want_measure(cfg: Config) -> bool:
     v = cfg.extra.get("measure", os.environ.get("MADNN_PLAN_MEASURE", "auto"))
     if isinstance(v, str):
@@ -305,8 +311,8 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt):
         pbytes = sum(chunk_est[v].param_bytes for v in vs)
         act_per_chunk = sum(chunk_est[v].act_bytes_per_sample for v in vs) / len(vs) * mb
         mem_list.append((pbytes + act_per_chunk * inflight[r]) / 1e9)
-    bucket_bytes = cfg.bucket_mb * 2**20
     rb = _reduce_bytes(cfg)
+    bucket_bytes = _bucket_bytes(cfg, costs, rb)
     if pp == 1:
         compute = rank_t[0]
         bubble = 0.0
@@ -401,7 +407,7 @@ def _tp_candidate(spine: Spine, costs, dp, tp, B, cfg, hw: Machine, opt, cap, ex
     if dp > 1:
         bwd = [c.bwd_s * per_replica for c in costs]
         grad_dp = dp_exposed_s(bwd, [c.params * _reduce_bytes(cfg) / tp for c in costs], dp, hw,
-                               cfg.bucket_mb * 2**20)
+                               _bucket_bytes(cfg, costs, _reduce_bytes(cfg)))
     step = compute + comm + grad_dp
     return {"strategy": "tp", "dp": dp, "pp": 1, "tp": tp, "M": 1, "V": 1, "schedule": "none", "ckpt": False,
             "bounds": [0, len(costs)], "step_s": step, "compute_s": compute, "comm_s": comm + grad_dp,

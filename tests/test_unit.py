@@ -509,3 +509,12 @@ def test_fused_linear_cpu_fallback_and_reference_gelu_grad():
     db, dp = ops.bias_grad(dy, pre.detach())
     torch.testing.assert_close(dp, pre.grad)
     torch.testing.assert_close(db, pre.grad.sum(0))
+
+
+def test_auto_bucket_size():
+    from madnn.config import auto_bucket_mb
+
+    assert auto_bucket_mb(51e6) == pytest.approx(51e6 / 2**20 / 8)      # ResNet-50 bf16: ~6 MB buckets
+    assert auto_bucket_mb(0.71e9) == 64.0                                 # GPT-2 medium: capped
+    assert auto_bucket_mb(1e6) == 4.0                                     # tiny models: floor
+    assert Config.from_env().bucket_mb == 0.0
