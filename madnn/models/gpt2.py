@@ -91,8 +91,9 @@ class GPT2Block(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x):
-        a = self.drop(self.attn(self.ln_1(x)))
-        y, h = self.ln_2(a, residual=x)      # h = x + a, y = LN(h): one kernel
+        y, xr = self.ln_1(x, fork=True)       # xr aliases x: its gradient joins ln_1's backward pass
+        a = self.drop(self.attn(y))
+        y, h = self.ln_2(a, residual=xr)     # h = x + a, y = LN(h): one kernel
         return self.mlp(y, residual=h)        # h + MLP(y): the add rides in c_proj's GEMM epilogue
 
 

@@ -75,8 +75,9 @@ class LlamaBlock(nn.Module):
         self.mlp = LlamaMLP(cfg)
 
     def forward(self, x):
-        a = self.attn(self.input_norm(x))
-        y, h = self.post_attn_norm(a, residual=x)
+        y, xr = self.input_norm(x, fork=True)  # residual path's gradient joins the norm's backward
+        a = self.attn(y)
+        y, h = self.post_attn_norm(a, residual=xr)
         return h + self.mlp(y)
 
 

@@ -37,11 +37,12 @@ class FusedLayerNorm(nn.Module):
             if self.bias is not None:
                 self.bias.zero_()
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
-        """LN(x) or, with ``residual``, (LN(x + residual), x + residual) in one kernel."""
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, fork: bool = False):
+        """LN(x); with ``residual``, (LN(x + residual), x + residual) in one kernel; with ``fork``,
+        (LN(x), x) whose second output's gradient joins x's inside the LN backward pass."""
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
-        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual=residual)
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual=residual, fork=fork)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}, kernel=madnn.K3"
@@ -57,10 +58,10 @@ class FusedRMSNorm(nn.Module):
         with torch.no_grad():
             self.weight.fill_(1.0)
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, fork: bool = False):
         if residual is not None and residual.dtype != x.dtype:
             residual = residual.to(x.dtype)
-        return ops.rms_norm(x, self.weight, self.eps, residual=residual)
+        return ops.rms_norm(x, self.weight, self.eps, residual=residual, fork=fork)
 
     def extra_repr(self):
         return f"{self.weight.numel()}, eps={self.eps}, kernel=madnn.K3"

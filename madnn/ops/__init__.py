@@ -161,8 +161,13 @@ def grad_norm(flats: Sequence[torch.Tensor], max_norm: float = 0.0, scale: float
 
 # ---------------------------------------------------------------------- K3
 class _NormFn(torch.autograd.Function):
+    """K3 norm.  Modes: plain (y), residual (y = N(x + res), s = x + res) and fork
+    (y = N(x), plus an alias of x for the block's residual path).  In residual and fork modes the
+    second output's gradient is added inside the same backward pass (``dres``), so a tensor used
+    both as the norm input and as the residual costs no separate autograd accumulation."""
+
     @staticmethod
-    def forward(ctx, x, res, w, b, eps, rms):
+    def forward(ctx, x, res, w, b, eps, rms, fork):
         shape = x.shape
         xc = x.contiguous()
         rc = res.contiguous() if res is not None else None
@@ -172,37 +177,44 @@ class _NormFn(torch.autograd.Function):
         ctx.rms = rms
         ctx.has_bias = b is not None
         ctx.has_res = res is not None
+        ctx.fork = fork and res is None
         ctx.shape = shape
         if res is not None:
             return y.view(shape), s.view(shape)
+        if ctx.fork:
+            return y.view(shape), x.view_as(x)
         return y.view(shape), None
 
     @staticmethod
     def backward(ctx, dy, ds):
         x, w, mean, rstd = ctx.saved_tensors
-        dres = ds.contiguous() if (ctx.has_res and ds is not None) else None
+        dres = ds.contiguous() if ((ctx.has_res or ctx.fork) and ds is not None) else None
         dx, dw, db = torch.ops.madnn.norm_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.rms, ctx.has_bias)
         dx = dx.view(ctx.shape)
-        return dx, (dx if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None
+        return dx, (dx if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None, None
 
 
-def _norm(x, weight, bias, eps, rms, residual):
+def _norm(x, weight, bias, eps, rms, residual, fork=False):
     if _is_dev(x):
         if weight is None:
             raise ValueError("madnn norm kernels need an affine weight")
-        y, s = _NormFn.apply(x, residual, weight, bias, eps, rms)
-        return (y, s) if residual is not None else y
-    return reference.norm(x, weight, bias, eps, rms, residual)
+        y, s = _NormFn.apply(x, residual, weight, bias, eps, rms, fork)
+        return (y, s) if (residual is not None or fork) else y
+    y = reference.norm(x, weight, bias, eps, rms, residual)
+    return (y, x) if (fork and residual is None) else y
 
 
-def layer_norm(x, weight, bias=None, eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
-    """LayerNorm over the last dim.  With ``residual``: returns (LN(x + residual), x + residual)."""
-    return _norm(x, weight, bias, eps, False, residual)
+def layer_norm(x, weight, bias=None, eps: float = 1e-5, residual: Optional[torch.Tensor] = None, fork: bool = False):
+    """LayerNorm over the last dim.  With ``residual``: returns (LN(x + residual), x + residual).
+    With ``fork``: returns (LN(x), x) where the second output's gradient is summed into x's
+    inside the LN backward kernel (use it as the block's residual path)."""
+    return _norm(x, weight, bias, eps, False, residual, fork)
 
 
-def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = None):
-    """RMSNorm over the last dim.  With ``residual``: returns (RMS(x + residual), x + residual)."""
-    return _norm(x, weight, None, eps, True, residual)
+def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = None, fork: bool = False):
+    """RMSNorm over the last dim.  With ``residual``: returns (RMS(x + residual), x + residual);
+    with ``fork``: (RMS(x), x) as in :func:`layer_norm`."""
+    return _norm(x, weight, None, eps, True, residual, fork)
 
 
 # ---------------------------------------------------------------------- K5

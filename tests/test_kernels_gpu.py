@@ -395,3 +395,25 @@ def test_lt_linear_epilogues_match_fp32(cuda, gelu, res, bias, M, K, N):
 
 def _rel(a, b):
     return float((a.detach().float() - b.detach().float()).norm() / b.detach().float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("rms", [False, True])
+def test_norm_fork_gradient_joins_backward(cuda, rms):
+    """fork=True: (N(x), x) where the alias's gradient is added inside the K3 backward pass."""
+    torch.manual_seed(3)
+    x = torch.randn(64, 1024, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.rand(1024, device=cuda) + 0.5).requires_grad_()
+    b = None if rms else (torch.randn(1024, device=cuda) * 0.1).requires_grad_()
+    fn = madnn.ops.rms_norm if rms else madnn.ops.layer_norm
+    y, xa = fn(x, w, eps=1e-5, fork=True) if rms else fn(x, w, b, eps=1e-5, fork=True)
+    g1, g2 = torch.randn_like(y), torch.randn_like(y)
+    (y.float() * g1.float()).sum().add((xa.float() * g2.float()).sum()).backward()
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    if rms:
+        yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    else:
+        yr = torch.nn.functional.layer_norm(xr, (1024,), wr, b.detach(), 1e-5)
+    ((yr * g1.float()).sum() + (xr * g2.float()).sum()).backward()
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
