@@ -4,6 +4,7 @@
 
 Variants toggle at run time (the model is built once):
   lt_res  : residual add in c_proj's hipBLASLt epilogue (on) vs a separate ATen add (off)
+  gelu    : K11-family GELU forward kernel (on) vs ATen's F.gelu (off)
 Prints a JSON line with the per-window ms/step and the median of each arm.
 """
 import argparse
@@ -24,7 +25,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--switch", default="lt_res", choices=["lt_res"])
+    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu"])
     a = ap.parse_args()
     import madnn
     from madnn import ops
@@ -41,6 +42,8 @@ def main():
     def set_arm(on):
         if a.switch == "lt_res":
             ops._LT_KIND["res"] = on
+        elif a.switch == "gelu":
+            ops.GELU_KERNEL = on
 
     def window(n):
         torch.cuda.synchronize()

@@ -653,6 +653,18 @@ def bias_grad(dy: torch.Tensor, pre: Optional[torch.Tensor] = None, bias_dtype: 
     return db, (dp.view(dy.shape) if pre is not None else None)
 
 
+GELU_KERNEL = os.environ.get("MADNN_GELU_KERNEL", "1") != "0"  # K11 GELU forward (A/B switch)
+
+
+def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
+    """tanh-approximate GELU forward: the K11-family streaming kernel on HIP tensors (16-byte
+    accesses, v_exp-based tanh), ``F.gelu(approximate="tanh")`` elsewhere.  No autograd: the
+    caller (the fused Linear) saves the pre-activation and runs the GELU backward in K11."""
+    if GELU_KERNEL and _is_dev(x) and x.numel() % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32):
+        return _need_native("gelu_tanh").gelu_fwd(x)
+    return F.gelu(x, approximate="tanh")
+
+
 def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
     """Where ``weight``'s gradient should be WRITTEN: a fresh view of its slot in the data-parallel
     reducer's flat gradient bucket when (a) the parameter lives in a FlatParamSpace with sinks
@@ -727,7 +739,7 @@ class _LinearFn(torch.autograd.Function):
         pre = F.linear(x, weight, bias)
         if gelu:
             ctx.save_for_backward(x, weight, pre)
-            y = F.gelu(pre, approximate="tanh")
+            y = gelu_tanh(pre)
         else:
             ctx.save_for_backward(x, weight)
             y = pre

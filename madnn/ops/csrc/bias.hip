@@ -26,6 +26,44 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 
+// y = gelu_tanh(x) with tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp (x -> +-inf gives +-1 exactly):
+// the standalone GELU forward pass after c_fc (hipBLASLt on gfx950 has no GELU epilogue that also
+// returns the pre-activation the backward needs, bench/lt_probe.py).
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * u);  // exp(2u) = 2^(2u log2 e)
+  const float t = 1.f - 2.f / (e + 1.f);
+  return 0.5f * x * (1.f + t);
+}
+
+// 8 elements per lane per access (16-byte loads/stores), 4 accesses in flight per lane,
+// grid-stride over the flat tensor.  HBM-bound: reads x, writes y, nothing else.
+template <int DT>
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                       int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n8; i += 4 * stride) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load8<DT>(x, (i + u * stride) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh(v[u][j]);
+      store8<DT>(y, (i + u * stride) * 8, v[u]);
+    }
+  }
+  for (; i < n8; i += stride) {
+    float v[8];
+    load8<DT>(x, i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+    store8<DT>(y, i * 8, v);
+  }
+}
+
 // Row slots: a 256-lane workgroup is RPI = 256 / TPR row slots of TPR = min(256, N/8) lanes,
 // so narrow layers (N = 1024: TPR 128, 2 rows per step) still run 4 full waves per workgroup.
 struct BiasGeom {
@@ -154,6 +192,19 @@ int madnn_bias_grad_rows(int64_t M, int N, int gelu) {
   if (r < 1) r = 1;
   if (r > 4096) r = 4096;
   return (int)r;
+}
+
+hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t stream) {
+  if (n % 8) return hipErrorInvalidValue;
+  const int64_t n8 = n / 8;
+  int64_t grid = (n8 + 4 * 256 - 1) / (4 * 256);
+  const int64_t cap = 8 * (int64_t)kNumCU;  // a few waves per CU, grid-stride beyond that
+  if (grid > cap) grid = cap;
+  if (grid < 1) grid = 1;
+  MADNN_DISPATCH_DT(dt, DT, {
+    hipLaunchKernelGGL((gelu_fwd_kernel<DT>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+  });
+  return hipGetLastError();
 }
 
 // dy, pre, dp: [M, N] of dtype xdt; partial: [R, N] fp32 with R = madnn_bias_grad_rows(M, N, pre != 0);

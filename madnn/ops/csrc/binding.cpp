@@ -39,6 +39,7 @@ hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t
 int madnn_bias_grad_supported(int64_t, int);
 int madnn_bias_grad_rows(int64_t, int, int);
 hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, hipStream_t);
+hipError_t madnn_gelu_fwd(const void*, void*, int64_t, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
@@ -609,6 +610,17 @@ std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::op
   return {db, dp};
 }
 
+// tanh-GELU forward (K11 family): y = gelu(x), x any contiguous float tensor with numel % 8 == 0.
+at::Tensor gelu_fwd(const at::Tensor& x) {
+  check_dev(x, "x");
+  at::Tensor xc = x.contiguous();
+  TORCH_CHECK(xc.numel() % 8 == 0, "gelu_fwd: numel must be a multiple of 8");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty_like(xc);
+  if (xc.numel()) check(madnn_gelu_fwd(xc.data_ptr(), y.data_ptr(), xc.numel(), dt_code(xc), cur_stream(xc)), "gelu_fwd");
+  return y;
+}
+
 // K8 attention.  q: [B, S, H, D], k/v: [B, S, Hkv, D] bf16 views with a contiguous last dim
 // (any other strides, e.g. slices of one packed QKV projection).
 void attn_check(const at::Tensor& t, const char* name, int64_t D) {
@@ -708,6 +720,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
+  m.def("gelu_fwd(Tensor x) -> Tensor");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
@@ -742,6 +755,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("xent_bwd", xent_bwd);
   m.impl("maxpool_fwd", maxpool_fwd);
   m.impl("bias_grad", bias_grad);
+  m.impl("gelu_fwd", gelu_fwd);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_bwd", attn_bwd);
   m.impl("maxpool_bwd", maxpool_bwd);

@@ -93,7 +93,7 @@ def test_activation_checkpointing_same_grads(cuda):
         torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-3)
 
 
-def _w_pp_gpu(rank, world):
+def _w_pp_gpu(rank, world, schedule="1f1b"):
     import madnn
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.optim import FusedAdam
@@ -104,20 +104,27 @@ def _w_pp_gpu(rank, world):
     opt = FusedAdam(model.parameters(), lr=1e-3)
     ids = torch.randint(0, 512, (8, 64), generator=torch.Generator().manual_seed(3)).cuda()
     eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=world, microbatches=4,
-                                example_input=ids[:1].cpu(), checkpointing="none")
+                                example_input=ids[:1].cpu(), checkpointing="none", schedule=schedule,
+                                global_batch=ids.shape[0])
+    assert eng.schedule == schedule
     assert next(eng.module.parameters()).is_cuda
     loss = eng.train_step(ids, ids)
     opt.step()
-    if eng.is_last:
+    if eng.holds_last:
         rl = ref.loss_fn(ref(ids), ids)
         assert abs(float(loss) - float(rl)) < 2e-2 * float(rl), (float(loss), float(rl))
     loss2 = eng.train_step(ids, ids)
-    if eng.is_last:
+    if eng.holds_last:
         assert float(loss2) < float(loss) + 0.5 and torch.isfinite(loss2)
 
 
 def test_pipeline_two_stages_on_device(cuda):
     run_dist(_w_pp_gpu, 2, device="cuda", backend="gloo")
+
+
+def test_pipeline_interleaved_on_device(cuda):
+    """Interleaved 1F1B (2 chunks per rank, ring edge 1 -> 0) with HIP tensors end to end."""
+    run_dist(_w_pp_gpu, 2, "interleaved", device="cuda", backend="gloo")
 
 
 def _w_dp_gpu(rank, world):

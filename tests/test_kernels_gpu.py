@@ -417,3 +417,16 @@ def test_norm_fork_gradient_joins_backward(cuda, rms):
     ((yr * g1.float()).sum() + (xr * g2.float()).sum()).backward()
     assert _rel(x.grad, xr.grad) < 2e-2
     assert _rel(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("shape,dt", [((4096, 4096), torch.bfloat16), ((333, 24), torch.float32),
+                                      ((7, 8), torch.bfloat16)])
+def test_gelu_fwd_kernel_matches_fp32(cuda, shape, dt):
+    torch.manual_seed(4)
+    x = (torch.randn(*shape, device=cuda) * 3).to(dt)
+    x.view(-1)[:4] = torch.tensor([-30.0, 30.0, 0.0, -0.75], device=cuda).to(dt)  # saturation, zero, minimum
+    y = madnn.ops.gelu_tanh(x)
+    yr = torch.nn.functional.gelu(x.float(), approximate="tanh")
+    assert y.dtype == dt
+    torch.testing.assert_close(y.float(), yr, atol=1e-2 if dt == torch.bfloat16 else 1e-5,
+                               rtol=1e-2 if dt == torch.bfloat16 else 1e-5)
