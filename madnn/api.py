@@ -289,18 +289,27 @@ def synchronize_model(model: nn.Module, group=None, params: bool = True, grads: 
 
 
 class _PeriodicSync:
-    """Backward-counting auto-sync (R7): every ``period`` backward passes of the
-    root model, average parameters and gradients.  Hooks go on the root's own
-    parameters only — no class-wide monkey patch (SURVEY A-8), so nested
-    containers cannot double-sync."""
+    """Auto-sync (R7): average parameters and gradients every ``period`` SAMPLES of the root
+    model's training, counted as the reference counts them (datamodule.lua:102,151: one per
+    backward / trainer step of a single example).  A backward over a minibatch advances the
+    counter by its batch size when the caller says how many samples it held
+    (:meth:`count_next`; ``Trainer`` does), otherwise by one.  The sync fires whenever the counter
+    crosses a multiple of the period.  Hooks go on the root's own parameters only -- no
+    class-wide monkey patch (SURVEY A-8), so nested containers cannot double-sync."""
 
     def __init__(self, model: nn.Module, period: int, local_size: int, group=None):
         self.model, self.period, self.local_size, self.group = model, period, local_size, group
-        self.counter = 0
+        self.counter = 0          # samples seen
+        self.backwards = 0
         self.syncs = 0
+        self._next = None
         self._armed = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._hook) for p in model.parameters()
                        if p.requires_grad]
+
+    def count_next(self, samples: int) -> None:
+        """The next backward pass covers ``samples`` samples (minibatch training)."""
+        self._next = int(samples)
 
     def _hook(self, _p):
         if not self._armed:
@@ -309,8 +318,12 @@ class _PeriodicSync:
 
     def _on_end(self):
         self._armed = False
-        self.counter += 1
-        if self.counter % self.period == 0:
+        n = self._next if self._next is not None else 1
+        self._next = None
+        before = self.counter
+        self.counter += n
+        self.backwards += 1
+        if self.counter // self.period > before // self.period:
             self.sync()
 
     def sync(self):
@@ -325,7 +338,7 @@ class _PeriodicSync:
 
 _USAGE = ("usage: madnn.parallelize(data, targets, model, size=None, sync_every=None)\n"
           "  data/targets: sliceable datasets; model: nn.Module; size: dataset size (default len(data));\n"
-          "  sync_every: sync period in backward passes (None = heuristic, -1 = manual)")
+          "  sync_every: sync period in SAMPLES, as the reference counts (None = heuristic, -1 = manual)")
 
 
 def parallelize(data, targets, model: nn.Module, size: Optional[int] = None, sync_every: Optional[int] = None, *,
@@ -335,8 +348,11 @@ def parallelize(data, targets, model: nn.Module, size: Optional[int] = None, syn
     Starts the communicator, broadcasts the initial parameters from rank 0
     (always — SURVEY A-6), shards ``data``/``targets`` into contiguous stripes
     (R5), and unless ``sync_every == -1`` (manual mode, R12) installs periodic
-    synchronisation of parameters and gradients every ``sync_every`` backward
-    passes (default: the reference heuristic on the local shard size, R6).
+    synchronisation of parameters and gradients every ``sync_every`` SAMPLES -- the
+    reference's unit (its ``batchSize`` argument counts per-example backward calls,
+    datamodule.lua:102,151; SURVEY A-1): a minibatch of B samples trained through
+    :class:`Trainer` advances the count by B, a bare ``loss.backward()`` by one.  Default:
+    the reference heuristic on the local shard size (R6).
 
     Returns ``(data_shard, target_shard, shard_size)``; on missing arguments
     prints the usage and returns ``-1`` like the reference.  The chosen period
@@ -425,6 +441,9 @@ class Trainer:
                     x, y = x.to(self.device), y.to(self.device)
                 if self.meter is not None:
                     self.meter.start()
+                ps = getattr(self.model, "_madnn_sync", None)
+                if ps is not None:
+                    ps.count_next(len(idx))  # the period counts samples (reference semantics)
                 self.optimizer.zero_grad(set_to_none=True)
                 out = self.model(x)
                 loss = self.criterion(out, y)

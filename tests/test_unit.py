@@ -518,3 +518,21 @@ def test_auto_bucket_size():
     assert auto_bucket_mb(0.71e9) == 64.0                                 # GPT-2 medium: capped
     assert auto_bucket_mb(1e6) == 4.0                                     # tiny models: floor
     assert Config.from_env().bucket_mb == 0.0
+
+
+def test_periodic_sync_counts_samples():
+    """The auto-sync period is in SAMPLES (reference datamodule.lua:102,151): a 16-sample
+    minibatch advances it by 16, a bare backward by 1; a sync fires on every crossed multiple."""
+    from madnn.api import _PeriodicSync
+
+    m = torch.nn.Linear(4, 2)
+    ps = _PeriodicSync(m, period=10, local_size=100)
+    calls = []
+    ps.sync = lambda: calls.append(ps.counter)
+    for _ in range(3):  # 16-sample minibatches: 16, 32, 48 cross 10, 30, 40
+        ps.count_next(16)
+        m(torch.randn(16, 4)).sum().backward()
+    assert ps.counter == 48 and calls == [16, 32, 48]
+    for _ in range(2):  # per-sample backward: 49, 50 -> crosses 50
+        m(torch.randn(1, 4)).sum().backward()
+    assert ps.counter == 50 and calls[-1] == 50 and ps.backwards == 5
