@@ -64,6 +64,10 @@ int madnn_stem_stat_rows(int, int, int);
 hipError_t madnn_stem_fwd(const void*, const void*, void*, float*, int, int, int, hipStream_t);
 int64_t madnn_stem_wgrad_ws(int, int, int);
 hipError_t madnn_stem_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
+int madnn_gemm_supported(int64_t, int64_t, int64_t, int64_t, int64_t);
+hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
+                            int64_t, int64_t, hipStream_t);
+hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
 }
 
 namespace {
@@ -451,6 +455,76 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x) {
   return dw;
 }
 
+// ---- K12 MFMA GEMM (Linear layers) ------------------------------------------------------------
+// x: [..., K] bf16 with contiguous rows, w: [N, K] bf16 contiguous.
+void gemm_check(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "linear: ", name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), "linear: ", name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "linear: ", name, " must be 16-B aligned");
+}
+
+// y = x w^T (+ bias) (-> tanh-GELU) (+ res); with save_aux the pre-activation is returned too
+std::tuple<at::Tensor, at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w,
+                                              const c10::optional<at::Tensor>& bias,
+                                              const c10::optional<at::Tensor>& res, int64_t act, bool save_aux) {
+  gemm_check(x, "x");
+  gemm_check(w, "w");
+  const int64_t K = x.size(-1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "linear: weight must be [N, K]");
+  TORCH_CHECK(madnn_gemm_supported(N, M, K, K, K), "linear: unsupported shape M=", M, " N=", N, " K=", K);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = N;
+  at::Tensor y = at::empty(shape, x.options());
+  at::Tensor aux = save_aux ? at::empty(shape, x.options()) : at::empty({0}, x.options());
+  const bool hb = bias.has_value() && bias->defined();
+  if (hb) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() &&
+                    (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16),
+                "linear: bias must be a contiguous fp32/bf16 [N]");
+  }
+  const bool hr = res.has_value() && res->defined();
+  if (hr) {
+    gemm_check(*res, "res");
+    TORCH_CHECK(res->numel() == M * N && res->size(-1) == N, "linear: residual shape");
+  }
+  check(madnn_linear_fwd(x.data_ptr(), w.data_ptr(), hb ? bias->data_ptr() : nullptr,
+                         hb && bias->scalar_type() == at::kFloat ? 1 : 0, hr ? res->data_ptr() : nullptr, y.data_ptr(),
+                         save_aux ? aux.data_ptr() : nullptr, (int)act, M, N, K, cur_stream(x)),
+        "linear_fwd");
+  return {y, aux};
+}
+
+// dx = dy w (+ res).  With accumulate, res itself receives the result (in-place beta = 1).
+at::Tensor linear_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res,
+                        bool accumulate) {
+  gemm_check(dy, "dy");
+  gemm_check(w, "w");
+  const int64_t N = dy.size(-1), K = w.size(1), M = dy.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == N, "linear_dgrad: weight must be [N, K]");
+  TORCH_CHECK(madnn_gemm_supported(K, M, N, K, N), "linear_dgrad: unsupported shape M=", M, " N=", N, " K=", K);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  const bool hr = res.has_value() && res->defined();
+  if (hr) {
+    gemm_check(*res, "res");
+    TORCH_CHECK(res->numel() == M * K && res->size(-1) == K, "linear_dgrad: residual shape");
+  }
+  at::Tensor dx;
+  if (hr && accumulate) {
+    dx = *res;
+  } else {
+    std::vector<int64_t> shape(dy.sizes().begin(), dy.sizes().end());
+    shape.back() = K;
+    dx = at::empty(shape, dy.options());
+  }
+  check(madnn_linear_dgrad(dy.data_ptr(), w.data_ptr(), hr ? res->data_ptr() : nullptr, dx.data_ptr(), M, N, K,
+                           cur_stream(dy)),
+        "linear_dgrad");
+  return dx;
+}
+
 // ---- K10 ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 ---------
 void stem_check_x(const at::Tensor& x) {
   check_dev(x, "x");
@@ -718,6 +792,8 @@ TORCH_LIBRARY(madnn, m) {
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
   m.def("conv1x1_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
+  m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
+  m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
@@ -764,4 +840,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("conv1x1_wgrad", conv1x1_wgrad);
   m.impl("stem_fwd", stem_fwd);
   m.impl("stem_wgrad", stem_wgrad);
+  m.impl("linear_fwd", linear_fwd);
+  m.impl("linear_dgrad", linear_dgrad);
 }

@@ -1,0 +1,396 @@
+// K12 — bf16 MFMA GEMM for gfx950 with fused epilogues: the Linear layers of the transformer
+// models (forward with bias / tanh-GELU / residual, data gradient with in-place accumulation).
+//
+// Why: the GPT-2 medium step is ~2/3 hipBLASLt GEMMs (profiles/r2_bench_all_rehearsal1.md),
+// which run at ~1.15 PF/s on MI355X (madnn/tuning/hw_mi355x.json, 8192^3), and hipBLASLt
+// refuses its GELU/bias epilogues at GPT-2's 65536-row shapes ("no algorithm"), so the GELU
+// is a separate HBM pass (K11 gelu_fwd).  This kernel follows the CDNA4 structure that
+// reaches ~1.3-1.5 PF/s in plain HIP (cdna_hip_programming.md §5 "The 256^2 8-phase
+// template"): a 256x256 output tile per 512-thread workgroup, LDS-DMA staging with counted
+// vmcnt waits that never drain in the main loop, and two wave groups one barrier apart so
+// that one group's LDS reads and DMA issue overlap the other group's MFMAs on the same SIMD.
+//
+// Problem: Out[j][i] = sum_k A(i, k) B(k, j)   (bf16 in, fp32 accumulate, bf16 out)
+//   * "row" operand memory: X[x][k], k contiguous (ds_read_b128 fragments);
+//   * "col" operand memory: X[k][x], x contiguous (ds_read_b64_tr_b16 fragments).
+//   linear forward : i = out feature (A = W[n][k], row), j = token (B = X[m][k], row)
+//   linear dgrad   : i = in feature  (A = W[n][k] read as [k=n][i], col), j = token (B = dY, row)
+// i sits on the accumulator rows, j on the MFMA lane, so a lane owns 4 consecutive i of one
+// output row (the same orientation as K9, conv.hip).
+//
+// Geometry: 8 waves = 2 groups (wr: i half of the tile) x 4 (wc: 64-column j quarter);
+// each wave owns a 128 x 64 block of D = 4 x 2 v_mfma_f32_32x32x16_bf16 accumulators
+// (128 VGPRs).  K steps of 64.  LDS = 2 stages x 4 half-tiles (A i-half 0/1, B j-half 0/1)
+// of 128 x 64 bf16 = 128 KiB, one workgroup per CU.
+//
+// Schedule (per K tile: 4 phases, one per 64x32 quadrant of the wave block):
+//   phase q: LOAD  = ds_read this quadrant's new fragments + issue one half-tile of DMA
+//            s_barrier
+//            MFMA  = 8 MFMAs (setprio 1)
+//            s_barrier
+//   Q0 reads A(i 0..63) + B(j 0..31), Q1 B(j 32..63), Q2 A(i 64..127), Q3 nothing.
+//   Group 1 issues one extra barrier first, so its LOAD segments coincide with group 0's MFMA
+//   segments and vice versa.
+//   DMA: half-tile H (K tile H/4, part H%4) is issued in global phase H-5; the Q3 LOAD of
+//   K tile t waits vmcnt(2) (only the half-tile just issued, H = 4t+8, stays in flight), so
+//   K tile t+1 has landed before barrier 8(t+1) and is read after it by both groups.
+//   WAR: a stage is last read in Q2; that LOAD ends with lgkmcnt(0) before its barrier, so
+//   every wave's reads of the stage retire before the barrier that precedes the first DMA
+//   into it (phase 4u-5 for K tile u).  Derivation in docs/ARCHITECTURE.md (K12).
+// LDS images are lane-linear (DMA writes base + 16*lane); the XOR swizzles of mfma.h are
+// applied to the per-lane SOURCE address and to the read address (cdna_hip_programming.md
+// rule 21), so both fragment kinds read conflict-free.
+//
+// Epilogue: bias added in fp32, rounded to bf16 once, the tile staged through LDS as bf16
+// [256 j][256 i] (XOR-swizzled 16-B chunks) and stored as full 512-B rows; in that row pass:
+// aux = pre-activation store, tanh-GELU, residual add (fp32 add of two bf16, one rounding:
+// the same two roundings as the unfused PyTorch graph).
+#include "mfma.h"
+
+namespace madnn {
+namespace gemm {
+
+using namespace mf;
+
+constexpr int kThreads = 512;
+constexpr int kT = 256;                  // output tile (both i and j)
+constexpr int kBK = 64;
+constexpr int kHalf = 128 * kBK;         // bf16 elements of one half-tile (16 KiB)
+constexpr int kStage = 4 * kHalf;        // A0 A1 B0 B1
+constexpr int kLds = 2 * kStage;         // 128 KiB
+
+struct Args {
+  const uint16_t* a;
+  const uint16_t* b;
+  uint16_t* out;
+  const uint16_t* res;  // epilogue: out = y + res (same [j][i] layout, row stride ldr), or null
+  const void* bias;     // [I] fp32 (bias_f32) or bf16, or null
+  uint16_t* aux;        // pre-activation store (row stride ldx), or null
+  int64_t lda, ldb, ldo, ldr, ldx;
+  int64_t I, J, K;
+  int i_tiles, j_tiles;
+  int bias_f32, act;    // act: 0 none, 1 tanh-GELU
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// per-lane source offset (elements) of DMA instruction `inst` (0..15) of a half-tile, relative to
+// the half-tile's first row (row mode) / first column at its first k row (col mode)
+template <bool COL>
+__device__ __forceinline__ int64_t dma_offset(int inst, int lane, int64_t ld, int64_t first, int64_t lim) {
+  if constexpr (!COL) {
+    // [128 rows][64 k], 128-B rows: LDS slot s of row r holds chunk s ^ f(r) (swz<64>)
+    const int r = inst * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3));
+    int64_t row = first + r;
+    row = row < lim ? row : lim - 1;
+    return (row - first) * ld + 8 * ch;
+  } else {
+    // [64 k][128 cols], 256-B rows: slot s of k row r holds chunk s ^ g(r) (swz<128>)
+    const int r = inst * 4 + (lane >> 4);
+    const int ch = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    int64_t col = first + 8 * ch;
+    col = col + 8 <= lim ? col : lim - 8;
+    return (int64_t)r * ld + (col - first);
+  }
+}
+
+template <bool COL>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* tile, int s, int x, int lane) {
+  if constexpr (COL) {
+    return lds_col<128>(tile, 16 * s, x, lane);
+  } else {
+    return lds_row(tile, x + (lane & 31), 2 * s + (lane >> 5));
+  }
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  // tanh(u) = 1 - 2 / (exp(2u) + 1)
+  const float e = __expf(2.f * u);
+  const float t = 1.f - 2.f / (e + 1.f);
+  return 0.5f * x * (1.f + t);
+}
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kLds];
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-grouped logical id (bijective remap), i tile fastest
+  int wid = blockIdx.x;
+  {
+    const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
+    wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
+  }
+  const int it = wid % p.i_tiles, jt = wid / p.i_tiles;
+  const int64_t i0 = (int64_t)it * kT, j0 = (int64_t)jt * kT;
+  const int nk = (int)(p.K / kBK);
+  const int total = 4 * nk;  // half-tiles
+
+  // per-lane DMA offsets: part (0,1: A halves; 2,3: B halves) x 2 instructions per wave
+  int64_t off[4][2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int inst = 2 * wave + e;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      off[h][e] = dma_offset<A_COL>(inst, lane, p.lda, i0 + 128 * h, p.I);
+      off[2 + h][e] = dma_offset<B_COL>(inst, lane, p.ldb, j0 + 128 * h, p.J);
+    }
+  }
+  // issue half-tile H: 2 DMA instructions per lane into stage (H/4)&1, part H%4
+  auto stage = [&](int H) {
+    const int u = H >> 2, part = H & 3;
+    const int64_t k0 = (int64_t)u * kBK;
+    const uint16_t* base;
+    if (part < 2) {
+      const int64_t x0 = i0 + 128 * part;
+      base = A_COL ? p.a + k0 * p.lda + x0 : p.a + x0 * p.lda + k0;
+    } else {
+      const int64_t x0 = j0 + 128 * (part - 2);
+      base = B_COL ? p.b + k0 * p.ldb + x0 : p.b + x0 * p.ldb + k0;
+    }
+    uint16_t* dst = smem + (u & 1) * kStage + part * kHalf + (2 * wave) * 512;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int64_t o;
+      // static index into off[][] (rule 20: no runtime-indexed register arrays)
+      if (part == 0) o = off[0][e];
+      else if (part == 1) o = off[1][e];
+      else if (part == 2) o = off[2][e];
+      else o = off[3][e];
+      __builtin_amdgcn_global_load_lds((const void*)(base + o), (lds_void*)(dst + e * 512), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+
+  // prologue: half-tiles 0..4 (K tile 0 + part 0 of K tile 1)
+#pragma unroll
+  for (int H = 0; H < 5; ++H)
+    if (H < total) stage(H);
+  if (total > 4) {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  if (wr == 1) barrier();  // group 1 runs one barrier behind
+
+  bf16x8 af[2][4], bf0[4], bf1[4];
+  const int bcol = (wc & 1) * 64;
+  for (int t = 0; t < nk; ++t) {
+    const uint16_t* sa = smem + (t & 1) * kStage + wr * kHalf;
+    const uint16_t* sb = smem + (t & 1) * kStage + (2 + (wc >> 1)) * kHalf;
+    const int P = 4 * t;
+    // ---- Q0: A rows 0..63, B cols 0..31
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf0[s] = frag<B_COL>(sb, s, bcol, lane);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, a * 32, lane);
+    }
+    if (P + 5 < total) stage(P + 5);
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[a][0] = mfma(af[a][s], bf0[s], acc[a][0]);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---- Q1: B cols 32..63
+#pragma unroll
+    for (int s = 0; s < 4; ++s) bf1[s] = frag<B_COL>(sb, s, bcol + 32, lane);
+    if (P + 6 < total) stage(P + 6);
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[a][1] = mfma(af[a][s], bf1[s], acc[a][1]);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---- Q2: A rows 64..127 (the stage's last reads: retire them before the barrier)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, 64 + a * 32, lane);
+    if (P + 7 < total) stage(P + 7);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[2 + a][1] = mfma(af[a][s], bf1[s], acc[2 + a][1]);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+    // ---- Q3: no reads; retire K tile t+1's DMA
+    if (P + 8 < total) {
+      stage(P + 8);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[2 + a][0] = mfma(af[a][s], bf0[s], acc[2 + a][0]);
+    __builtin_amdgcn_s_setprio(0);
+    barrier();
+  }
+  if (wr == 0) barrier();  // balance the stagger: every wave has now passed the same barriers
+
+  // ---- epilogue: (acc + bias) -> bf16 -> LDS [256 j][256 i] -> rows
+  char* ot = reinterpret_cast<char*>(smem);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int il = wr * 128 + a * 32 + 8 * g + 4 * hh;  // first of this lane's 4 i
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias != nullptr) {
+        const int64_t ig = i0 + il;
+        if (ig < p.I) {
+          if (p.bias_f32) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(p.bias) + ig);
+            bv[0] = v[0]; bv[1] = v[1]; bv[2] = v[2]; bv[3] = v[3];
+          } else {
+            const u32x2 v = *reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(p.bias) + ig);
+            bv[0] = bf16_to_f32((unsigned short)(v[0] & 0xffffu));
+            bv[1] = bf16_to_f32((unsigned short)(v[0] >> 16));
+            bv[2] = bf16_to_f32((unsigned short)(v[1] & 0xffffu));
+            bv[3] = bf16_to_f32((unsigned short)(v[1] >> 16));
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int jl = wc * 64 + b * 32 + l32;
+        const unsigned lo = (unsigned)f32_to_bf16(acc[a][b][4 * g] + bv[0]) |
+                            ((unsigned)f32_to_bf16(acc[a][b][4 * g + 1] + bv[1]) << 16);
+        const unsigned hi = (unsigned)f32_to_bf16(acc[a][b][4 * g + 2] + bv[2]) |
+                            ((unsigned)f32_to_bf16(acc[a][b][4 * g + 3] + bv[3]) << 16);
+        *reinterpret_cast<u32x2*>(ot + jl * 512 + 16 * ((il >> 3) ^ (jl & 31)) + 8 * hh) = u32x2{lo, hi};
+      }
+    }
+  }
+  __syncthreads();
+  const int c = tid & 31;
+  const int64_t ig = i0 + 8 * c;
+  if (ig < p.I) {
+#pragma unroll 4
+    for (int r = tid >> 5; r < kT; r += kThreads / 32) {
+      const int64_t jg = j0 + r;
+      if (jg >= p.J) break;
+      u32x4 v = *reinterpret_cast<const u32x4*>(ot + r * 512 + 16 * (c ^ (r & 31)));
+      if (p.aux != nullptr) *reinterpret_cast<u32x4*>(p.aux + jg * p.ldx + ig) = v;
+      if (p.act != 0 || p.res != nullptr) {
+        u32x4 rv = u32x4{0u, 0u, 0u, 0u};
+        if (p.res != nullptr) rv = *reinterpret_cast<const u32x4*>(p.res + jg * p.ldr + ig);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x0 = bf16_to_f32((unsigned short)(v[e] & 0xffffu));
+          float x1 = bf16_to_f32((unsigned short)(v[e] >> 16));
+          if (p.act == 1) {
+            x0 = round_bf16(gelu_tanh(x0));
+            x1 = round_bf16(gelu_tanh(x1));
+          }
+          if (p.res != nullptr) {
+            x0 += bf16_to_f32((unsigned short)(rv[e] & 0xffffu));
+            x1 += bf16_to_f32((unsigned short)(rv[e] >> 16));
+          }
+          v[e] = (unsigned)f32_to_bf16(x0) | ((unsigned)f32_to_bf16(x1) << 16);
+        }
+      }
+      *reinterpret_cast<u32x4*>(p.out + jg * p.ldo + ig) = v;
+    }
+  }
+}
+
+template <bool A_COL, bool B_COL>
+hipError_t launch(Args& p, hipStream_t s) {
+  p.i_tiles = (int)((p.I + kT - 1) / kT);
+  p.j_tiles = (int)((p.J + kT - 1) / kT);
+  const int64_t grid = (int64_t)p.i_tiles * p.j_tiles;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace gemm
+}  // namespace madnn
+
+using namespace madnn::gemm;
+
+extern "C" {
+
+// Shapes K12 takes: reduction % 64 == 0, output features % 8 == 0, 16-B aligned rows, and
+// 32-bit-safe per-lane DMA offsets.
+int madnn_gemm_supported(int64_t I, int64_t J, int64_t K, int64_t lda, int64_t ldb) {
+  if (I <= 0 || J <= 0 || K <= 0) return 0;
+  if (K % kBK || I % 8 || lda % 8 || ldb % 8) return 0;
+  return 1;
+}
+
+// Y[m][n] = X[m][k] W[n][k] (+ bias[n]) (-> gelu) (+ res[m][n]); aux (if given) = pre-activation
+hipError_t madnn_linear_fwd(const void* x, const void* w, const void* bias, int bias_f32, const void* res,
+                            void* y, void* aux, int act, int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  if (!madnn_gemm_supported(N, M, K, K, K)) return hipErrorInvalidValue;
+  Args p{};
+  p.a = static_cast<const uint16_t*>(w);
+  p.lda = K;
+  p.b = static_cast<const uint16_t*>(x);
+  p.ldb = K;
+  p.out = static_cast<uint16_t*>(y);
+  p.ldo = N;
+  p.res = static_cast<const uint16_t*>(res);
+  p.ldr = N;
+  p.bias = bias;
+  p.bias_f32 = bias_f32;
+  p.aux = static_cast<uint16_t*>(aux);
+  p.ldx = N;
+  p.act = act;
+  p.I = N;
+  p.J = M;
+  p.K = K;
+  return launch<false, false>(p, s);
+}
+
+// dX[m][k] = dY[m][n] W[n][k] (+ res[m][k]; res may alias dX for in-place accumulation)
+hipError_t madnn_linear_dgrad(const void* dy, const void* w, const void* res, void* dx, int64_t M, int64_t N,
+                              int64_t K, hipStream_t s) {
+  if (!madnn_gemm_supported(K, M, N, K, N)) return hipErrorInvalidValue;
+  Args p{};
+  p.a = static_cast<const uint16_t*>(w);  // A[i = k][kk = n] = W[n][k]: column memory
+  p.lda = K;
+  p.b = static_cast<const uint16_t*>(dy);  // B[kk = n][j = m] = dY[m][n]: row memory
+  p.ldb = N;
+  p.out = static_cast<uint16_t*>(dx);
+  p.ldo = K;
+  p.res = static_cast<const uint16_t*>(res);
+  p.ldr = K;
+  p.I = K;
+  p.J = M;
+  p.K = N;
+  return launch<true, false>(p, s);
+}
+
+}  // extern "C"
