@@ -31,12 +31,14 @@
 //   Q0 reads A(i 0..63) + B(j 0..31), Q1 B(j 32..63), Q2 A(i 64..127), Q3 nothing.
 //   Group 1 issues one extra barrier first, so its LOAD segments coincide with group 0's MFMA
 //   segments and vice versa.
-//   DMA: half-tile H (K tile H/4, part H%4) is issued in global phase H-5; the Q3 LOAD of
-//   K tile t waits vmcnt(2) (only the half-tile just issued, H = 4t+8, stays in flight), so
-//   K tile t+1 has landed before barrier 8(t+1) and is read after it by both groups.
-//   WAR: a stage is last read in Q2; that LOAD ends with lgkmcnt(0) before its barrier, so
-//   every wave's reads of the stage retire before the barrier that precedes the first DMA
-//   into it (phase 4u-5 for K tile u).  Derivation in docs/ARCHITECTURE.md (K12).
+//   DMA: half-tile H = 4u + p of K tile u, parts in the order B0, B1, A0, A1, is issued in
+//   global phase H-6; the Q3 LOAD of K tile t waits vmcnt(4) (the two B half-tiles of K tile
+//   t+2 issued in Q2/Q3 stay in flight), so K tile t+1 has landed before barrier 8(t+1) and
+//   is read after it by both groups; each half-tile gets >= 2 phases of latency cover.
+//   WAR: B half-tiles are last read in Q1, A half-tiles in Q2; both LOADs end with
+//   lgkmcnt(0) before their barrier, so every wave's reads of a half-tile retire before the
+//   barrier that precedes the first DMA into it (B: phase 4u-6, A: phase 4u-4 for K tile u).
+//   Derivation in docs/ARCHITECTURE.md (K12).
 // LDS images are lane-linear (DMA writes base + 16*lane); the XOR swizzles of mfma.h are
 // applied to the per-lane SOURCE address and to the read address (cdna_hip_programming.md
 // rule 21), so both fragment kinds read conflict-free.
@@ -148,9 +150,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
       off[2 + h][e] = dma_offset<B_COL>(inst, lane, p.ldb, j0 + 128 * h, p.J);
     }
   }
-  // issue half-tile H: 2 DMA instructions per lane into stage (H/4)&1, part H%4
+  // issue half-tile H: 2 DMA instructions per lane into stage (H/4)&1; H%4 = 0,1: B halves,
+  // 2,3: A halves (the B halves are consumed first, so they are restaged first)
   auto stage = [&](int H) {
-    const int u = H >> 2, part = H & 3;
+    const int u = H >> 2, part = (H + 2) & 3;
     const int64_t k0 = (int64_t)u * kBK;
     const uint16_t* base;
     if (part < 2) {
@@ -179,12 +182,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
 
-  // prologue: half-tiles 0..4 (K tile 0 + part 0 of K tile 1)
+  // prologue: half-tiles 0..5 (K tile 0 + the B halves of K tile 1)
 #pragma unroll
-  for (int H = 0; H < 5; ++H)
+  for (int H = 0; H < 6; ++H)
     if (H < total) stage(H);
   if (total > 4) {
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -204,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, a * 32, lane);
     }
-    if (P + 5 < total) stage(P + 5);
+    if (P + 6 < total) stage(P + 6);
     barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -216,7 +219,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     // ---- Q1: B cols 32..63
 #pragma unroll
     for (int s = 0; s < 4; ++s) bf1[s] = frag<B_COL>(sb, s, bcol + 32, lane);
-    if (P + 6 < total) stage(P + 6);
+    if (P + 7 < total) stage(P + 7);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the B half-tiles' last reads
     barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -230,8 +234,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, 64 + a * 32, lane);
-    if (P + 7 < total) stage(P + 7);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (P + 8 < total) stage(P + 8);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the A half-tiles' last reads
     barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -240,9 +244,11 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
       for (int a = 0; a < 2; ++a) acc[2 + a][1] = mfma(af[a][s], bf1[s], acc[2 + a][1]);
     __builtin_amdgcn_s_setprio(0);
     barrier();
-    // ---- Q3: no reads; retire K tile t+1's DMA
-    if (P + 8 < total) {
-      stage(P + 8);
+    // ---- Q3: no reads; retire K tile t+1's DMA (the B halves of K tile t+2 stay in flight)
+    if (P + 9 < total) {
+      stage(P + 9);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (P + 8 < total) {
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
