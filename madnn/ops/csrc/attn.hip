@@ -372,17 +372,24 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
           dp[kb] = mfma(lds_row<D>(sV[cur], kb * 32 + l32, 2 * s + hh), df[s], dp[kb]);
         }
       }
-      const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
+      // masking as one wave-uniform block on the scores (exp2(-inf) = 0): interior tiles run
+      // none of it (a per-element `if` costs an exec-mask branch per element)
+      if ((k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kb * 32 + acc_row(r, hh);
+            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+            sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
+          }
+        }
+      }
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = ex2(fmaf(sc[kb][r], a.scale_log2, -lse));
-          if (edge) {
-            const int key = k0 + kb * 32 + acc_row(r, hh);
-            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
-            p = ok ? p : 0.f;
-          }
+          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -lse));
           sc[kb][r] = p * (dp[kb][r] - dl);
         }
       }
@@ -452,49 +459,65 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   const int t0 = CAUSAL ? (kblk * kRowsWG) / kTile : 0;
   const int nt = (a.S + kTile - 1) / kTile - t0;
   const int total = G * nt;
-  auto src = [&](int it, const uint16_t*& qp, const uint16_t*& dp, int& q0, int& hq) {
-    hq = hk * G + it / nt;
-    q0 = (t0 + it % nt) * kTile;
+  // tile `it` = (query head hk*G + it / nt, query tile t0 + it % nt); the loop walks it with two
+  // counters instead of a per-tile integer division
+  auto src = [&](int hq_i, int t_i, const uint16_t*& qp, const uint16_t*& dp, int& q0, int& hq) {
+    hq = hk * G + hq_i;
+    q0 = (t0 + t_i) * kTile;
     qp = a.q + b * a.q_sb + hq * a.q_sh;
     dp = a.dout + b * a.o_sb + hq * a.o_sh;
   };
-  auto load_stats = [&](int it, int buf) {
-    const uint16_t *qp, *dp;
-    int q0, hq;
-    src(it, qp, dp, q0, hq);
+  // the tile's LSE (threads 0..63) / delta (64..127) row statistics: fetched into a register
+  // together with the tile's Q/dO loads and written to LDS with them, so their global-load
+  // latency is covered by the tile's compute (a load stored right away exposes it every tile)
+  auto fetch_stats = [&](int hq, int q0) -> float {
+    float v = 0.f;
+    if (tid < 2 * kTile) {
+      const int q = q0 + (tid & (kTile - 1));
+      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + min(q, a.S - 1);
+      v = tid < kTile ? a.lse[sr] : a.delta[sr];
+      if (q >= a.S) v = tid < kTile ? __builtin_inff() : 0.f;
+    }
+    return v;
+  };
+  auto put_stats = [&](float v, int buf) {
     if (tid < kTile) {
-      const int q = q0 + tid;
-      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + q;
-      sL[buf][tid] = q < a.S ? a.lse[sr] : __builtin_inff();
+      sL[buf][tid] = v;
     } else if (tid < 2 * kTile) {
-      const int q = q0 + tid - kTile;
-      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + q;
-      sD[buf][tid - kTile] = q < a.S ? a.delta[sr] : 0.f;
+      sD[buf][tid - kTile] = v;
     }
   };
   TileStage<D> stq, sto;
   if (total > 0) {
     const uint16_t *qp, *dp;
     int q0, hq;
-    src(0, qp, dp, q0, hq);
+    src(0, 0, qp, dp, q0, hq);
     stq.load(qp, a.q_ss, q0, a.S, tid);
     sto.load(dp, a.o_ss, q0, a.S, tid);
     stq.store(sQ[0], tid);
     sto.store(sO[0], tid);
-    load_stats(0, 0);
+    put_stats(fetch_stats(hq, q0), 0);
   }
   __syncthreads();
+  int cur_t = 0, nxt_h = 0, nxt_t = 0;  // this tile's query-tile index; the next tile's (head, tile)
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
     const bool more = it + 1 < total;
+    if (++nxt_t == nt) {
+      nxt_t = 0;
+      ++nxt_h;
+    }
+    float stat_next = 0.f;
     if (more) {
       const uint16_t *qp, *dp;
       int q0n, hqn;
-      src(it + 1, qp, dp, q0n, hqn);
+      src(nxt_h, nxt_t, qp, dp, q0n, hqn);
       stq.load(qp, a.q_ss, q0n, a.S, tid);
       sto.load(dp, a.o_ss, q0n, a.S, tid);
+      stat_next = fetch_stats(hqn, q0n);
     }
-    const int q0 = (t0 + it % nt) * kTile;
+    const int q0 = (t0 + cur_t) * kTile;
+    cur_t = nxt_t;
     if (!CAUSAL || q0 + kTile - 1 >= k0w) {
       f32x16 sc[2], dp[2];
 #pragma unroll
@@ -507,14 +530,22 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
           dp[qb] = mfma(lds_row<D>(sO[cur], qb * 32 + l32, 2 * s + hh), vf[s], dp[qb]);
         }
       }
-      const bool edge = CAUSAL && q0 < k0w + 31;
+      if (CAUSAL && q0 < k0w + 31) {  // diagonal tile: one wave-uniform masking block
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int qi = qb * 32 + acc_row(r, hh);
+            sc[qb][r] = (krow <= q0 + qi) ? sc[qb][r] : -__builtin_inff();
+          }
+        }
+      }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qi = qb * 32 + acc_row(r, hh);
-          float p = ex2(fmaf(sc[qb][r], a.scale_log2, -sL[cur][qi]));
-          if (edge) p = (krow <= q0 + qi) ? p : 0.f;
+          const float p = ex2(fmaf(sc[qb][r], a.scale_log2, -sL[cur][qi]));
           sc[qb][r] = p;
           dp[qb][r] = p * (dp[qb][r] - sD[cur][qi]);
         }
@@ -537,7 +568,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
     if (more) {
       stq.store(sQ[cur ^ 1], tid);
       sto.store(sO[cur ^ 1], tid);
-      load_stats(it + 1, cur ^ 1);
+      put_stats(stat_next, cur ^ 1);
     }
     __syncthreads();
   }
