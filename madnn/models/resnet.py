@@ -3,8 +3,10 @@ torchvision is not installed.  BASELINE config 2:
 "ResNet-50 auto data-parallel bf16 on 8xMI355X".
 
 The bottleneck 1x1 convolutions (stride 1) run on madnn's K9 MFMA GEMM kernels,
-which also compute the following BatchNorm's batch statistics in their epilogue; the
-3x3 / stride-2 convolutions run on MIOpen through PyTorch-ROCm; the 7x7 stem runs on K10 (MFMA
+which also compute the following BatchNorm's batch statistics in their epilogue; the stride-1
+3x3 convolutions run on K13 (MFMA implicit GEMM over an LDS-staged input halo, statistics in the
+epilogue, data grad on the flipped weight); the stride-2 convolutions run on MIOpen through
+PyTorch-ROCm; the 7x7 stem runs on K10 (MFMA
 forward with the BatchNorm statistics in its epilogue, MFMA weight gradient); the stem max-pool is madnn's
 NHWC kernel (K7, byte argmax + gather backward); every
 BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
@@ -30,7 +32,8 @@ _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
+    # stride 1 runs on K13 (forward + BN statistics, data grad); stride 2 on MIOpen
+    return FusedConv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
 
 
 def conv1x1(cin, cout, stride=1):
@@ -50,8 +53,10 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), relu=True)
-        return self.bn2(self.conv2(out), residual=idt, relu=True)
+        y, st = self.conv1(x, stats=True)
+        out = self.bn1(y, relu=True, stats=st)
+        y, st = self.conv2(out, stats=True)
+        return self.bn2(y, residual=idt, relu=True, stats=st)
 
 
 class Bottleneck(nn.Module):
@@ -80,7 +85,8 @@ class Bottleneck(nn.Module):
             idt = self.downsample(x)
             y, st = self.conv1(x, stats=True)
         out = self.bn1(y, relu=True, stats=st)
-        out = self.bn2(self.conv2(out), relu=True)
+        y, st = self.conv2(out, stats=True)   # K13 at stride 1: BN statistics from the epilogue
+        out = self.bn2(y, relu=True, stats=st)
         y, st = self.conv3(out, stats=True)
         return self.bn3(y, residual=idt, relu=True, stats=st)   # relu(bn3 + idt): one kernel
 

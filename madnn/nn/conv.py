@@ -7,8 +7,11 @@ forward, data grad, weight grad) and can hand the following
 :class:`~madnn.nn.FusedBatchNorm2d` its batch statistics, computed in the GEMM
 epilogue, so the BatchNorm skips its statistics pass.  Every other configuration runs
 ``nn.Conv2d`` (MIOpen on the GPU), except the ResNet stem (7x7, stride 2, pad 3, 3 -> 64
-channels), which runs on K10 (``madnn.ops.stem_conv``, also with the BatchNorm statistics).
-``MADNN_CONV1X1=0`` / ``MADNN_STEM=0`` disable the K9 / K10 paths (A/B runs).
+channels), which runs on K10 (``madnn.ops.stem_conv``, also with the BatchNorm statistics), and
+3x3 / stride 1 / pad 1 convolutions with channel counts that are multiples of 64, which run on K13
+(``madnn.ops.conv3x3``: forward with the statistics, data grad; weight grad on MIOpen).
+``MADNN_CONV1X1=0`` / ``MADNN_STEM=0`` / ``MADNN_CONV3X3=0`` disable the K9 / K10 / K13 paths
+(A/B runs).
 """
 from __future__ import annotations
 
@@ -28,6 +31,11 @@ class FusedConv2d(nn.Conv2d):
                 and self.groups == 1 and self.bias is None and self.padding in ((0, 0), "valid")
                 and ops.conv1x1_supported(x, self.weight))
 
+    def _k13(self, x: torch.Tensor) -> bool:
+        return (self.kernel_size == (3, 3) and self.stride == (1, 1) and self.padding == (1, 1)
+                and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
+                and self.padding_mode == "zeros" and ops.conv3x3_supported(x, self.weight))
+
     def _k10(self, x: torch.Tensor) -> bool:
         return (self.kernel_size == (7, 7) and self.stride == (2, 2) and self.padding == (3, 3)
                 and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
@@ -40,6 +48,8 @@ class FusedConv2d(nn.Conv2d):
         inside this convolution's data-grad kernel instead of by a separate add."""
         if self._k9(x):
             return ops.conv1x1(x, self.weight, stats=stats, fork=fork)
+        if not fork and self._k13(x):
+            return ops.conv3x3(x, self.weight, stats=stats)
         if not fork and self._k10(x):
             return ops.stem_conv(x, self.weight, stats=stats)
         out = [super().forward(x)]
@@ -50,5 +60,6 @@ class FusedConv2d(nn.Conv2d):
         return out[0] if len(out) == 1 else tuple(out)
 
     def extra_repr(self):
-        k = {(1, 1): ", kernel=madnn.K9", (7, 7): ", kernel=madnn.K10"}.get(self.kernel_size, "")
+        k = {(1, 1): ", kernel=madnn.K9", (7, 7): ", kernel=madnn.K10",
+             (3, 3): ", kernel=madnn.K13" if self.stride == (1, 1) else ""}.get(self.kernel_size, "")
         return super().extra_repr() + k

@@ -553,6 +553,75 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
     return ret[0] if len(ret) == 1 else tuple(ret)
 
 
+# ---------------------------------------------------------------------- K13
+_K13 = os.environ.get("MADNN_CONV3X3", "1") != "0"
+_K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A/B runs)
+
+
+def _k13_halo_ok(W: int) -> bool:
+    # conv3.hip: halo_capacity(W) * 128 + 128 + 16 KiB of weights <= 80 KiB (two workgroups per CU)
+    cap = ((255 // W) * W + 4 * W + 7) // 8 * 8
+    return cap * 128 + 128 + 2 * 64 * 64 * 2 <= 80 * 1024
+
+
+def conv3x3_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Inputs K13 takes: NHWC bf16 HIP activations, bf16 [Co, Ci, 3, 3] weight, Ci and Co multiples
+    of 64, image width whose input halo fits the kernel's LDS budget (W <= 56 or so)."""
+    if not _K13 or x.device.type != "cuda" or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.numel() == 0:
+        return False
+    if w.dim() != 4 or tuple(w.shape[1:]) != (x.size(1), 3, 3):
+        return False
+    return x.size(1) % 64 == 0 and w.size(0) % 64 == 0 and _k13_halo_ok(x.size(3))
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    """3x3 / stride 1 / pad 1 convolution (K13): MFMA implicit GEMM forward over an LDS-staged input
+    halo with the BatchNorm statistics in its epilogue; the data gradient is the same kernel on the
+    flipped, transposed weight (a correlation with W'[ci][kh][kw][co] = W[co][2-kh][2-kw][ci]); the
+    weight gradient stays on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, stats):
+        y, part = torch.ops.madnn.conv3x3_fwd(x, _cl(w), bool(stats))
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        dy = _nhwc(dy.to(x.dtype))
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if _K13_DGRAD == "k13":
+                wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+                dx = torch.ops.madnn.conv3x3_fwd(dy, wt, False)[0]
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                                                         (True, False, False))[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                                                     (False, True, False))[1]
+            if dw.stride() != w.stride():
+                dw = torch.empty_like(w).copy_(dw)
+        return dx, dw, None
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False):
+    """``conv2d(x, w, stride=1, padding=1)`` of an NHWC bf16 HIP tensor on K13 (see
+    :func:`conv3x3_supported`).  ``stats``: also return per-tile channel (sum, sum of squares)
+    partials of y for :func:`batch_norm_act`."""
+    _need_native("conv3x3")
+    y, part = _Conv3x3Fn.apply(x, w, stats)
+    return (y, part) if stats else y
+
+
 # ---------------------------------------------------------------------- K10
 _K10 = os.environ.get("MADNN_STEM", "1") != "0"
 

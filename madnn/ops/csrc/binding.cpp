@@ -65,6 +65,9 @@ hipError_t madnn_stem_fwd(const void*, const void*, void*, float*, int, int, int
 int64_t madnn_stem_wgrad_ws(int, int, int);
 hipError_t madnn_stem_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
 int madnn_gemm_supported(int64_t, int64_t, int64_t, int64_t, int64_t);
+int madnn_conv3x3_supported(int, int, int, int);
+int madnn_conv3x3_stat_rows(int64_t);
+hipError_t madnn_conv3x3_fwd(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
@@ -525,6 +528,28 @@ at::Tensor linear_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::op
   return dx;
 }
 
+// ---- K13 NHWC 3x3 / stride 1 / pad 1 convolution on MFMA --------------------------------------
+// x: [N, Ci, H, W] channels_last bf16; w: [Co, Ci, 3, 3] channels_last ([Co][3][3][Ci] in memory).
+std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3: bf16 only");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv3x3: x must be NHWC 4-D");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: w must be a channels_last [Co, Ci, 3, 3]");
+  const int N = (int)x.size(0), Ci = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Co = (int)w.size(0);
+  TORCH_CHECK(madnn_conv3x3_supported(H, W, Ci, Co), "conv3x3: unsupported shape Ci=", Ci, " Co=", Co, " W=", W);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t rows = stats ? madnn_conv3x3_stat_rows((int64_t)N * H * W) : 0;
+  at::Tensor part = at::empty({rows, 2, Co}, x.options().dtype(at::kFloat));
+  check(madnn_conv3x3_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, N, H,
+                          W, Ci, Co, cur_stream(x)),
+        "conv3x3_fwd");
+  return {y, part};
+}
+
 // ---- K10 ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 ---------
 void stem_check_x(const at::Tensor& x) {
   check_dev(x, "x");
@@ -794,6 +819,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
+  m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
@@ -842,4 +868,5 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("stem_wgrad", stem_wgrad);
   m.impl("linear_fwd", linear_fwd);
   m.impl("linear_dgrad", linear_dgrad);
+  m.impl("conv3x3_fwd", conv3x3_fwd);
 }

@@ -1,0 +1,285 @@
+// K13 — NHWC 3x3 / stride 1 / pad 1 convolution on MFMA for gfx950 (forward with the following
+// BatchNorm's batch statistics in the epilogue; the data gradient is the same kernel run on the
+// flipped, transposed weight).
+//
+// Why: ResNet-50's 3x3 stride-1 convolutions on MIOpen's find-db solvers run at 0.18-0.34 of
+// their roofline bound in every pass (profiles/r2_resnet50_conv_roofline_b1536.md: 26 ms/step
+// against 6.5 ms at batch 1536) -- the furthest of any kernel family in the step.
+//
+// Structure: implicit GEMM  D[co][m] = sum_{tap, ci} W[co][tap][ci] X[pix(m) + off(tap)][ci]
+// with the output pixel m on the MFMA lane and the output channel co on the accumulator rows
+// (a lane owns 4 consecutive co of one pixel, the K9 orientation).  A workgroup (4 waves)
+// owns 256 consecutive output pixels (NHWC order) x 64 output channels; each wave 64 pixels x 64
+// channels = 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators.  Per 64-channel input chunk the
+// workgroup stages the input HALO once -- every input row the tile's 3x3 windows touch, a
+// contiguous NHWC range -- into LDS, so the nine taps read it nine times from LDS instead of
+// nine times from L2.  The weights of one (tap, chunk), [64 co][64 ci] = 8 KiB, stream through a
+// two-slot LDS ring one tap ahead.  Both images are filled by LDS-DMA (global_load_lds, 16 B per
+// lane, lane-linear destination) with the swz<64> XOR applied to the per-lane source address
+// (cdna_hip_programming.md rule 21), and read conflict-free with ds_read_b128.
+// A tap whose source pixel leaves the image (top/bottom rows, first/last column, image seams in
+// the flattened NHWC order) reads a zero row in LDS instead: no data-dependent branches.
+// LDS: halo (<= (255/W + 4) * W pixels x 128 B, 57 KiB at W = 56) + zero row + 16 KiB weights:
+// two workgroups per CU, so one workgroup's halo load overlaps the other's MFMAs.
+// Epilogue: the K9 LDS-transposed row store (16-B stores of 64 contiguous channels per pixel)
+// and, with `stats`, per-channel sum / sum of squares of the bf16-rounded outputs as one
+// [2][Cout] partial row per pixel tile (the input of bn.hip's finalize).
+#include "mfma.h"
+
+namespace madnn {
+namespace conv3 {
+
+using namespace mf;
+
+constexpr int kThreads = 256;
+constexpr int kBJ = 256;  // output pixels per workgroup
+constexpr int kBI = 64;   // output channels per workgroup
+constexpr int kWElems = 64 * 64;  // one (tap, chunk) weight tile
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct Args {
+  const uint16_t* x;   // [M = N*H*W][Ci]
+  const uint16_t* w;   // [Co][9][Ci] (channels_last weight)
+  uint16_t* y;         // [M][Co]
+  float* stats;        // [m_tiles][2][Co] or null
+  int64_t M;
+  int H, W, Ci, Co;
+  int halo_px;         // LDS halo capacity in pixels
+  int m_tiles, co_tiles;
+};
+
+// halo pixels a tile can touch, rounded up to whole 8-pixel DMA instructions (so the last
+// instruction never writes past the halo into the zero row)
+__host__ __device__ inline int halo_capacity(int W) { return ((kBJ - 1) / W * W + 4 * W + 7) / 8 * 8; }
+
+__device__ __forceinline__ int fswz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+
+template <bool STATS>
+__global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* halo = smem;                               // [halo_px][64]
+  uint16_t* zrow = smem + (int64_t)p.halo_px * 64;     // [1][64] zeros
+  uint16_t* wring = zrow + 64;                         // [2][64][64]
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // XCD-grouped logical id; output-channel tile fastest (co tiles of one pixel tile share its halo in L2)
+  int wid = blockIdx.x;
+  {
+    const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
+    wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
+  }
+  const int cot = wid % p.co_tiles, mt = wid / p.co_tiles;
+  const int64_t j0 = (int64_t)mt * kBJ;
+  const int co0 = cot * kBI;
+  const int W = p.W, H = p.H;
+  const int64_t r_first = j0 / W;
+  const int64_t j_last = min(j0 + kBJ, p.M) - 1;
+  const int64_t hrow0 = r_first - 1;                   // first halo row (may be -1: clamped, never read)
+  const int hpx = (int)((j_last / W - r_first + 3) * W);  // halo pixels this tile
+
+  // per-lane output pixels (two 32-pixel blocks of this wave): centre-tap halo index + edge flags
+  int hb[2];
+  unsigned edge[2];  // bit0: h >= 1 (row above exists), bit1: h <= H-2, bit2: w >= 1, bit3: w <= W-2
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    int64_t m = j0 + wave * 64 + jb * 32 + l32;
+    m = m < p.M ? m : p.M - 1;
+    const int64_t r = m / W;
+    const int wc = (int)(m - r * W);
+    const int h = (int)(r % H);
+    hb[jb] = (int)(r - hrow0) * W + wc;
+    edge[jb] = (h >= 1 ? 1u : 0u) | (h <= H - 2 ? 2u : 0u) | (wc >= 1 ? 4u : 0u) | (wc <= W - 2 ? 8u : 0u);
+  }
+  if (tid < 8) *reinterpret_cast<u32x4*>(zrow + tid * 8) = u32x4{0u, 0u, 0u, 0u};
+
+  const int nchunk = p.Ci / 64;
+  const int total = nchunk * 9;
+  const int64_t ldw = 9LL * p.Ci;
+
+  // LDS-DMA of the halo of input chunk c: 8 pixel rows (1 KiB) per wave-instruction
+  auto stage_halo = [&](int c) {
+    const int ninst = (hpx + 7) / 8;
+    for (int i = wave; i < ninst; i += 4) {
+      const int prow = i * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ fswz(prow);
+      int64_t src = hrow0 * W + prow;
+      src = src < 0 ? 0 : (src >= p.M ? p.M - 1 : src);
+      __builtin_amdgcn_global_load_lds((const void*)(p.x + src * p.Ci + c * 64 + 8 * ch),
+                                       (lds_void*)(halo + i * 512), 16, 0, 0);
+    }
+  };
+  // weights of step idx = (chunk idx / 9, tap idx % 9) into ring slot idx & 1: 2 instructions per wave
+  auto stage_w = [&](int c, int t, int slot) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int inst = wave * 2 + e;
+      const int row = inst * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ fswz(row);
+      __builtin_amdgcn_global_load_lds((const void*)(p.w + (int64_t)(co0 + row) * ldw + t * p.Ci + c * 64 + 8 * ch),
+                                       (lds_void*)(wring + slot * kWElems + inst * 512), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+
+  stage_halo(0);
+  stage_w(0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const char* hbase = reinterpret_cast<const char*>(halo);
+  const char* zbase = reinterpret_cast<const char*>(zrow);
+  int c = 0, t = 0;
+  for (int idx = 0; idx < total; ++idx) {
+    // next step's weights into the other slot (its last reader finished before the last barrier)
+    int cn = c, tn = t + 1;
+    if (tn == 9) {
+      tn = 0;
+      ++cn;
+    }
+    if (idx + 1 < total) stage_w(cn, tn, (idx + 1) & 1);
+    const uint16_t* wt = wring + (idx & 1) * kWElems;
+    // this tap's B-fragment row addresses (halo pixel or the zero row)
+    const int dh = t / 3, dw = t - 3 * (t / 3);
+    const unsigned need = (dh == 0 ? 1u : dh == 2 ? 2u : 0u) | (dw == 0 ? 4u : dw == 2 ? 8u : 0u);
+    const char* brow[2];
+    int bsw[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int hp = hb[jb] + (dh - 1) * W + (dw - 1);
+      const bool ok = (edge[jb] & need) == need;
+      brow[jb] = ok ? hbase + hp * 128 : zbase;
+      bsw[jb] = ok ? fswz(hp) : 0;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 af[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = lds_row(wt, a * 32 + l32, 2 * s + hh);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bv[b] = *reinterpret_cast<const bf16x8*>(brow[b] + 16 * ((2 * s + hh) ^ bsw[b]));
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma(af[a], bv[b], acc[a][b]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // next weights landed; this tap's reads of the ring slot / halo are done
+    if (tn == 0 && cn < nchunk) {  // next input chunk: restage the halo (every wave is past its reads)
+      stage_halo(cn);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    c = cn;
+    t = tn;
+  }
+
+  // ---- epilogue: D[co][px] -> bf16 tile [256 px][64 co] in LDS (128-B rows) -> 16-B row stores
+  char* ot = reinterpret_cast<char*>(smem);  // the halo region (>= 256 x 128 B) is free now
+  auto out_off = [](int r, int ch) { return r * 128 + 16 * (ch ^ ((r >> 1) & 7)); };
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int pr = wave * 64 + b * 32 + l32;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ic = a * 32 + 8 * g + 4 * hh;
+        const unsigned lo = (unsigned)f32_to_bf16(acc[a][b][4 * g]) | ((unsigned)f32_to_bf16(acc[a][b][4 * g + 1]) << 16);
+        const unsigned hi = (unsigned)f32_to_bf16(acc[a][b][4 * g + 2]) | ((unsigned)f32_to_bf16(acc[a][b][4 * g + 3]) << 16);
+        *reinterpret_cast<u32x2*>(ot + out_off(pr, ic >> 3) + 8 * ((ic >> 2) & 1)) = u32x2{lo, hi};
+      }
+  }
+  __syncthreads();
+  const int ch = tid & 7;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  for (int r = tid >> 3; r < kBJ; r += kThreads / 8) {
+    const int64_t m = j0 + r;
+    if (m >= p.M) break;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, ch));
+    *reinterpret_cast<u32x4*>(p.y + m * p.Co + co0 + 8 * ch) = v;
+    if constexpr (STATS) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x0 = bf16_to_f32((unsigned short)(v[e] & 0xffffu));
+        const float x1 = bf16_to_f32((unsigned short)(v[e] >> 16));
+        ssum[2 * e] += x0;
+        ssq[2 * e] += x0 * x0;
+        ssum[2 * e + 1] += x1;
+        ssq[2 * e + 1] += x1 * x1;
+      }
+    }
+  }
+  if constexpr (STATS) {
+    __syncthreads();  // the tile image is consumed
+    float* red = reinterpret_cast<float*>(smem);  // [32 row groups][2][64]
+    const int rg = tid >> 3;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(rg * 2) * 64 + 8 * ch + e] = ssum[e];
+      red[(rg * 2 + 1) * 64 + 8 * ch + e] = ssq[e];
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int which = tid >> 6, ci = tid & 63;
+      float v = 0.f;
+      for (int g = 0; g < kThreads / 8; ++g) v += red[(g * 2 + which) * 64 + ci];
+      p.stats[((int64_t)mt * 2 + which) * p.Co + co0 + ci] = v;
+    }
+  }
+}
+
+}  // namespace conv3
+}  // namespace madnn
+
+using namespace madnn::conv3;
+
+extern "C" {
+
+int madnn_conv3x3_supported(int H, int W, int Ci, int Co) {
+  if (H < 1 || W < 1 || Ci % 64 || Co % 64 || Ci < 64 || Co < 64 || Ci > 8192) return 0;
+  const size_t lds = (size_t)halo_capacity(W) * 128 + 128 + 2 * kWElems * 2;
+  return lds <= 80 * 1024 ? 1 : 0;  // two workgroups per CU
+}
+
+int madnn_conv3x3_stat_rows(int64_t M) { return (int)((M + kBJ - 1) / kBJ); }
+
+// y = conv3x3(x, w) (stride 1, pad 1); x [N, H, W, Ci] NHWC, w [Co, 3, 3, Ci] (channels_last),
+// y [N, H, W, Co]; stats (optional): [ceil(M/256)][2][Co] partial sums of y
+hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats, int N, int H, int W, int Ci, int Co,
+                             hipStream_t s) {
+  if (!madnn_conv3x3_supported(H, W, Ci, Co)) return hipErrorInvalidValue;
+  Args p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(y);
+  p.stats = stats;
+  p.M = (int64_t)N * H * W;
+  if (p.M <= 0) return hipSuccess;
+  p.H = H;
+  p.W = W;
+  p.Ci = Ci;
+  p.Co = Co;
+  p.halo_px = halo_capacity(W);
+  p.m_tiles = (int)((p.M + kBJ - 1) / kBJ);
+  p.co_tiles = Co / kBI;
+  const int64_t grid = (int64_t)p.m_tiles * p.co_tiles;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  const size_t lds = (size_t)p.halo_px * 128 + 128 + 2 * kWElems * 2;
+  if (stats) {
+    hipLaunchKernelGGL(conv3x3_kernel<true>, dim3((unsigned)grid), dim3(kThreads), lds, s, p);
+  } else {
+    hipLaunchKernelGGL(conv3x3_kernel<false>, dim3((unsigned)grid), dim3(kThreads), lds, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // extern "C"
