@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""K13 (madnn 3x3 conv) vs MIOpen (shipped find-db) on ResNet-50's stride-1 3x3 shapes, forward and
-data grad, same random bf16 NHWC operands, interleaved rounds in one process.
+"""K13 (madnn 3x3 conv) vs MIOpen (shipped find-db) on ResNet-50's stride-1 3x3 shapes, forward,
+data grad and weight grad, same random bf16 NHWC operands, interleaved rounds in one process.
     python bench/conv3x3_ab.py [--batch 1536] [--rounds 3] [--json out]"""
 from __future__ import annotations
 
@@ -53,7 +53,10 @@ def main():
              "dgrad_miopen": lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False,
                                                                           (0, 0), 1, (True, False, False)),
              "dgrad_k13": lambda: torch.ops.madnn.conv3x3_fwd(
-                 dy, w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last), False)}
+                 dy, w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last), False),
+             "wgrad_miopen": lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False,
+                                                                          (0, 0), 1, (False, True, False)),
+             "wgrad_k13": lambda: torch.ops.madnn.conv3x3_wgrad(dy, x, True)}
         ts = {k: [] for k in c}
         for k, f in c.items():
             f()

@@ -3,6 +3,7 @@
 interleaved timing windows (same box, same tensors):
 
     python bench/flag_ab.py --flag _K13 --windows 8 --steps 4 [--batch 1536]
+    python bench/flag_ab.py --flag _K13_WGRAD --on auto --off miopen
 """
 import argparse
 import json
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1536)
     ap.add_argument("--windows", type=int, default=8)
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--on", default="True", help="flag value of the 'on' arm (True/False or a string)")
+    ap.add_argument("--off", default="False")
     a = ap.parse_args()
     import madnn
     from madnn import ops
@@ -36,9 +39,10 @@ def main():
     dm, o = madnn.distribute(m, o, strategy="dp")
     x, y = madnn.data.synthetic_batch("image", a.batch, madnn.device(), dtype=torch.bfloat16, channels_last=True)
     base = getattr(ops, a.flag)
+    val = {True: {"True": True, "False": False}.get(a.on, a.on), False: {"True": True, "False": False}.get(a.off, a.off)}
 
     def window(on, n):
-        setattr(ops, a.flag, on)
+        setattr(ops, a.flag, val[on])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(n):
@@ -54,7 +58,7 @@ def main():
         on = w % 2 == 0
         res[on].append(window(on, a.steps))
     setattr(ops, a.flag, base)
-    out = {"flag": a.flag, "batch": a.batch, "on_ms": res[True], "off_ms": res[False],
+    out = {"flag": a.flag, "on": a.on, "off": a.off, "batch": a.batch, "on_ms": res[True], "off_ms": res[False],
            "on_median": statistics.median(res[True]), "off_median": statistics.median(res[False]),
            "on_img_s": round(a.batch / statistics.median(res[True]) * 1e3, 1),
            "off_img_s": round(a.batch / statistics.median(res[False]) * 1e3, 1)}

@@ -556,6 +556,10 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
 # ---------------------------------------------------------------------- K13
 _K13 = os.environ.get("MADNN_CONV3X3", "1") != "0"
 _K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A/B runs)
+# weight grad: "auto" = K13 on the wide layers (W >= 48: 686 vs 910 us at ResNet-50's 56x56 layer,
+# batch 1536), MIOpen on the narrower ones where it is as fast or faster
+# (profiles/r2_k13_conv3x3_vs_miopen.json); "k13" | "miopen" force one (A/B runs)
+_K13_WGRAD = os.environ.get("MADNN_CONV3X3_WGRAD", "auto")
 
 
 def _k13_halo_ok(W: int) -> bool:
@@ -606,9 +610,12 @@ class _Conv3x3Fn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
                                                          (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
-                                                     (False, True, False))[1]
-            if dw.stride() != w.stride():
+            if _K13_WGRAD == "k13" or (_K13_WGRAD == "auto" and x.size(3) >= 48):
+                dw = torch.ops.madnn.conv3x3_wgrad(dy, x, w.dtype == torch.bfloat16)
+            else:
+                dw = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                                                         (False, True, False))[1]
+            if dw.stride() != w.stride() or dw.dtype != w.dtype:
                 dw = torch.empty_like(w).copy_(dw)
         return dx, dw, None
 

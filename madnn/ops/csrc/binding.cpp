@@ -68,6 +68,8 @@ int madnn_gemm_supported(int64_t, int64_t, int64_t, int64_t, int64_t);
 int madnn_conv3x3_supported(int, int, int, int);
 int madnn_conv3x3_stat_rows(int64_t);
 hipError_t madnn_conv3x3_fwd(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
+int64_t madnn_conv3x3_wgrad_ws(int, int, int, int, int);
+hipError_t madnn_conv3x3_wgrad(const void*, const void*, float*, void*, int, int, int, int, int, int, hipStream_t);
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
@@ -550,6 +552,28 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Te
   return {y, part};
 }
 
+// dW [Co, Ci, 3, 3] (channels_last) of y = conv3x3(x, w): dy [N, Co, H, W], x [N, Ci, H, W], both NHWC bf16
+at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, bool out_bf16) {
+  check_dev(x, "x");
+  check_dev(dy, "dy");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16, "conv3x3_wgrad: bf16 only");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_wgrad: NHWC 4-D tensors");
+  TORCH_CHECK(dy.size(0) == x.size(0) && dy.size(2) == x.size(2) && dy.size(3) == x.size(3), "conv3x3_wgrad: shapes");
+  const int N = (int)x.size(0), Ci = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Co = (int)dy.size(1);
+  const int64_t nws = madnn_conv3x3_wgrad_ws(N, H, W, Ci, Co);
+  TORCH_CHECK(nws > 0, "conv3x3_wgrad: unsupported shape Ci=", Ci, " Co=", Co, " H=", H, " W=", W);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor ws = at::empty({nws}, x.options().dtype(at::kFloat));
+  at::Tensor dw = at::empty({Co, Ci, 3, 3},
+                            x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  check(madnn_conv3x3_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), dw.data_ptr(), out_bf16 ? 1 : 0, N, H, W,
+                            Ci, Co, cur_stream(x)),
+        "conv3x3_wgrad");
+  return dw;
+}
+
 // ---- K10 ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, NHWC bf16 ---------
 void stem_check_x(const at::Tensor& x) {
   check_dev(x, "x");
@@ -820,6 +844,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
+  m.def("conv3x3_wgrad(Tensor dy, Tensor x, bool out_bf16) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
@@ -869,4 +894,5 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_fwd", linear_fwd);
   m.impl("linear_dgrad", linear_dgrad);
   m.impl("conv3x3_fwd", conv3x3_fwd);
+  m.impl("conv3x3_wgrad", conv3x3_wgrad);
 }

@@ -237,6 +237,163 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
   }
 }
 
+
+// ------------------------------------------------------------------ weight gradient
+// dW[co][tap][ci] = sum_m dY[m][co] X[pix(m) + off(tap)][ci]: one wave per tap (9 waves), each
+// a 64 (co) x 64 (ci) block = 2 x 2 accumulators, reducing over the pixels of a tile of R whole
+// output rows of one image.  Both the dY tile and the input halo (R + 2 rows) sit in LDS in a
+// zero-padded row layout of W + 2 slots per image row (pixel w at slot w + 1), so for every tap
+// the halo slot of reduction index k is k + dh (W + 2) + dw - 1: a uniform shift, and taps that
+// leave the image read the zero pad columns / zero rows.  Reduction index k runs over the padded
+// dY slots (pads hold zero dY, rounded up to 16), read with the transposing ds_read_b64_tr_b16
+// (k down the LDS rows, swz<64> images).  Workgroups split the tiles of a (co, ci) block; each
+// writes fp32 partials [split][Co][9][Ci]; wgrad_reduce sums them in split order (deterministic)
+// into the channels_last weight layout.  The next tile's loads are issued into registers before
+// this tile's MFMAs and written to LDS after them.
+constexpr int kWThreads = 576;  // 9 waves
+constexpr int kWMaxChunks = 8;  // per thread per tile: dY + halo 16-B chunks
+
+struct WArgs {
+  const uint16_t* x;   // [M][Ci]
+  const uint16_t* dy;  // [M][Co]
+  float* ws;           // [splits][Co][9][Ci]
+  int N, H, W, Ci, Co;
+  int R, kpad, xslots, tiles_per_img, ntiles;
+  int co_tiles, ci_tiles, splits;
+};
+
+__host__ __device__ inline int wgrad_rows(int H, int W) {
+  int R = 1;
+  for (int r = 1; r <= H; ++r)
+    if (H % r == 0 && r * (W + 2) <= 256) R = r;
+  return R;
+}
+
+__global__ __launch_bounds__(kWThreads) void conv3x3_wgrad_kernel(const WArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* sdy = smem;                       // [kpad][64]
+  uint16_t* sx = smem + (int64_t)p.kpad * 64;  // [xslots][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = tap
+  const int W = p.W, WP = p.W + 2;
+  const int pair = blockIdx.x % (p.co_tiles * p.ci_tiles), split = blockIdx.x / (p.co_tiles * p.ci_tiles);
+  const int co0 = (pair % p.co_tiles) * 64, ci0 = (pair / p.co_tiles) * 64;
+
+  // zero both images once: pad columns, pad rows and slack stay zero (tile writes touch real pixels only)
+  for (int i = tid; i < (p.kpad + p.xslots) * 8; i += kWThreads)
+    *reinterpret_cast<u32x4*>(smem + (int64_t)i * 8) = u32x4{0u, 0u, 0u, 0u};
+
+  // this thread's 16-B chunks of a tile (identical for every tile): LDS element offset, global
+  // element offset relative to the tile's first pixel row, halo row (-1: a dY chunk)
+  const int ndy = p.R * W * 8, nx = (p.R + 2) * W * 8;
+  // loc[u]: LDS element offset (< 2^18) | (halo row + 1) << 24 (0: a dY chunk); -1: no chunk
+  int loc[kWMaxChunks], gofs[kWMaxChunks];  // gofs < (R + 1) W Ci < 2^31
+#pragma unroll
+  for (int u = 0; u < kWMaxChunks; ++u) {
+    const int i = tid + kWThreads * u;
+    loc[u] = -1;
+    gofs[u] = 0;
+    if (i < ndy) {
+      const int ch = i & 7, px = i >> 3, rr = px / W, w = px - rr * W;
+      const int slot = rr * WP + w + 1;
+      loc[u] = slot * 64 + 8 * (ch ^ fswz(slot));
+      gofs[u] = (rr * W + w) * p.Co + co0 + 8 * ch;
+    } else if (i < ndy + nx) {
+      const int j = i - ndy, ch = j & 7, px = j >> 3, q = px / W, w = px - q * W;
+      const int slot = 1 + q * WP + w + 1;
+      loc[u] = (p.kpad * 64 + slot * 64 + 8 * (ch ^ fswz(slot))) | ((q + 1) << 24);
+      gofs[u] = ((q - 1) * W + w) * p.Ci + ci0 + 8 * ch;
+    }
+  }
+  u32x4 stg[kWMaxChunks];
+  auto load_tile = [&](int t) {
+    const int n = t / p.tiles_per_img, h0 = (t - n * p.tiles_per_img) * p.R;
+    const int64_t pix0 = ((int64_t)n * p.H + h0) * W;
+#pragma unroll
+    for (int u = 0; u < kWMaxChunks; ++u) {
+      stg[u] = u32x4{0u, 0u, 0u, 0u};
+      if (loc[u] >= 0) {
+        const int q1 = loc[u] >> 24;
+        if (q1 == 0) {
+          stg[u] = *reinterpret_cast<const u32x4*>(p.dy + pix0 * p.Co + gofs[u]);
+        } else {
+          const int hr = h0 + q1 - 2;
+          if (hr >= 0 && hr < p.H) stg[u] = *reinterpret_cast<const u32x4*>(p.x + pix0 * p.Ci + gofs[u]);
+        }
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int u = 0; u < kWMaxChunks; ++u)
+      if (loc[u] >= 0) *reinterpret_cast<u32x4*>(smem + (loc[u] & 0xffffff)) = stg[u];
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+  const int dh = wave / 3, dw = wave - 3 * (wave / 3);
+  const int shift = 1 + dh * WP + dw - 1;  // halo slot of reduction index k = k + shift
+  const int nk = p.kpad / 16;
+
+  int t = split;
+  __syncthreads();  // zero fill done
+  if (t < p.ntiles) {
+    load_tile(t);
+    store_tile();
+  }
+  __syncthreads();
+  for (; t < p.ntiles; t += p.splits) {
+    const int tn = t + p.splits;
+    if (tn < p.ntiles) load_tile(tn);
+    for (int ks = 0; ks < nk; ++ks) {
+      bf16x8 af[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) af[a] = lds_col<64>(sdy, 16 * ks, a * 32, lane);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bv[b] = lds_col<64>(sx, 16 * ks + shift, b * 32, lane);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma(af[a], bv[b], acc[a][b]);
+    }
+    __syncthreads();  // every wave is done reading this tile
+    if (tn < p.ntiles) store_tile();
+    __syncthreads();
+  }
+  // partial [split][co][tap][ci]: lane holds D[co = a*32 + acc_row(r, h)][ci = b*32 + (lane & 31)]
+  const int hh = lane >> 5, l32 = lane & 31;
+  float* out = p.ws + (int64_t)split * p.Co * 9 * p.Ci;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + a * 32 + acc_row(r, hh);
+        out[((int64_t)co * 9 + wave) * p.Ci + ci0 + b * 32 + l32] = acc[a][b][r];
+      }
+}
+
+// out[e] = sum_s ws[s][e] (fixed order), fp32 or bf16
+__global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                                   int64_t n, void* __restrict__ out, int bf16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < splits; ++s) acc += *reinterpret_cast<const f32x4*>(ws + (int64_t)s * n + i);
+    if (bf16) {
+      const unsigned lo = (unsigned)f32_to_bf16(acc[0]) | ((unsigned)f32_to_bf16(acc[1]) << 16);
+      const unsigned hi = (unsigned)f32_to_bf16(acc[2]) | ((unsigned)f32_to_bf16(acc[3]) << 16);
+      *reinterpret_cast<u32x2*>(static_cast<uint16_t*>(out) + i) = u32x2{lo, hi};
+    } else {
+      *reinterpret_cast<f32x4*>(static_cast<float*>(out) + i) = acc;
+    }
+  }
+}
+
 }  // namespace conv3
 }  // namespace madnn
 
@@ -279,6 +436,58 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
   } else {
     hipLaunchKernelGGL(conv3x3_kernel<false>, dim3((unsigned)grid), dim3(kThreads), lds, s, p);
   }
+  return hipGetLastError();
+}
+
+
+// weight-gradient plan: workspace floats needed (0 if unsupported)
+static bool wgrad_plan(int N, int H, int W, int Ci, int Co, WArgs& p) {
+  if (Ci % 64 || Co % 64 || Ci < 64 || Co < 64 || Ci > 8192 || Co > 8192 || N < 1 || H < 1 || W < 1) return false;
+  p.N = N;
+  p.H = H;
+  p.W = W;
+  p.Ci = Ci;
+  p.Co = Co;
+  p.R = wgrad_rows(H, W);
+  const int kreal = p.R * (W + 2);
+  if (kreal > 256) return false;
+  p.kpad = (kreal + 15) / 16 * 16;
+  p.xslots = p.kpad + 2 * (W + 2) + 2;
+  if ((p.R * W * 8 + (p.R + 2) * W * 8 + kWThreads - 1) / kWThreads > kWMaxChunks) return false;
+  if ((size_t)(p.kpad + p.xslots) * 128 > 160 * 1024) return false;
+  p.tiles_per_img = H / p.R;
+  p.ntiles = N * p.tiles_per_img;
+  p.co_tiles = Co / 64;
+  p.ci_tiles = Ci / 64;
+  const int pairs = p.co_tiles * p.ci_tiles;
+  int splits = (2 * 256 + pairs - 1) / pairs;  // ~2 workgroups per CU over the whole grid
+  splits = splits > p.ntiles ? p.ntiles : splits;
+  p.splits = splits < 1 ? 1 : splits;
+  return true;
+}
+
+int64_t madnn_conv3x3_wgrad_ws(int N, int H, int W, int Ci, int Co) {
+  WArgs p{};
+  if (!wgrad_plan(N, H, W, Ci, Co, p)) return -1;
+  return (int64_t)p.splits * Co * 9 * Ci;
+}
+
+// dw [Co][3][3][Ci] (channels_last weight layout), fp32 (out_bf16 = 0) or bf16; ws: madnn_conv3x3_wgrad_ws floats
+hipError_t madnn_conv3x3_wgrad(const void* dy, const void* x, float* ws, void* dw, int out_bf16, int N, int H, int W,
+                               int Ci, int Co, hipStream_t s) {
+  WArgs p{};
+  if (!wgrad_plan(N, H, W, Ci, Co, p)) return hipErrorInvalidValue;
+  p.x = static_cast<const uint16_t*>(x);
+  p.dy = static_cast<const uint16_t*>(dy);
+  p.ws = ws;
+  const size_t lds = (size_t)(p.kpad + p.xslots) * 128;
+  const int grid = p.co_tiles * p.ci_tiles * p.splits;
+  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(grid), dim3(kWThreads), lds, s, p);
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)Co * 9 * Ci;
+  int rg = (int)((n / 4 + 255) / 256);
+  rg = rg > 1024 ? 1024 : rg;
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(rg), dim3(256), 0, s, ws, p.splits, n, dw, out_bf16);
   return hipGetLastError();
 }
 

@@ -88,3 +88,35 @@ def test_resnet_block_uses_k13():
     y = blk(x.bfloat16())
     yr = ref(x)
     torch.testing.assert_close(y.float(), yr, atol=0.1, rtol=0.05)
+
+
+@pytest.mark.parametrize("N,Ci,Co,H,W", [(2, 64, 64, 56, 56), (3, 128, 128, 28, 28), (4, 256, 64, 14, 14),
+                                          (5, 64, 128, 7, 7), (2, 64, 64, 5, 9)])
+def test_conv3x3_wgrad(N, Ci, Co, H, W):
+    _ops()
+    g = torch.Generator(device="cuda").manual_seed(N + Ci * 3 + W)
+    x = _cl(torch.randn(N, Ci, H, W, device="cuda", generator=g).bfloat16())
+    dy = _cl(torch.randn(N, Co, H, W, device="cuda", generator=g).bfloat16())
+    dw = torch.ops.madnn.conv3x3_wgrad(dy, x, False)
+    assert dw.shape == (Co, Ci, 3, 3) and dw.dtype == torch.float32
+    assert dw.is_contiguous(memory_format=torch.channels_last)
+    xr = x.float().requires_grad_(True)
+    wr = torch.zeros(Co, Ci, 3, 3, device="cuda", requires_grad=True)
+    F.conv2d(xr, wr, None, 1, 1).backward(dy.float())
+    torch.testing.assert_close(dw, wr.grad, atol=2e-3 * (N * H * W) ** 0.5, rtol=1e-3)
+    dwb = torch.ops.madnn.conv3x3_wgrad(dy, x, True)
+    assert dwb.dtype == torch.bfloat16
+    torch.testing.assert_close(dwb.float(), dw, atol=1e-2 * float(dw.abs().max()), rtol=1e-2)
+
+
+def test_conv3x3_wgrad_exact_small_integers():
+    _ops()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    N, Ci, Co, H, W = 2, 64, 128, 6, 10
+    x = _cl(torch.randint(-2, 3, (N, Ci, H, W), device="cuda", generator=g).bfloat16())
+    dy = _cl(torch.randint(-2, 3, (N, Co, H, W), device="cuda", generator=g).bfloat16())
+    dw = torch.ops.madnn.conv3x3_wgrad(dy, x, False)
+    xr = x.float().requires_grad_(True)
+    wr = torch.zeros(Co, Ci, 3, 3, device="cuda", requires_grad=True)
+    F.conv2d(xr, wr, None, 1, 1).backward(dy.float())
+    assert torch.equal(dw, wr.grad)
