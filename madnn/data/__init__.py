@@ -43,7 +43,7 @@ def shard(data, rank: Optional[int] = None, world: Optional[int] = None, remaind
     n = len(data)
     if strided:
         stripe = n // world
-        idx = torch.arange(rank, stripe * world, world)
+        idx = torch.arange(stripe) * world + rank  # empty when n < world (arange(rank, 0, W) would raise)
         out = data[idx] if isinstance(data, torch.Tensor) else [data[i] for i in idx.tolist()]
         if verbose:
             get_logger().info("rank %d: strided shard stripe=%d", rank, stripe)
