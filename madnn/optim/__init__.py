@@ -53,20 +53,35 @@ class _FlatOptimizer(torch.optim.Optimizer):
     def migrate(self, old: dict):
         """Follow a ``FlatParamSpace.relayout``: move every parameter's optimizer state from its
         old bucket slot (``old[id(p)] = (bucket, offset)``) to its new one."""
-        old_state, old_steps = self.flat_state, self.bucket_steps
-        self.flat_state, self.bucket_steps = {}, {}
+        self.migrate_begin()
         for bk in self.space.buckets:
-            st = {n: torch.zeros_like(bk.master) for n in self._state_names if
-                  any(n in v for v in old_state.values())}
-            steps = 0
-            for p, off in zip(bk.params, bk.offsets):
-                obk, ooff = old[id(p)]
-                steps = max(steps, old_steps.get(obk.index, 0))
-                for n, t in st.items():
-                    if n in old_state.get(obk.index, {}):
-                        t[off:off + p.numel()].copy_(old_state[obk.index][n][ooff:ooff + p.numel()])
-            self.flat_state[bk.index] = st
-            self.bucket_steps[bk.index] = steps
+            self.migrate_bucket(bk, old)
+        self.migrate_end()
+
+    # streaming form, driven by FlatParamSpace.relayout(on_bucket=..., on_release=...)
+    def migrate_begin(self):
+        self._old_state, self._old_steps = self.flat_state, self.bucket_steps
+        self._old_names = {n for v in self._old_state.values() for n in v}
+        self.flat_state, self.bucket_steps = {}, {}
+
+    @torch.no_grad()
+    def migrate_bucket(self, bk, old: dict):
+        st = {n: torch.zeros_like(bk.master) for n in self._state_names if n in self._old_names}
+        steps = 0
+        for p, off in zip(bk.params, bk.offsets):
+            obk, ooff = old[id(p)]
+            steps = max(steps, self._old_steps.get(obk.index, 0))
+            for n, t in st.items():
+                if n in self._old_state.get(obk.index, {}):
+                    t[off:off + p.numel()].copy_(self._old_state[obk.index][n][ooff:ooff + p.numel()])
+        self.flat_state[bk.index] = st
+        self.bucket_steps[bk.index] = steps
+
+    def migrate_release(self, obk):
+        self._old_state.pop(obk.index, None)
+
+    def migrate_end(self):
+        del self._old_state, self._old_steps, self._old_names
 
     def _bind_local(self):
         groups = [g["params"] for g in self.param_groups]

@@ -307,9 +307,13 @@ class DataParallel(nn.Module):
             return
         if self.optimizer is None and self.unpack_grads is False:
             return  # a flat state we cannot migrate
-        old = self.space.relayout(seen)
-        if self.optimizer is not None:
-            self.optimizer.migrate(old)
+        opt = self.optimizer
+        if opt is not None:
+            opt.migrate_begin()
+            self.space.relayout(seen, on_bucket=opt.migrate_bucket, on_release=opt.migrate_release)
+            opt.migrate_end()
+        else:
+            self.space.relayout(seen)
         for h in self._hooks:
             h.remove()
         self._hooks.clear()

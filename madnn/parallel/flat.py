@@ -110,11 +110,18 @@ class FlatParamSpace:
         return len(runs) == len(set(runs))
 
     @torch.no_grad()
-    def relayout(self, observed: Sequence[int]):
+    def relayout(self, observed: Sequence[int], on_bucket=None, on_release=None):
         """Re-lay the buckets in the OBSERVED gradient-ready order: values move
         exactly (fp32 masters copied, compute copies re-derived), parameters are re-pointed at
-        the new buffers.  Returns ``{id(p): (old bucket, old offset)}`` for state migration."""
+        the new buffers.  Returns ``{id(p): (old bucket, old offset)}`` for state migration.
+
+        Streaming: ``on_bucket(new_bucket, old)`` runs right after each new bucket is built (the
+        optimizer moves that bucket's state then), and an old bucket's buffers are dropped --
+        ``on_release(old_bucket)`` lets the optimizer drop its state -- as soon as every one of
+        its parameters has moved.  The transient is a few buckets, not a second copy of every
+        master / moment buffer (Llama-3 8B on one GPU: +96 GB without streaming)."""
         old = {id(p): (bk, off) for bk in self.buckets for p, off in zip(bk.params, bk.offsets)}
+        left = {bk.index: len(bk.params) for bk in self.buckets}
         old_info = dict(self.param_info)
         sinks = self._sinks_on
         if sinks:
@@ -135,6 +142,15 @@ class FlatParamSpace:
                 self.param_info[id(p)] = (bk, off, cl)
                 p.data = _phys_view(model[off:off + n], p.shape, cl)
             bk.master, bk.model = master, model
+            if on_bucket is not None:
+                on_bucket(bk, old)
+            for p in bk.params:
+                obk = old[id(p)][0]
+                left[obk.index] -= 1
+                if left[obk.index] == 0:  # every parameter of obk has moved: free its buffers now
+                    if on_release is not None:
+                        on_release(obk)
+                    obk.master = obk.model = obk.grad = None
         if sinks:
             self.enable_grad_sinks()
         return old
