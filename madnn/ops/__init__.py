@@ -562,10 +562,16 @@ _K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A
 _K13_WGRAD = os.environ.get("MADNN_CONV3X3_WGRAD", "auto")
 
 
+_K13_CH = 64 if os.environ.get("MADNN_K13_CH", "32") == "64" else 32  # input channels per LDS stage (A/B knob)
+
+
 def _k13_halo_ok(W: int) -> bool:
-    # conv3.hip: halo_capacity(W) * 128 + 128 + 16 KiB of weights <= 80 KiB (two workgroups per CU)
-    cap = ((255 // W) * W + 4 * W + 7) // 8 * 8
-    return cap * 128 + 128 + 2 * 64 * 64 * 2 <= 80 * 1024
+    # conv3.hip conv3x3_lds: halo pixels (rounded to whole 1-KiB DMA pieces) x 2*CH bytes + zero row +
+    # two weight slots, at least the 32 KiB epilogue tile, must leave two workgroups per CU
+    rb = 2 * _K13_CH
+    rpi = 1024 // rb
+    cap = ((255 // W) * W + 4 * W + rpi - 1) // rpi * rpi
+    return max(cap * rb + rb + 2 * 64 * rb, 32 * 1024) <= 80 * 1024
 
 
 def conv3x3_supported(x: torch.Tensor, w: torch.Tensor) -> bool:

@@ -19,11 +19,17 @@
 // (cdna_hip_programming.md rule 21), and read conflict-free with ds_read_b128.
 // A tap whose source pixel leaves the image (top/bottom rows, first/last column, image seams in
 // the flattened NHWC order) reads a zero row in LDS instead: no data-dependent branches.
-// LDS: halo (<= (255/W + 4) * W pixels x 128 B, 57 KiB at W = 56) + zero row + 16 KiB weights:
-// two workgroups per CU, so one workgroup's halo load overlaps the other's MFMAs.
+// Stages are 32 input channels (64-B pixel rows; `MADNN_K13_CH=64` selects 128-B rows): LDS =
+// halo (<= (255/W + 4) * W pixels x 64 B, 28 KiB at W = 56) + zero row + 8 KiB of weights, so four
+// workgroups share a CU and one workgroup's halo / weight loads and epilogue stores overlap the
+// others' MFMAs (measured: a kernel with the MFMAs removed still took 70 % of the time at two
+// workgroups per CU, and a persistent double-buffered variant at one workgroup per CU was 1.7x
+// slower -- occupancy, not explicit double buffering, hides this kernel's memory latency).
 // Epilogue: the K9 LDS-transposed row store (16-B stores of 64 contiguous channels per pixel)
 // and, with `stats`, per-channel sum / sum of squares of the bf16-rounded outputs as one
 // [2][Cout] partial row per pixel tile (the input of bn.hip's finalize).
+#include <cstdlib>
+
 #include "mfma.h"
 
 namespace madnn {
@@ -49,18 +55,37 @@ struct Args {
   int m_tiles, co_tiles;
 };
 
-// halo pixels a tile can touch, rounded up to whole 8-pixel DMA instructions (so the last
-// instruction never writes past the halo into the zero row)
-__host__ __device__ inline int halo_capacity(int W) { return ((kBJ - 1) / W * W + 4 * W + 7) / 8 * 8; }
-
 __device__ __forceinline__ int fswz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
 
-template <bool STATS>
-__global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
+// chunk geometry: CH input channels per stage, pixel rows of RB = 2 CH bytes (NC 16-B chunks),
+// swizzle f(row) (128-B rows: fswz; 64-B rows: (row >> 2) & 3 -- both conflict-free for the 16
+// consecutive rows of a ds_read_b128 lane group at any row alignment, i.e. for every tap shift)
+template <int CH>
+struct Chunk {
+  static constexpr int RB = 2 * CH, NC = CH / 8, RPI = 1024 / RB, KS = CH / 16, WE = 64 * CH;
+  static __device__ __forceinline__ int f(int row) {
+    if constexpr (CH == 64) return fswz(row);
+    else return (row >> 2) & 3;
+  }
+  static __device__ __forceinline__ int off(int row, int ch) { return row * RB + 16 * (ch ^ f(row)); }
+};
+
+__host__ __device__ inline int halo_rows_px(int W, int rpi) {  // halo capacity in pixels
+  return ((kBJ - 1) / W * W + 4 * W + rpi - 1) / rpi * rpi;
+}
+
+__host__ inline size_t conv3x3_lds(int W, int CH) {
+  const size_t rb = 2 * CH, cap = (size_t)halo_rows_px(W, 1024 / (int)rb) * rb + rb + 2 * 64 * rb;
+  return cap > 32 * 1024 ? cap : 32 * 1024;  // the epilogue's [256][64] bf16 tile reuses the whole image
+}
+
+template <int CH, bool STATS>
+__global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(const Args p) {
+  using C = Chunk<CH>;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* halo = smem;                               // [halo_px][64]
-  uint16_t* zrow = smem + (int64_t)p.halo_px * 64;     // [1][64] zeros
-  uint16_t* wring = zrow + 64;                         // [2][64][64]
+  uint16_t* halo = smem;                                     // [halo_px][CH]
+  uint16_t* zrow = smem + (int64_t)p.halo_px * CH;           // [1][CH] zeros
+  uint16_t* wring = zrow + CH;                               // [2][64][CH]
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -92,33 +117,32 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
     hb[jb] = (int)(r - hrow0) * W + wc;
     edge[jb] = (h >= 1 ? 1u : 0u) | (h <= H - 2 ? 2u : 0u) | (wc >= 1 ? 4u : 0u) | (wc <= W - 2 ? 8u : 0u);
   }
-  if (tid < 8) *reinterpret_cast<u32x4*>(zrow + tid * 8) = u32x4{0u, 0u, 0u, 0u};
+  if (tid < C::NC) *reinterpret_cast<u32x4*>(zrow + tid * 8) = u32x4{0u, 0u, 0u, 0u};
 
-  const int nchunk = p.Ci / 64;
+  const int nchunk = p.Ci / CH;
   const int total = nchunk * 9;
   const int64_t ldw = 9LL * p.Ci;
 
-  // LDS-DMA of the halo of input chunk c: 8 pixel rows (1 KiB) per wave-instruction
+  // LDS-DMA of the halo of input chunk c: RPI pixel rows (1 KiB) per wave-instruction
   auto stage_halo = [&](int c) {
-    const int ninst = (hpx + 7) / 8;
+    const int ninst = (hpx + C::RPI - 1) / C::RPI;
     for (int i = wave; i < ninst; i += 4) {
-      const int prow = i * 8 + (lane >> 3);
-      const int ch = (lane & 7) ^ fswz(prow);
+      const int prow = i * C::RPI + lane / C::NC;
+      const int ch = (lane % C::NC) ^ C::f(prow);
       int64_t src = hrow0 * W + prow;
       src = src < 0 ? 0 : (src >= p.M ? p.M - 1 : src);
-      __builtin_amdgcn_global_load_lds((const void*)(p.x + src * p.Ci + c * 64 + 8 * ch),
+      __builtin_amdgcn_global_load_lds((const void*)(p.x + src * p.Ci + c * CH + 8 * ch),
                                        (lds_void*)(halo + i * 512), 16, 0, 0);
     }
   };
-  // weights of step idx = (chunk idx / 9, tap idx % 9) into ring slot idx & 1: 2 instructions per wave
+  // weights of (chunk c, tap t) into ring slot `slot`: 64 rows of RB bytes, 64 * RB / 1 KiB instructions
   auto stage_w = [&](int c, int t, int slot) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int inst = wave * 2 + e;
-      const int row = inst * 8 + (lane >> 3);
-      const int ch = (lane & 7) ^ fswz(row);
-      __builtin_amdgcn_global_load_lds((const void*)(p.w + (int64_t)(co0 + row) * ldw + t * p.Ci + c * 64 + 8 * ch),
-                                       (lds_void*)(wring + slot * kWElems + inst * 512), 16, 0, 0);
+    constexpr int NI = 64 * C::RB / 1024;
+    for (int inst = wave; inst < NI; inst += 4) {
+      const int row = inst * C::RPI + lane / C::NC;
+      const int ch = (lane % C::NC) ^ C::f(row);
+      __builtin_amdgcn_global_load_lds((const void*)(p.w + (int64_t)(co0 + row) * ldw + t * p.Ci + c * CH + 8 * ch),
+                                       (lds_void*)(wring + slot * C::WE + inst * 512), 16, 0, 0);
     }
   };
 
@@ -144,7 +168,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
       ++cn;
     }
     if (idx + 1 < total) stage_w(cn, tn, (idx + 1) & 1);
-    const uint16_t* wt = wring + (idx & 1) * kWElems;
+    const char* wt = reinterpret_cast<const char*>(wring + (idx & 1) * C::WE);
     // this tap's B-fragment row addresses (halo pixel or the zero row)
     const int dh = t / 3, dw = t - 3 * (t / 3);
     const unsigned need = (dh == 0 ? 1u : dh == 2 ? 2u : 0u) | (dw == 0 ? 4u : dw == 2 ? 8u : 0u);
@@ -154,14 +178,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
     for (int jb = 0; jb < 2; ++jb) {
       const int hp = hb[jb] + (dh - 1) * W + (dw - 1);
       const bool ok = (edge[jb] & need) == need;
-      brow[jb] = ok ? hbase + hp * 128 : zbase;
-      bsw[jb] = ok ? fswz(hp) : 0;
+      brow[jb] = ok ? hbase + hp * C::RB : zbase;
+      bsw[jb] = ok ? C::f(hp) : 0;
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < C::KS; ++s) {
       bf16x8 af[2], bv[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) af[a] = lds_row(wt, a * 32 + l32, 2 * s + hh);
+      for (int a = 0; a < 2; ++a) af[a] = *reinterpret_cast<const bf16x8*>(wt + C::off(a * 32 + l32, 2 * s + hh));
 #pragma unroll
       for (int b = 0; b < 2; ++b) bv[b] = *reinterpret_cast<const bf16x8*>(brow[b] + 16 * ((2 * s + hh) ^ bsw[b]));
 #pragma unroll
@@ -181,7 +205,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
   }
 
   // ---- epilogue: D[co][px] -> bf16 tile [256 px][64 co] in LDS (128-B rows) -> 16-B row stores
-  char* ot = reinterpret_cast<char*>(smem);  // the halo region (>= 256 x 128 B) is free now
+  char* ot = reinterpret_cast<char*>(smem);  // the whole image (>= 32 KiB) is free now
   auto out_off = [](int r, int ch) { return r * 128 + 16 * (ch ^ ((r >> 1) & 7)); };
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
@@ -220,13 +244,12 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
   }
   if constexpr (STATS) {
     __syncthreads();  // the tile image is consumed
-    float* red = reinterpret_cast<float*>(smem);  // [32 row groups][2][64]
+    float* red = reinterpret_cast<float*>(smem);  // [32 row groups][2][64], 16-B vector writes
     const int rg = tid >> 3;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(rg * 2) * 64 + 8 * ch + e] = ssum[e];
-      red[(rg * 2 + 1) * 64 + 8 * ch + e] = ssq[e];
-    }
+    *reinterpret_cast<f32x4*>(red + (rg * 2) * 64 + 8 * ch) = f32x4{ssum[0], ssum[1], ssum[2], ssum[3]};
+    *reinterpret_cast<f32x4*>(red + (rg * 2) * 64 + 8 * ch + 4) = f32x4{ssum[4], ssum[5], ssum[6], ssum[7]};
+    *reinterpret_cast<f32x4*>(red + (rg * 2 + 1) * 64 + 8 * ch) = f32x4{ssq[0], ssq[1], ssq[2], ssq[3]};
+    *reinterpret_cast<f32x4*>(red + (rg * 2 + 1) * 64 + 8 * ch + 4) = f32x4{ssq[4], ssq[5], ssq[6], ssq[7]};
     __syncthreads();
     if (tid < 128) {
       const int which = tid >> 6, ci = tid & 63;
@@ -236,7 +259,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv3x3_kernel(const Args p) {
     }
   }
 }
-
 
 // ------------------------------------------------------------------ weight gradient
 // dW[co][tap][ci] = sum_m dY[m][co] X[pix(m) + off(tap)][ci]: one wave per tap (9 waves), each
@@ -401,10 +423,15 @@ using namespace madnn::conv3;
 
 extern "C" {
 
+// chunk width: 32 channels (LDS ~37 KiB at W = 56: four workgroups per CU) unless MADNN_K13_CH=64
+static int k13_ch(int Ci) {
+  static const int want = getenv("MADNN_K13_CH") ? atoi(getenv("MADNN_K13_CH")) : 32;
+  return (want == 64 && Ci % 64 == 0) ? 64 : 32;
+}
+
 int madnn_conv3x3_supported(int H, int W, int Ci, int Co) {
   if (H < 1 || W < 1 || Ci % 64 || Co % 64 || Ci < 64 || Co < 64 || Ci > 8192) return 0;
-  const size_t lds = (size_t)halo_capacity(W) * 128 + 128 + 2 * kWElems * 2;
-  return lds <= 80 * 1024 ? 1 : 0;  // two workgroups per CU
+  return conv3x3_lds(W, k13_ch(Ci)) <= 80 * 1024 ? 1 : 0;  // at least two workgroups per CU
 }
 
 int madnn_conv3x3_stat_rows(int64_t M) { return (int)((M + kBJ - 1) / kBJ); }
@@ -425,20 +452,23 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
   p.W = W;
   p.Ci = Ci;
   p.Co = Co;
-  p.halo_px = halo_capacity(W);
+  const int CH = k13_ch(Ci);
+  p.halo_px = halo_rows_px(W, 1024 / (2 * CH));
   p.m_tiles = (int)((p.M + kBJ - 1) / kBJ);
   p.co_tiles = Co / kBI;
   const int64_t grid = (int64_t)p.m_tiles * p.co_tiles;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  const size_t lds = (size_t)p.halo_px * 128 + 128 + 2 * kWElems * 2;
-  if (stats) {
-    hipLaunchKernelGGL(conv3x3_kernel<true>, dim3((unsigned)grid), dim3(kThreads), lds, s, p);
+  const size_t lds = conv3x3_lds(W, CH);
+  const dim3 g((unsigned)grid), b(kThreads);
+  if (CH == 32) {
+    if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true>), g, b, lds, s, p);
+    else hipLaunchKernelGGL((conv3x3_kernel<32, false>), g, b, lds, s, p);
   } else {
-    hipLaunchKernelGGL(conv3x3_kernel<false>, dim3((unsigned)grid), dim3(kThreads), lds, s, p);
+    if (stats) hipLaunchKernelGGL((conv3x3_kernel<64, true>), g, b, lds, s, p);
+    else hipLaunchKernelGGL((conv3x3_kernel<64, false>), g, b, lds, s, p);
   }
   return hipGetLastError();
 }
-
 
 // weight-gradient plan: workspace floats needed (0 if unsupported)
 static bool wgrad_plan(int N, int H, int W, int Ci, int Co, WArgs& p) {

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Persistent K13 forward: correctness tests, then A/B against the one-tile-per-workgroup kernel.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_conv3x3_gpu.py tests/test_fuzz_gpu.py -x -q --timeout 120 \
+   --timeout-method thread -k "conv3x3 or k13" > $OUT/k13p_tests.log 2>&1; rc=$?; tail -n 15 $OUT/k13p_tests.log; [ $rc -ne 0 ] && exit $rc
+for v in 0 1; do MADNN_K13_PERSISTENT=$v timeout -k 10 200 python bench/conv3x3_ab.py --rounds 3 > $OUT/k13p$v.log 2>&1 || exit 3
+  echo "persistent=$v"; grep '"C"' $OUT/k13p$v.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    r=json.loads(l); print(r['C'], 'fwd', r['fwd_k13_us'], 'dgrad', r['dgrad_k13_us'], 'miopen', r['fwd_miopen_us'], r['dgrad_miopen_us'])"; done
