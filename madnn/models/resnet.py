@@ -26,9 +26,12 @@ from torch import nn
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
+from ..ops import batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_supported
 
 # A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
 _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
+# A/B knob: the downsample path's BatchNorm runs inside bn3's kernels (1) or as its own passes (0)
+_DUAL_BN = os.environ.get("MADNN_DUAL_BN", "1") != "0"
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -80,15 +83,36 @@ class Bottleneck(nn.Module):
         elif _FORK_DS:
             # the downsample path's input gradient is likewise summed inside conv1's data grad
             y, st, xf = self.conv1(x, stats=True, fork=True)
+            if self._dual_bn():
+                # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's
+                # passes (forward and backward), its normalised output never written to HBM
+                yd, std = self.downsample[0](xf, stats=True)
+                out = self.bn1(y, relu=True, stats=st)
+                y, st = self.conv2(out, stats=True)
+                y, st = self._bn2_conv3(y, st)
+                return batch_norm_add_bn_relu(y, yd, self.bn3, self.downsample[1], st, std)
             idt = self.downsample(xf)
         else:
             idt = self.downsample(x)
             y, st = self.conv1(x, stats=True)
         out = self.bn1(y, relu=True, stats=st)
         y, st = self.conv2(out, stats=True)   # K13 at stride 1: BN statistics from the epilogue
-        out = self.bn2(y, relu=True, stats=st)
-        y, st = self.conv3(out, stats=True)
+        y, st = self._bn2_conv3(y, st)
         return self.bn3(y, residual=idt, relu=True, stats=st)   # relu(bn3 + idt): one kernel
+
+    def _bn2_conv3(self, y, st):
+        """conv3(relu(bn2(y))): on K9 the bn2 apply + ReLU run in conv3's operand prologue
+        (forward and weight grad), so relu(bn2(y)) is never written to HBM."""
+        if isinstance(self.bn2, BN) and isinstance(self.conv3, FusedConv2d) and self.conv3._k9(y) \
+                and bn_relu_conv1x1_supported(y, self.bn2, self.conv3.weight):
+            return bn_relu_conv1x1(y, self.bn2, self.conv3.weight, stats_in=st, stats=True)
+        out = self.bn2(y, relu=True, stats=st)
+        return self.conv3(out, stats=True)
+
+    def _dual_bn(self) -> bool:
+        ds = self.downsample
+        return (_DUAL_BN and isinstance(ds, nn.Sequential) and len(ds) == 2
+                and isinstance(ds[0], FusedConv2d) and isinstance(ds[1], BN) and isinstance(self.bn3, BN))
 
 
 class ResNet(nn.Module):

@@ -280,6 +280,54 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, num_batches_track
                                     training=training, momentum=momentum, eps=eps, relu=relu, residual=residual)
 
 
+class _BNDualFn(torch.autograd.Function):
+    """relu(BN(x) + BN_r(r)), training.  The residual BatchNorm's output is never materialised:
+    one apply pass forward, one reduction + one apply pass backward serve both BNs."""
+
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, weight_r, bias_r, bn, bn_r, stats, stats_r):
+        out = torch.ops.madnn.bn_fwd_dual(x, r, weight, bias, bn.running_mean, bn.running_var,
+                                          bn.num_batches_tracked, float(bn.momentum), float(bn.eps), stats,
+                                          weight_r, bias_r, bn_r.running_mean, bn_r.running_var,
+                                          bn_r.num_batches_tracked, float(bn_r.momentum), float(bn_r.eps), stats_r)
+        y, mask, mean, invstd, _, _, mean_r, invstd_r, _, _ = out
+        ctx.save_for_backward(x, r, mask, weight, mean, invstd, weight_r, mean_r, invstd_r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, r, mask, weight, mean, invstd, weight_r, mean_r, invstd_r = ctx.saved_tensors
+        dx, dr, dw, db, dw_r, db_r = torch.ops.madnn.bn_bwd_dual(dy, x, r, mask, weight, mean, invstd,
+                                                                 weight_r, mean_r, invstd_r)
+        return dx, dr, dw, db, dw_r, db_r, None, None, None, None
+
+
+def batch_norm_dual_supported(x: torch.Tensor, r: torch.Tensor, bn, bn_r) -> bool:
+    """Shapes/modes :func:`batch_norm_add_bn_relu` runs as one fused kernel pair."""
+    def ok(m):
+        return (m.training and m.track_running_stats and m.affine and m.momentum is not None
+                and m.weight.dtype == torch.float32)
+    return (x.dtype == torch.bfloat16 and bn_supported(x, bn.weight) and r.shape == x.shape
+            and r.dtype == x.dtype and r.stride() == x.stride() and ok(bn) and ok(bn_r))
+
+
+def batch_norm_add_bn_relu(x, r, bn, bn_r, stats=None, stats_r=None):
+    """``relu(bn(x) + bn_r(r))`` for two training-mode BatchNorm modules (ResNet's bn3 plus the
+    downsample path's BN): both BNs' statistics, running-stat updates and gradients, with the
+    residual BN applied inside bn's passes instead of in passes of its own (K5 ``RAFF`` variants).
+    Falls back to the two-module composition when the fused path does not apply."""
+    if batch_norm_dual_supported(x, r, bn, bn_r):
+        _need_native("batch_norm_add_bn_relu")
+        return _BNDualFn.apply(x, r, bn.weight, bn.bias, bn_r.weight, bn_r.bias, bn, bn_r, stats, stats_r)
+    idt = bn_r(r, stats=stats_r) if _is_fused_bn(bn_r) else bn_r(r)
+    return bn(x, residual=idt, relu=True, stats=stats) if _is_fused_bn(bn) else torch.relu(bn(x) + idt)
+
+
+def _is_fused_bn(m) -> bool:
+    from ..nn.norm import FusedBatchNorm2d
+    return isinstance(m, FusedBatchNorm2d)
+
+
 # ---------------------------------------------------------------------- K7
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
@@ -553,6 +601,65 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
     return ret[0] if len(ret) == 1 else tuple(ret)
 
 
+class _BNReluConv1x1Fn(torch.autograd.Function):
+    """``conv1x1(relu(bn(y)), w)`` in training with the BatchNorm apply + ReLU inside K9's operand
+    prologue (forward and weight grad): ``relu(bn(y))`` never exists in HBM.  Backward: the data
+    grad (K9 / hipBLASLt per :func:`conv1x1_route`) gives d relu(bn(y)), then one K5 backward
+    (ReLU mask recomputed from y) gives dy and the BN parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, y, w, bn_w, bn_b, bn, stats_in, want_stats):
+        mean, invstd, scale, shift = torch.ops.madnn.bn_coef(y, bn_w, bn_b, bn.running_mean, bn.running_var,
+                                                             bn.num_batches_tracked, float(bn.momentum),
+                                                             float(bn.eps), stats_in)
+        out, part = torch.ops.madnn.conv1x1_fwd(y, w, bool(want_stats), scale, shift)
+        ctx.save_for_backward(y, w, bn_w, mean, invstd, scale, shift)
+        ctx.dgrad = conv1x1_route(y.size(1), w.size(0))[1]
+        ctx.mark_non_differentiable(part)
+        return out, part
+
+    @staticmethod
+    def backward(ctx, dout, _dpart):
+        y, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        dout = _nhwc(dout.to(y.dtype))
+        if ctx.dgrad == "k9":
+            da = torch.ops.madnn.conv1x1_dgrad(dout, w, None)
+        else:
+            da = torch.empty_like(y)
+            torch.mm(_rows(dout), w.reshape(w.size(0), -1), out=_rows(da))
+        dw = torch.ops.madnn.conv1x1_wgrad(dout, y, scale, shift).to(w.dtype).view(w.shape)
+        need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dy, dbw, dbb, _ = torch.ops.madnn.bn_bwd(da, y, None, False, bn_w, mean, invstd, scale, shift, True, need_bn)
+        return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
+
+
+def bn_relu_conv1x1_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
+    """Whether :func:`bn_relu_conv1x1` runs fused: training-mode BN with running statistics and an
+    fp32 affine, bf16 NHWC input, K9-shaped weight."""
+    return (_BN_PROLOGUE and bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None
+            and bn.weight.dtype == torch.float32 and conv1x1_supported(y, w) and bn_supported(y, bn.weight))
+
+
+def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[torch.Tensor] = None,
+                    stats: bool = False):
+    """``conv1x1(relu(bn(y)), w)``: the BatchNorm's apply pass is fused into the convolution's
+    operand load (ResNet's bn2 -> conv3).  ``stats_in``: ``y``'s partial statistics from its
+    producer; ``stats``: also return the output's partial statistics (None if not computed)."""
+    if bn_relu_conv1x1_supported(y, bn, w):
+        _need_native("bn_relu_conv1x1")
+        out, part = _BNReluConv1x1Fn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
+        return (out, part if part.numel() else None) if stats else out
+    a = bn(y, relu=True, stats=stats_in) if _is_fused_bn(bn) else torch.relu(bn(y))
+    if conv1x1_supported(a, w):
+        return conv1x1(a, w, stats=stats)
+    out = torch.nn.functional.conv2d(a, w.view(w.size(0), -1, 1, 1)) if a.dim() == 4 else torch.mm(
+        a, w.reshape(w.size(0), -1).t())
+    return (out, None) if stats else out
+
+
+_BN_PROLOGUE = os.environ.get("MADNN_BN_PROLOGUE", "1") != "0"
+
+
 # ---------------------------------------------------------------------- K13
 _K13 = os.environ.get("MADNN_CONV3X3", "1") != "0"
 _K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A/B runs)
@@ -702,7 +809,8 @@ def hidden_supported(h: int) -> bool:
 __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
-    "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "batch_norm_add_bn_relu",
+    "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

@@ -54,11 +54,22 @@ hipError_t madnn_xent_bwd(const void*, int, const int64_t*, const float*, int64_
 hipError_t madnn_bn_bwd(const void*, const void*, const unsigned char*, int, void*, void*, int64_t, int, int, int,
                         const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
                         float*, hipStream_t);
+hipError_t madnn_bn_fwd_dual(const void*, const void*, void*, unsigned char*, int64_t, int, float, float, const float*,
+                             const float*, float*, float*, int64_t*, float*, float*, float*, float*, const float*, int,
+                             float, float, const float*, const float*, float*, float*, int64_t*, float*, float*,
+                             float*, float*, const float*, int, float*, hipStream_t);
+hipError_t madnn_bn_bwd_dual(const void*, const void*, const void*, const unsigned char*, void*, void*, int64_t, int,
+                             const float*, const float*, const float*, const float*, const float*, const float*,
+                             float*, float*, float*, float*, float*, float*, hipStream_t);
 int madnn_conv1x1_supported(int64_t, int64_t);
 int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
-hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, hipStream_t);
+hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, const float*,
+                             const float*, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, hipStream_t);
-hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, hipStream_t);
+hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
+                               hipStream_t);
+hipError_t madnn_bn_coef(const void*, int64_t, int, float, float, const float*, const float*, float*, float*, int64_t*,
+                         float*, float*, float*, float*, float*, const float*, int, hipStream_t);
 int madnn_stem_supported(int, int);
 int madnn_stem_stat_rows(int, int, int);
 hipError_t madnn_stem_fwd(const void*, const void*, void*, float*, int, int, int, hipStream_t);
@@ -383,6 +394,126 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
   return {dx, dw, db, dres};
 }
 
+// relu(BN(x) + BN_r(r)) in training (ResNet's bn3 with the downsample BatchNorm folded in).
+// Returns y, the ReLU bit mask and (mean, invstd, scale, shift) of each BN: 10 tensors.
+std::vector<at::Tensor> bn_fwd_dual(const at::Tensor& x, const at::Tensor& r, const c10::optional<at::Tensor>& w,
+                                    const c10::optional<at::Tensor>& b, const c10::optional<at::Tensor>& run_mean,
+                                    const c10::optional<at::Tensor>& run_var, const c10::optional<at::Tensor>& nbt,
+                                    double momentum, double eps, const c10::optional<at::Tensor>& partial,
+                                    const c10::optional<at::Tensor>& w_r, const c10::optional<at::Tensor>& b_r,
+                                    const c10::optional<at::Tensor>& run_mean_r,
+                                    const c10::optional<at::Tensor>& run_var_r,
+                                    const c10::optional<at::Tensor>& nbt_r, double momentum_r, double eps_r,
+                                    const c10::optional<at::Tensor>& partial_r) {
+  check_dev(x, "x");
+  check_dev(r, "r");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && r.scalar_type() == at::kBFloat16, "bn_fwd_dual: bf16 only");
+  const int64_t C = x.size(1);
+  TORCH_CHECK(madnn_bn_supported((int)C), "bn kernel needs C % 8 == 0 and C <= 2048, got ", C);
+  const int64_t M = bn_rows(x, C);
+  TORCH_CHECK(r.sizes() == x.sizes() && r.strides() == x.strides(), "bn_fwd_dual: residual layout");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  auto ext = [&](const c10::optional<at::Tensor>& p) -> const float* {
+    if (!p.has_value() || !p->defined() || p->numel() == 0) return nullptr;
+    TORCH_CHECK(p->scalar_type() == at::kFloat && p->is_contiguous() && p->dim() == 3 && p->size(1) == 2 &&
+                    p->size(2) == C,
+                "bn: partial statistics must be fp32 [rows, 2, C]");
+    return p->data_ptr<float>();
+  };
+  auto nbp = [](const c10::optional<at::Tensor>& t) -> int64_t* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kLong && t->is_cuda(), "num_batches_tracked must be an int64 device tensor");
+    return t->data_ptr<int64_t>();
+  };
+  std::vector<at::Tensor> out;
+  out.push_back(at::empty_like(x));
+  out.push_back(at::empty({x.numel() / 8}, x.options().dtype(at::kByte)));
+  for (int k = 0; k < 8; ++k) out.push_back(at::empty({C}, fo));
+  at::Tensor ws = at::empty({(int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
+  const float* pe = ext(partial);
+  const float* pr = ext(partial_r);
+  check(madnn_bn_fwd_dual(x.data_ptr(), r.data_ptr(), out[0].data_ptr(), out[1].data_ptr<uint8_t>(), M, (int)C,
+                          (float)eps, (float)momentum, optf(w), optf(b), optf_mut(run_mean), optf_mut(run_var),
+                          nbp(nbt), out[2].data_ptr<float>(), out[3].data_ptr<float>(), out[4].data_ptr<float>(),
+                          out[5].data_ptr<float>(), pe, pe ? (int)partial->size(0) : 0, (float)eps_r,
+                          (float)momentum_r, optf(w_r), optf(b_r), optf_mut(run_mean_r), optf_mut(run_var_r),
+                          nbp(nbt_r), out[6].data_ptr<float>(), out[7].data_ptr<float>(), out[8].data_ptr<float>(),
+                          out[9].data_ptr<float>(), pr, pr ? (int)partial_r->size(0) : 0, ws.data_ptr<float>(),
+                          cur_stream(x)),
+        "bn_fwd_dual");
+  return out;
+}
+
+// -> dx, dr, dw, db, dw_r, db_r
+std::vector<at::Tensor> bn_bwd_dual(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& r,
+                                    const at::Tensor& mask, const c10::optional<at::Tensor>& w,
+                                    const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                    const c10::optional<at::Tensor>& w_r, const at::Tensor& save_mean_r,
+                                    const at::Tensor& save_invstd_r) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = bn_rows(x, C);
+  TORCH_CHECK(r.sizes() == x.sizes() && r.strides() == x.strides() && r.scalar_type() == x.scalar_type(),
+              "bn_bwd_dual: residual layout");
+  TORCH_CHECK(mask.numel() == x.numel() / 8, "bn_bwd_dual: ReLU bit mask required");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor dyc = dy;
+  if (dy.strides() != x.strides() || dy.scalar_type() != x.scalar_type()) {
+    dyc = at::empty_like(x);
+    dyc.copy_(dy);
+  }
+  auto fo = x.options().dtype(at::kFloat);
+  std::vector<at::Tensor> out{at::empty_like(x), at::empty_like(x), at::empty({C}, fo), at::empty({C}, fo),
+                              at::empty({C}, fo), at::empty({C}, fo)};
+  at::Tensor coef = at::empty({6 * C}, fo);
+  at::Tensor ws = at::empty({(int64_t)madnn_bn_partial_rows(M, (int)C) * 3 * C}, fo);
+  check(madnn_bn_bwd_dual(dyc.data_ptr(), x.data_ptr(), r.data_ptr(), mask.data_ptr<uint8_t>(), out[0].data_ptr(),
+                          out[1].data_ptr(), M, (int)C, optf(w), save_mean.data_ptr<float>(),
+                          save_invstd.data_ptr<float>(), optf(w_r), save_mean_r.data_ptr<float>(),
+                          save_invstd_r.data_ptr<float>(), out[2].data_ptr<float>(), out[3].data_ptr<float>(),
+                          out[4].data_ptr<float>(), out[5].data_ptr<float>(), coef.data_ptr<float>(),
+                          ws.data_ptr<float>(), cur_stream(x)),
+        "bn_bwd_dual");
+  return out;
+}
+
+// Training BatchNorm coefficients only (statistics pass unless `partial` is given, finalize with
+// the running-stat update): -> mean, invstd, scale, shift.  The apply is left to a consumer
+// kernel (K9's BatchNorm prologue).
+std::vector<at::Tensor> bn_coef(const at::Tensor& x, const c10::optional<at::Tensor>& w,
+                                const c10::optional<at::Tensor>& b, const c10::optional<at::Tensor>& run_mean,
+                                const c10::optional<at::Tensor>& run_var, const c10::optional<at::Tensor>& nbt,
+                                double momentum, double eps, const c10::optional<at::Tensor>& partial) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  TORCH_CHECK(madnn_bn_supported((int)C), "bn kernel needs C % 8 == 0 and C <= 2048, got ", C);
+  const int64_t M = bn_rows(x, C);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "bn_coef: bf16 only");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  std::vector<at::Tensor> out;
+  for (int k = 0; k < 4; ++k) out.push_back(at::empty({C}, fo));
+  const bool ext = partial.has_value() && partial->defined() && partial->numel() > 0;
+  if (ext) {
+    TORCH_CHECK(partial->scalar_type() == at::kFloat && partial->is_contiguous() && partial->dim() == 3 &&
+                    partial->size(1) == 2 && partial->size(2) == C,
+                "bn: partial statistics must be fp32 [rows, 2, C]");
+  }
+  at::Tensor ws = at::empty({ext ? 1 : (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
+  int64_t* nb = nullptr;
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "num_batches_tracked must be an int64 device tensor");
+    nb = nbt->data_ptr<int64_t>();
+  }
+  check(madnn_bn_coef(x.data_ptr(), M, (int)C, (float)eps, (float)momentum, optf(w), optf(b), optf_mut(run_mean),
+                      optf_mut(run_var), nb, out[0].data_ptr<float>(), out[1].data_ptr<float>(),
+                      out[2].data_ptr<float>(), out[3].data_ptr<float>(), ws.data_ptr<float>(),
+                      ext ? partial->data_ptr<float>() : nullptr, ext ? (int)partial->size(0) : 0, cur_stream(x)),
+        "bn_coef");
+  return out;
+}
+
 bool bn_supported(int64_t C) { return madnn_bn_supported((int)C) != 0; }
 
 // ---- K9 NHWC 1x1 convolution (stride 1) on MFMA --------------------------------
@@ -416,16 +547,29 @@ void conv_check_w(const at::Tensor& w, int64_t cout, int64_t cin) {
 }
 
 // y = conv(x, w); with stats: partial [rows, 2, Cout] per-channel (sum, sum of squares) of y
-std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
+// optional BatchNorm prologue: x is convolved as relu(x * scale + shift) (fp32 [cin] each)
+const float* pro_ptr(const c10::optional<at::Tensor>& t, int64_t C, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, "conv1x1: ", name,
+              " must be fp32 [Cin]");
+  return t->data_ptr<float>();
+}
+
+std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, bool stats,
+                                               const c10::optional<at::Tensor>& scale,
+                                               const c10::optional<at::Tensor>& shift) {
   const int64_t cin = x.size(1), cout = w.size(0);
   const int64_t M = conv_rows(x, cin, "x");
   conv_check_w(w, cout, cin);
+  const float* sc = pro_ptr(scale, cin, "scale");
+  const float* sh = pro_ptr(shift, cin, "shift");
+  TORCH_CHECK((sc == nullptr) == (sh == nullptr), "conv1x1: scale and shift go together");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = conv_out_like(x, cout);
   const int64_t rows = stats ? madnn_conv1x1_stat_rows(M, cin, cout) : 0;
   at::Tensor part = at::empty({rows, 2, cout}, x.options().dtype(at::kFloat));
   check(madnn_conv1x1_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, M, cin,
-                          cout, cur_stream(x)),
+                          cout, sc, sh, cur_stream(x)),
         "conv1x1_fwd");
   return {y, part};
 }
@@ -448,14 +592,18 @@ at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::o
 }
 
 // fp32 [Cout, Cin] weight gradient
-at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x) {
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
+                         const c10::optional<at::Tensor>& shift) {
   const int64_t cout = dy.size(1), cin = x.size(1);
+  const float* sc = pro_ptr(scale, cin, "scale");
+  const float* sh = pro_ptr(shift, cin, "shift");
+  TORCH_CHECK((sc == nullptr) == (sh == nullptr), "conv1x1: scale and shift go together");
   const int64_t M = conv_rows(x, cin, "x");
   TORCH_CHECK(conv_rows(dy, cout, "dy") == M && dy.dim() == x.dim(), "conv1x1_wgrad: dy / x pixel mismatch");
   TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor dw = at::zeros({cout, cin}, x.options().dtype(at::kFloat));
-  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, cin, cout, cur_stream(x)),
+  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, cin, cout, sc, sh, cur_stream(x)),
         "conv1x1_wgrad");
   return dw;
 }
@@ -833,13 +981,24 @@ TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? mask, bool has_res, Tensor? w, Tensor save_mean, Tensor save_invstd, "
       "Tensor scale, Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "bn_fwd_dual(Tensor x, Tensor r, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
+      "Tensor(c!)? nbt, float momentum, float eps, Tensor? partial, Tensor? w_r, Tensor? b_r, "
+      "Tensor(d!)? run_mean_r, Tensor(e!)? run_var_r, Tensor(f!)? nbt_r, float momentum_r, float eps_r, "
+      "Tensor? partial_r) -> Tensor[]");
+  m.def(
+      "bn_bwd_dual(Tensor dy, Tensor x, Tensor r, Tensor mask, Tensor? w, Tensor save_mean, Tensor save_invstd, "
+      "Tensor? w_r, Tensor save_mean_r, Tensor save_invstd_r) -> Tensor[]");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
       "Tensor(c!) dv, bool causal, float scale) -> ()");
-  m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
+  m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
-  m.def("conv1x1_wgrad(Tensor dy, Tensor x) -> Tensor");
+  m.def("conv1x1_wgrad(Tensor dy, Tensor x, Tensor? scale=None, Tensor? shift=None) -> Tensor");
+  m.def(
+      "bn_coef(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, "
+      "float momentum, float eps, Tensor? partial=None) -> Tensor[]");
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
@@ -878,6 +1037,9 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("norm_bwd", norm_bwd);
   m.impl("bn_fwd", bn_fwd);
   m.impl("bn_bwd", bn_bwd);
+  m.impl("bn_fwd_dual", bn_fwd_dual);
+  m.impl("bn_coef", bn_coef);
+  m.impl("bn_bwd_dual", bn_bwd_dual);
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
   m.impl("maxpool_fwd", maxpool_fwd);

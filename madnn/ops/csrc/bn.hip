@@ -219,12 +219,16 @@ __global__ void bn_eval_coef_kernel(int C, float eps, const float* __restrict__ 
 // y = act(x*scale + shift + res)
 // RELU && RES: also write the ReLU mask as bits (1 byte per 8 elements), so the
 // backward passes need neither the residual nor the affine recompute for it.
-template <int XDT, bool RELU, bool RES>
+// RAFF: the residual is itself a BatchNorm input (ResNet's downsample path): res is read raw and
+// normalised in place, res*rscale + rshift, so the downsample BN never materialises its output.
+template <int XDT, bool RELU, bool RES, bool RAFF = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ x, const void* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, void* __restrict__ y,
                                                        unsigned char* __restrict__ mask, int64_t total, int C,
-                                                       int reverse) {
+                                                       int reverse, const float* __restrict__ rscale = nullptr,
+                                                       const float* __restrict__ rshift = nullptr) {
+  static_assert(!RAFF || RES, "a residual BatchNorm needs the residual");
   for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
     const int64_t i = w.i;
     const int c0 = w.c0;
@@ -234,6 +238,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
     load8<kF32>(shift, c0, sh);
     float r[8];
     if constexpr (RES) load8<XDT>(res, i, r);
+    if constexpr (RAFF) {
+      float rs[8], rh[8];
+      load8<kF32>(rscale, c0, rs);
+      load8<kF32>(rshift, c0, rh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] * rs[j] + rh[j];
+    }
     unsigned bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -256,20 +267,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
 // partial[blk][0:C] = sum g, partial[blk][C:2C] = sum g * x
 // MASKED (RELU && residual): the ReLU mask comes from the forward's bit mask;
 // plain RELU recomputes it from x (which is read anyway).
-template <int XDT, bool RELU, bool MASKED>
+// RAFF (residual BatchNorm, see bn_apply_kernel): the residual's raw input r gets its own
+// reduction from the same g, partial[blk][2C:3C] = sum g * r, so one pass serves both BNs.
+template <int XDT, bool RELU, bool MASKED, bool RAFF = false>
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const unsigned char* __restrict__ mask,
     const float* __restrict__ scale, const float* __restrict__ shift, int64_t M, int C,
-    float* __restrict__ partial) {
+    float* __restrict__ partial, const void* __restrict__ rin = nullptr) {
+  static_assert(!RAFF || MASKED, "a residual BatchNorm comes with the fused residual + ReLU mask");
+  constexpr int NS = RAFF ? 3 : 2;  // sums per channel
   extern __shared__ __attribute__((aligned(16))) float slab[];
   const BnGeom g = bn_geom(C);
   const int t = threadIdx.x;
   const int cg = t % g.tpr;
   const int rs = t / g.tpr;
   const bool active = rs < g.rpi;
-  float sg[8], sgx[8], sc[8], sh[8];
+  float sg[8], sgx[8], sgr[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = sgr[j] = 0.f;
   if (active) {
     if constexpr (RELU && !MASKED) {
       load8<kF32>(scale, cg * 8, sc);
@@ -277,7 +292,7 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
     }
     const int64_t step = (int64_t)gridDim.x * g.rpi;
     int64_t r = (int64_t)blockIdx.x * g.rpi + rs;
-    auto body = [&](const float (&dv)[8], const float (&xv)[8], unsigned bits) {
+    auto body = [&](const float (&dv)[8], const float (&xv)[8], const float (&rv)[8], unsigned bits) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float gj = dv[j];
@@ -291,56 +306,62 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_reduce_kernel(
         }
         sg[j] += gj;
         sgx[j] += gj * xv[j];
+        if constexpr (RAFF) sgr[j] += gj * rv[j];
       }
     };
-    for (; r + step < M; r += 2 * step) {  // 2 rows x (dy, x[, mask]) in flight per lane
-      float dv[2][8], xv[2][8];
+    for (; r + step < M; r += 2 * step) {  // 2 rows x (dy, x[, r][, mask]) in flight per lane
+      float dv[2][8], xv[2][8], rv[2][8];
       unsigned mb[2] = {0u, 0u};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         load8<XDT>(dy, (r + u * step) * C + cg * 8, dv[u]);
         load8<XDT>(x, (r + u * step) * C + cg * 8, xv[u]);
+        if constexpr (RAFF) load8<XDT>(rin, (r + u * step) * C + cg * 8, rv[u]);
         if constexpr (MASKED) mb[u] = mask[((r + u * step) * C + cg * 8) >> 3];
       }
-      body(dv[0], xv[0], mb[0]);
-      body(dv[1], xv[1], mb[1]);
+      body(dv[0], xv[0], rv[0], mb[0]);
+      body(dv[1], xv[1], rv[1], mb[1]);
     }
     for (; r < M; r += step) {
-      float dv[8], xv[8];
+      float dv[8], xv[8], rv[8];
       load8<XDT>(dy, r * C + cg * 8, dv);
       load8<XDT>(x, r * C + cg * 8, xv);
+      if constexpr (RAFF) load8<XDT>(rin, r * C + cg * 8, rv);
       unsigned mb = 0u;
       if constexpr (MASKED) mb = mask[(r * C + cg * 8) >> 3];
-      body(dv, xv, mb);
+      body(dv, xv, rv, mb);
     }
   }
   if (g.rpi == 1) {
     if (active) {
-      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + cg * 8, sg);
-      store8<kF32>(partial, (int64_t)blockIdx.x * 2 * C + C + cg * 8, sgx);
+      store8<kF32>(partial, (int64_t)blockIdx.x * NS * C + cg * 8, sg);
+      store8<kF32>(partial, (int64_t)blockIdx.x * NS * C + C + cg * 8, sgx);
+      if constexpr (RAFF) store8<kF32>(partial, (int64_t)blockIdx.x * NS * C + 2 * C + cg * 8, sgr);
     }
     return;
   }
   if (active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      slab[(rs * 2 + 0) * C + cg * 8 + j] = sg[j];
-      slab[(rs * 2 + 1) * C + cg * 8 + j] = sgx[j];
+      slab[(rs * NS + 0) * C + cg * 8 + j] = sg[j];
+      slab[(rs * NS + 1) * C + cg * 8 + j] = sgx[j];
+      if constexpr (RAFF) slab[(rs * NS + 2) * C + cg * 8 + j] = sgr[j];
     }
   }
   __syncthreads();
-  for (int c = t; c < 2 * C; c += kBnThreads) {
+  for (int c = t; c < NS * C; c += kBnThreads) {
     const int which = c / C, ch = c % C;
     float a = 0.f;
-    for (int r = 0; r < g.rpi; ++r) a += slab[(r * 2 + which) * C + ch];
-    partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+    for (int r = 0; r < g.rpi; ++r) a += slab[(r * NS + which) * C + ch];
+    partial[(int64_t)blockIdx.x * NS * C + c] = a;
   }
 }
 
 // dbeta = sum g ; dgamma = sum g*xhat = invstd*(sum g*x - mean*sum g)
 // dx = w*invstd*(g - dbeta/M - xhat*dgamma/M) = A*g + Bc*x + Cc  (per channel)
+// partial rows are pstride floats apart; sum g at offset 0, sum g*x at qoff
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
-    const float* __restrict__ partial, int G, int C, int64_t M, const float* __restrict__ w,
+    const float* __restrict__ partial, int G, int C, int pstride, int qoff, int64_t M, const float* __restrict__ w,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dw,
     float* __restrict__ db, float* __restrict__ ca, float* __restrict__ cb, float* __restrict__ cc) {
   __shared__ double red[2][kFinSlices][33];
@@ -354,8 +375,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
     for (; k + 3 * kFinSlices < G; k += 4 * kFinSlices) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        fs[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + c];
-        fq[u] = partial[(int64_t)(k + u * kFinSlices) * 2 * C + C + c];
+        fs[u] = partial[(int64_t)(k + u * kFinSlices) * pstride + c];
+        fq[u] = partial[(int64_t)(k + u * kFinSlices) * pstride + qoff + c];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -364,8 +385,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
       }
     }
     for (; k < G; k += kFinSlices) {
-      s += partial[(int64_t)k * 2 * C + c];
-      q += partial[(int64_t)k * 2 * C + C + c];
+      s += partial[(int64_t)k * pstride + c];
+      q += partial[(int64_t)k * pstride + qoff + c];
     }
   }
   red[0][ls][lc] = s;
@@ -392,18 +413,24 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(
   }
 }
 
-template <int XDT, bool RELU, bool RES>
+// RAFF: dres is the residual BatchNorm's input gradient, rca*g + rcb*r + rcc, instead of g itself
+template <int XDT, bool RELU, bool RES, bool RAFF = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const unsigned char* __restrict__ mask,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ ca,
     const float* __restrict__ cb, const float* __restrict__ cc, void* __restrict__ dx, void* __restrict__ dres,
-    int64_t total, int C, int reverse) {
+    int64_t total, int C, int reverse, const void* __restrict__ rin = nullptr,
+    const float* __restrict__ rca = nullptr, const float* __restrict__ rcb = nullptr,
+    const float* __restrict__ rcc = nullptr) {
+  static_assert(!RAFF || (RELU && RES), "a residual BatchNorm comes with the fused residual + ReLU mask");
   for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
     const int64_t i = w.i;
     const int c0 = w.c0;
     float dv[8], xv[8], a[8], b[8], c[8];
     load8<XDT>(dy, i, dv);
     load8<XDT>(x, i, xv);
+    float rv[8];
+    if constexpr (RAFF) load8<XDT>(rin, i, rv);
     load8<kF32>(ca, c0, a);
     load8<kF32>(cb, c0, b);
     load8<kF32>(cc, c0, c);
@@ -425,7 +452,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = a[j] * dv[j] + b[j] * xv[j] + c[j];
     store8<XDT>(dx, i, o);
-    if constexpr (RES) store8<XDT>(dres, i, dv);
+    if constexpr (RAFF) {
+      load8<kF32>(rca, c0, a);
+      load8<kF32>(rcb, c0, b);
+      load8<kF32>(rcc, c0, c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = a[j] * dv[j] + b[j] * rv[j] + c[j];
+      store8<XDT>(dres, i, o);
+    } else if constexpr (RES) {
+      store8<XDT>(dres, i, dv);
+    }
   }
 }
 
@@ -519,7 +555,7 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const unsigned char* mask
   float* ca = coef;
   float* cb = coef + C;
   float* cc = coef + 2 * C;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C, M, w,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C, 2 * C, C, M, w,
                      save_mean, save_invstd, dw, db, ca, cb, cc);
   MADNN_HIP_CHECK(hipGetLastError());
   const int64_t total = M * C;
@@ -531,4 +567,111 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const unsigned char* mask
   return hipGetLastError();
 }
 
+
+// Training forward of relu(BN(x) + BN_r(r)): ResNet's last bottleneck BatchNorm with the downsample
+// path's BatchNorm folded into the same apply pass (bf16 only).  Each BN's statistics come from its
+// producer's epilogue (ext_partial*) or a statistics pass; both finalize into their own coefficients
+// and running statistics; one pass then writes y and the ReLU bit mask.
+hipError_t madnn_bn_fwd_dual(const void* x, const void* r, void* y, unsigned char* mask, int64_t M, int C,
+                             float eps, float momentum, const float* w, const float* b, float* run_mean,
+                             float* run_var, int64_t* nbt, float* save_mean, float* save_invstd, float* scale,
+                             float* shift, const float* ext_partial, int ext_rows, float eps_r, float momentum_r,
+                             const float* w_r, const float* b_r, float* run_mean_r, float* run_var_r,
+                             int64_t* nbt_r, float* save_mean_r, float* save_invstd_r, float* scale_r,
+                             float* shift_r, const float* ext_partial_r, int ext_rows_r, float* workspace,
+                             hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C) || mask == nullptr) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const BnGeom g = bn_geom(C);
+  const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
+  const void* src[2] = {x, r};
+  const float* ext[2] = {ext_partial, ext_partial_r};
+  const int erows[2] = {ext_rows, ext_rows_r};
+  const float epsv[2] = {eps, eps_r}, mom[2] = {momentum, momentum_r};
+  const float* wv[2] = {w, w_r};
+  const float* bv[2] = {b, b_r};
+  float* rm[2] = {run_mean, run_mean_r};
+  float* rv[2] = {run_var, run_var_r};
+  int64_t* nb[2] = {nbt, nbt_r};
+  float* sm[2] = {save_mean, save_mean_r};
+  float* si[2] = {save_invstd, save_invstd_r};
+  float* sc[2] = {scale, scale_r};
+  float* sh[2] = {shift, shift_r};
+  for (int k = 0; k < 2; ++k) {
+    const float* part = workspace;
+    int G = bn_grid_rows(M, C);
+    if (ext[k] != nullptr && erows[k] > 0) {
+      part = ext[k];
+      G = erows[k];
+    } else {
+      hipLaunchKernelGGL((bn_stats_kernel<kBF16>), dim3(G), dim3(kBnThreads), lds, stream, src[k], M, C, workspace);
+      MADNN_HIP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, part, G, C, M,
+                       epsv[k], mom[k], wv[k], bv[k], sm[k], si[k], sc[k], sh[k], rm[k], rv[k], nb[k]);
+    MADNN_HIP_CHECK(hipGetLastError());
+  }
+  const int64_t total = M * C;
+  const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
+  hipLaunchKernelGGL((bn_apply_kernel<kBF16, true, true, true>), dim3(grid), dim3(256), 0, stream, x, r, scale, shift,
+                     y, mask, total, C, bn_tune().reverse, scale_r, shift_r);
+  return hipGetLastError();
+}
+
+// Backward of madnn_bn_fwd_dual: one reduction pass (sum g, sum g*x, sum g*r), two finalizes, one
+// apply pass writing dx and dr.  workspace: bn_partial_rows(M, C) * 3 * C floats; coef: 6 * C.
+hipError_t madnn_bn_bwd_dual(const void* dy, const void* x, const void* r, const unsigned char* mask, void* dx,
+                             void* dr, int64_t M, int C, const float* w, const float* save_mean,
+                             const float* save_invstd, const float* w_r, const float* save_mean_r,
+                             const float* save_invstd_r, float* dw, float* db, float* dw_r, float* db_r, float* coef,
+                             float* workspace, hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C) || mask == nullptr) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  const int G = bn_grid_rows(M, C);
+  const BnGeom g = bn_geom(C);
+  const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 3 * C * sizeof(float) : 0;
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<kBF16, true, true, true>), dim3(G), dim3(kBnThreads), lds, stream, dy, x,
+                     mask, nullptr, nullptr, M, C, workspace, r);
+  MADNN_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C,
+                     3 * C, C, M, w, save_mean, save_invstd, dw, db, coef, coef + C, coef + 2 * C);
+  MADNN_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, workspace, G, C,
+                     3 * C, 2 * C, M, w_r, save_mean_r, save_invstd_r, dw_r, db_r, coef + 3 * C, coef + 4 * C,
+                     coef + 5 * C);
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int64_t total = M * C;
+  const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, true, true, true>), dim3(grid), dim3(256), 0, stream, dy, x, mask,
+                     nullptr, nullptr, coef, coef + C, coef + 2 * C, dx, dr, total, C, bn_tune().reverse, r,
+                     coef + 3 * C, coef + 4 * C, coef + 5 * C);
+  return hipGetLastError();
+}
+
+
+// Training statistics + finalize only (see bn_coef in binding.cpp): the apply runs in a consumer.
+hipError_t madnn_bn_coef(const void* x, int64_t M, int C, float eps, float momentum, const float* w, const float* b,
+                         float* run_mean, float* run_var, int64_t* nbt, float* save_mean, float* save_invstd,
+                         float* scale, float* shift, float* workspace, const float* ext_partial, int ext_rows,
+                         hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C)) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  int G = bn_grid_rows(M, C);
+  const float* part = workspace;
+  if (ext_partial != nullptr && ext_rows > 0) {
+    part = ext_partial;
+    G = ext_rows;
+  } else {
+    const BnGeom g = bn_geom(C);
+    const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
+    hipLaunchKernelGGL((bn_stats_kernel<kBF16>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
+    MADNN_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, part, G, C, M, eps,
+                     momentum, w, b, save_mean, save_invstd, scale, shift, run_mean, run_var, nbt);
+  return hipGetLastError();
+}
 }  // extern "C"

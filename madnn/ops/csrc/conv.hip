@@ -34,6 +34,13 @@
 // the sum and sum of squares of the bf16-rounded outputs it stores, in registers across
 // all its tiles, and writes one [2][Cout] partial row.  That slab is the input format of
 // bn.hip's finalize kernel, so the BatchNorm forward skips its statistics pass over Y.
+//
+// Fused BatchNorm apply + ReLU prologue (forward and weight grad, operand X): when X is the
+// raw output of the previous convolution, x = relu(y * scale[c] + shift[c]) is computed on the
+// register-staged chunk (8 channels) between its global load and its LDS store, so the
+// normalised activation is never written to or read from HBM (ResNet's bn2 -> conv3).  The
+// channel of a thread's chunk is the same for all of its chunks of a k step (row memory: k0 +
+// 8 (tid & 7); column memory: x0 + 8 (tid % (R/8))), so scale/shift are loaded once per step.
 #include "mfma.h"
 
 namespace madnn {
@@ -64,6 +71,8 @@ struct GemmArgs {
   void* out;
   const uint16_t* res;  // store epilogue: out = D + res (same layout as out), or null
   float* stats;
+  const float* bsc;  // B-operand BatchNorm prologue: relu(b * bsc[c] + bsh[c]) (PRO kernels)
+  const float* bsh;
   int64_t lda, ldb, ldo;
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
@@ -73,13 +82,43 @@ struct GemmArgs {
 // One operand's 64-deep slice, register-staged: R rows of "row" memory ([x][ld], k
 // contiguous) or 64 k-rows of "column" memory ([k][ld], R contiguous x).  Rows past the
 // end load a valid row and are zeroed by a mask (no per-load branch).
+// relu(v * sc + sh) on 8 packed bf16 (fp32 math, one rounding: bn_apply_kernel's arithmetic)
+__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const float4 s0, const float4 s1, const float4 h0,
+                                          const float4 h1) {
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float lo = bf16_to_f32((unsigned short)(v[e] & 0xffffu)) * sc[2 * e] + sh[2 * e];
+    float hi = bf16_to_f32((unsigned short)(v[e] >> 16)) * sc[2 * e + 1] + sh[2 * e + 1];
+    lo = lo > 0.f ? lo : 0.f;
+    hi = hi > 0.f ? hi : 0.f;
+    o[e] = (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+  }
+  return o;
+}
+
 template <bool COL, int R>
 struct Stage {
   static constexpr int PER = R / 32;  // 16-B chunks per thread
   u32x4 r[PER];
+  float4 ps0, ps1, ph0, ph1;  // PRO: this thread's 8 channels of scale / shift
 
+  // PRO: also fetch scale/shift of the chunk's channels (ch = the chunk's first channel = col);
+  // the transform itself waits until store(), so the global loads stay in flight across the
+  // MFMAs of the current step like the plain path's
+  template <bool PRO = false>
   __device__ __forceinline__ void load(const uint16_t* __restrict__ base, int64_t ld, int64_t x0, int64_t xlim,
-                                       int64_t k0, int64_t klim, int tid) {
+                                       int64_t k0, int64_t klim, int tid, const float* __restrict__ sc = nullptr,
+                                       const float* __restrict__ sh = nullptr) {
+    if constexpr (PRO) {  // chunk channel is thread-invariant across i (kThreads is a multiple of R / 8 and 8)
+      const int64_t ch = COL ? x0 + (tid % (R / 8)) * 8 : k0 + (tid & 7) * 8;
+      ps0 = *reinterpret_cast<const float4*>(sc + ch);
+      ps1 = *reinterpret_cast<const float4*>(sc + ch + 4);
+      ph0 = *reinterpret_cast<const float4*>(sh + ch);
+      ph1 = *reinterpret_cast<const float4*>(sh + ch + 4);
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + kThreads * i;
@@ -100,6 +139,9 @@ struct Stage {
     }
   }
 
+  // PRO: masked-off rows become relu(shift), which is harmless: forward B rows past J only feed
+  // output columns that are never stored, and weight-grad k rows past K meet a zeroed A row
+  template <bool PRO = false>
   __device__ __forceinline__ void store(uint16_t* tile, int tid) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -110,7 +152,9 @@ struct Stage {
       } else {
         boff = swz<64>(c >> 3, c & 7);
       }
-      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(tile) + boff) = r[i];
+      u32x4 v = r[i];
+      if constexpr (PRO) v = bn_relu8(v, ps0, ps1, ph0, ph1);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(tile) + boff) = v;
     }
   }
 
@@ -124,7 +168,7 @@ struct Stage {
   }
 };
 
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS>
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   constexpr int NI = (BI == 64 && BJ == 64) ? 1 : 2;  // 32-row i blocks per wave
   constexpr int WI = BI / (32 * NI), WJ = 4 / WI, NJ = BJ / (32 * WJ);
@@ -183,9 +227,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   };
 
   sta.load(p.a, p.lda, i0, p.I, (int64_t)kbeg * kBK, p.K, tid);
-  stb.load(p.b, p.ldb, (int64_t)jt * BJ, p.J, (int64_t)kbeg * kBK, p.K, tid);
+  stb.template load<PRO>(p.b, p.ldb, (int64_t)jt * BJ, p.J, (int64_t)kbeg * kBK, p.K, tid, p.bsc, p.bsh);
   sta.store(smem, tid);
-  stb.store(smem + AE, tid);
+  stb.template store<PRO>(smem + AE, tid);
   __syncthreads();
   int cur = 0, ks = kbeg;
   for (;;) {
@@ -197,7 +241,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
     const bool more = njt < p.j_tiles;
     if (more) {
       sta.load(p.a, p.lda, i0, p.I, (int64_t)nks * kBK, p.K, tid);
-      stb.load(p.b, p.ldb, (int64_t)njt * BJ, p.J, (int64_t)nks * kBK, p.K, tid);
+      stb.template load<PRO>(p.b, p.ldb, (int64_t)njt * BJ, p.J, (int64_t)nks * kBK, p.K, tid, p.bsc, p.bsh);
     }
     uint16_t* buf = smem + cur * SE;
 #pragma unroll
@@ -214,7 +258,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
     }
     if (more) {  // the other buffer was last read before the previous barrier
       sta.store(smem + (cur ^ 1) * SE, tid);
-      stb.store(smem + (cur ^ 1) * SE + AE, tid);
+      stb.template store<PRO>(smem + (cur ^ 1) * SE + AE, tid);
     }
     if (ks == kend - 1) {  // tile done: epilogue
       if constexpr (MODE == kStoreT) {
@@ -313,9 +357,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   }
 }
 
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS>
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false>
 hipError_t launch(const GemmArgs& p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS>), dim3(grid), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS, PRO>), dim3(grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
 }
 
@@ -360,8 +404,9 @@ int madnn_conv1x1_stat_rows(int64_t M, int64_t cin, int64_t cout) {
   return p.j_groups;
 }
 
+// bsc/bsh (optional, [cin] fp32): x is a raw BatchNorm input, convolved as relu(x * bsc + bsh)
 hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats, int64_t M, int64_t cin,
-                             int64_t cout, hipStream_t s) {
+                             int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -372,6 +417,8 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
   p.out = y;
   p.ldo = cout;
   p.stats = stats;
+  p.bsc = bsc;
+  p.bsh = bsh;
   p.xcd = tune().xcd;
   p.I = cout;
   p.J = M;
@@ -379,6 +426,15 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
   const bool wide = cout % 128 == 0;
   plan_persistent(p, M, wide ? 128 : 64, cout, cin);
   const int grid = p.i_tiles * p.j_groups;
+  if ((bsc == nullptr) != (bsh == nullptr)) return hipErrorInvalidValue;
+  if (bsc != nullptr) {
+    if (wide) {
+      return stats ? launch<false, false, 128, 128, kStoreT, true, true>(p, grid, s)
+                   : launch<false, false, 128, 128, kStoreT, false, true>(p, grid, s);
+    }
+    return stats ? launch<false, false, 64, 128, kStoreT, true, true>(p, grid, s)
+                 : launch<false, false, 64, 128, kStoreT, false, true>(p, grid, s);
+  }
   if (wide) {
     return stats ? launch<false, false, 128, 128, kStoreT, true>(p, grid, s)
                  : launch<false, false, 128, 128, kStoreT, false>(p, grid, s);
@@ -412,8 +468,9 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
 }
 
 // dw: zero-initialised fp32 [cout][cin]; partial sums over m are added atomically
+// bsc/bsh (optional): x is convolved as relu(x * bsc + bsh), as in madnn_conv1x1_fwd
 hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t M, int64_t cin, int64_t cout,
-                               hipStream_t s) {
+                               const float* bsc, const float* bsh, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -422,6 +479,8 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t
   p.b = static_cast<const uint16_t*>(x);  // B[k = m][j = ci] = X[m][ci]: column memory
   p.ldb = cin;
   p.out = dw;
+  p.bsc = bsc;
+  p.bsh = bsh;
   p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cout;
@@ -438,6 +497,13 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t
   splits = (nk + p.k_chunk - 1) / p.k_chunk;
   const int grid = (int)(tiles * splits);
   p.j_groups = 0;
+  if ((bsc == nullptr) != (bsh == nullptr)) return hipErrorInvalidValue;
+  if (bsc != nullptr) {
+    if (bi == 128 && bj == 128) return launch<true, true, 128, 128, kAtomic, false, true>(p, grid, s);
+    if (bi == 128) return launch<true, true, 128, 64, kAtomic, false, true>(p, grid, s);
+    if (bj == 128) return launch<true, true, 64, 128, kAtomic, false, true>(p, grid, s);
+    return launch<true, true, 64, 64, kAtomic, false, true>(p, grid, s);
+  }
   if (bi == 128 && bj == 128) return launch<true, true, 128, 128, kAtomic, false>(p, grid, s);
   if (bi == 128) return launch<true, true, 128, 64, kAtomic, false>(p, grid, s);
   if (bj == 128) return launch<true, true, 64, 128, kAtomic, false>(p, grid, s);

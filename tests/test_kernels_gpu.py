@@ -430,3 +430,95 @@ def test_gelu_fwd_kernel_matches_fp32(cuda, shape, dt):
     assert y.dtype == dt
     torch.testing.assert_close(y.float(), yr, atol=1e-2 if dt == torch.bfloat16 else 1e-5,
                                rtol=1e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("with_stats", [False, True])
+def test_batchnorm_dual_residual_bn(cuda, C, with_stats):
+    """K5 RAFF: relu(bn(x) + bn_r(r)) in one kernel pair vs fp32 eager: output, both BNs' running
+    stats / nbt and every gradient (x, r, both weights and biases)."""
+    from madnn.nn.norm import FusedBatchNorm2d
+
+    torch.manual_seed(9)
+    N, H, W = 6, 7, 9
+    x = (torch.randn(N, C, H, W, device=cuda) * 1.5 + 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    r = (torch.randn(N, C, H, W, device=cuda) * 0.7 - 0.2).bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    r.requires_grad_(True)
+    bn, bn_r = FusedBatchNorm2d(C).to(cuda), FusedBatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        for m in (bn, bn_r):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.normal_(0, 0.1)
+    ref_bn, ref_bn_r = torch.nn.BatchNorm2d(C).to(cuda), torch.nn.BatchNorm2d(C).to(cuda)
+    ref_bn.load_state_dict(bn.state_dict())
+    ref_bn_r.load_state_dict(bn_r.state_dict())
+    st = st_r = None
+    if with_stats:  # producer-epilogue format: [rows, 2, C] partial (sum, sum of squares)
+        def part(t):
+            v = t.detach().float().permute(0, 2, 3, 1).reshape(3, -1, C)
+            return torch.stack([v.sum(1), (v * v).sum(1)], 1).contiguous()
+        st, st_r = part(x), part(r)
+    assert ops.batch_norm_dual_supported(x, r, bn, bn_r)
+    y = ops.batch_norm_add_bn_relu(x, r, bn, bn_r, st, st_r)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True)
+    yr = torch.relu(ref_bn(xr) + ref_bn_r(rr))
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    for m, mr in ((bn, ref_bn), (bn_r, ref_bn_r)):
+        torch.testing.assert_close(m.running_mean, mr.running_mean, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(m.running_var, mr.running_var, atol=1e-3, rtol=1e-3)
+        assert int(m.num_batches_tracked) == 1
+        torch.testing.assert_close(m.weight.grad, mr.weight.grad, atol=0.15, rtol=0.05)
+        torch.testing.assert_close(m.bias.grad, mr.bias.grad, atol=0.15, rtol=0.05)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=9e-2, rtol=9e-2)
+    torch.testing.assert_close(r.grad.float(), rr.grad, atol=9e-2, rtol=9e-2)
+
+
+def test_resnet50_downsample_block_dual_bn_matches_composition(cuda):
+    """A downsample Bottleneck with the dual BN path vs the same block with it switched off."""
+    import madnn.models.resnet as R
+
+    torch.manual_seed(10)
+    ds = torch.nn.Sequential(R.conv1x1(64, 256, 2), R.BN(256))
+    blk = R.Bottleneck(64, 64, 2, ds).to(cuda).bfloat16()
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.float()
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    import copy
+    blk2 = copy.deepcopy(blk)
+    assert blk._dual_bn()
+    x = torch.randn(8, 64, 28, 28, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    y1 = blk(x1)
+    old = R._DUAL_BN
+    R._DUAL_BN = False
+    try:
+        assert not blk2._dual_bn()
+        y2 = blk2(x2)
+    finally:
+        R._DUAL_BN = old
+    # fp32 copy of the same block (eager convolutions, composed BNs) as the oracle: bf16 ReLU-mask
+    # flips make two bf16 paths differ element-wise, so compare each path's error against fp32
+    blk3 = copy.deepcopy(blk2).float()
+    x3 = x.float().requires_grad_(True)
+    y3 = blk3(x3)
+    dy = torch.randn_like(y1)
+    y1.backward(dy)
+    y2.backward(dy)
+    y3.backward(dy.float())
+
+    def rel(a, b):
+        return ((a.float() - b).norm() / b.norm()).item()
+
+    assert rel(y1, y3) <= 1.5 * rel(y2, y3) + 1e-3
+    assert rel(x1.grad, x3.grad) <= 1.5 * rel(x2.grad, x3.grad) + 1e-3
+    assert rel(x1.grad, x3.grad) < 0.1   # bf16 end to end through a whole block: ~0.06
+    for (n, p1), p2, p3 in zip(blk.named_parameters(), blk2.parameters(), blk3.parameters()):
+        assert rel(p1.grad, p3.grad) <= 1.5 * rel(p2.grad, p3.grad) + 2e-3, n
+    for (n, b1), b2 in zip(blk.named_buffers(), blk2.buffers()):
+        torch.testing.assert_close(b1.float(), b2.float(), atol=1e-3, rtol=1e-3, msg=n)
