@@ -26,7 +26,8 @@ from torch import nn
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
-from ..ops import batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_supported
+from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_supported, bn_relu_maxpool,
+                   bn_relu_maxpool_supported)
 
 # A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
 _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
@@ -154,6 +155,11 @@ class ResNet(nn.Module):
 
     def stem(self, x):
         y, st = self.conv1(x, stats=True)
+        if isinstance(self.bn1, BN) and isinstance(self.maxpool, FusedMaxPool2d) \
+                and bn_relu_maxpool_supported(y, self.bn1, self.maxpool):
+            # BN apply + ReLU inside the max-pool's window loads; the pool gradient gathered
+            # inside the BN backward: relu(bn1(y)) and its gradient never reach HBM
+            return bn_relu_maxpool(y, self.bn1, self.maxpool, st)
         return self.maxpool(self.bn1(y, relu=True, stats=st))
 
     def head(self, x):

@@ -307,6 +307,8 @@ def batch_norm_dual_supported(x: torch.Tensor, r: torch.Tensor, bn, bn_r) -> boo
     def ok(m):
         return (m.training and m.track_running_stats and m.affine and m.momentum is not None
                 and m.weight.dtype == torch.float32)
+    if not (isinstance(x, torch.Tensor) and isinstance(r, torch.Tensor)):   # e.g. fx tracing proxies
+        return False
     return (x.dtype == torch.bfloat16 and bn_supported(x, bn.weight) and r.shape == x.shape
             and r.dtype == x.dtype and r.stride() == x.stride() and ok(bn) and ok(bn_r))
 
@@ -636,7 +638,7 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
 def bn_relu_conv1x1_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
     """Whether :func:`bn_relu_conv1x1` runs fused: training-mode BN with running statistics and an
     fp32 affine, bf16 NHWC input, K9-shaped weight."""
-    return (_BN_PROLOGUE and bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None
+    return (_BN_PROLOGUE and isinstance(y, torch.Tensor) and bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None
             and bn.weight.dtype == torch.float32 and conv1x1_supported(y, w) and bn_supported(y, bn.weight))
 
 
@@ -657,7 +659,60 @@ def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[
     return (out, None) if stats else out
 
 
-_BN_PROLOGUE = os.environ.get("MADNN_BN_PROLOGUE", "1") != "0"
+# Off by default: same-process A/B at batch 1536 (profiles/r2_ab_bn_prologue.json): 121.8 -> 122.2
+# ms/step.  The fused forward costs +0.8 ms/step over the plain K9 forward (its prologue VALU work sits
+# on the LDS-store path of a one-k-step-per-tile, write-bound GEMM) and K9's weight grad is 1.1 ms/step
+# slower than MIOpen's on the conv3 shapes; together they eat the 1.5 ms/step bn2 apply pass saved.
+_BN_PROLOGUE = os.environ.get("MADNN_BN_PROLOGUE", "0") != "0"
+
+
+class _BNReluMaxPoolFn(torch.autograd.Function):
+    """``max_pool2d(relu(bn(y)), 3, 2, 1)`` in training (ResNet's stem): the BN apply + ReLU run
+    inside the pool's window loads; backward gathers the pool gradient per input pixel inside the
+    BN backward's two passes, so neither relu(bn(y)) nor its gradient is ever written to HBM."""
+
+    @staticmethod
+    def forward(ctx, y, bn_w, bn_b, bn, stats_in, p):
+        mean, invstd, scale, shift = torch.ops.madnn.bn_coef(y, bn_w, bn_b, bn.running_mean, bn.running_var,
+                                                             bn.num_batches_tracked, float(bn.momentum),
+                                                             float(bn.eps), stats_in)
+        out, arg = torch.ops.madnn.pool_bn_fwd(y, scale, shift, int(p))
+        ctx.save_for_backward(y, arg, bn_w, mean, invstd, scale, shift)
+        ctx.p = int(p)
+        return out
+
+    @staticmethod
+    def backward(ctx, dp):
+        y, arg, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        dy, dw, db = torch.ops.madnn.pool_bn_bwd(dp, arg, y, bn_w, mean, invstd, scale, shift, ctx.p)
+        return dy, dw, db, None, None, None
+
+
+def bn_relu_maxpool_supported(y: torch.Tensor, bn, pool) -> bool:
+    """The stem shape the fused BN + ReLU + 3x3/s2 max-pool takes (training BN, bf16 NHWC)."""
+    def pair(v):
+        return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+    return (_POOL_BN and isinstance(y, torch.Tensor) and y.device.type == "cuda" and y.dtype == torch.bfloat16 and y.dim() == 4
+            and y.is_contiguous(memory_format=torch.channels_last) and bn.training and bn.track_running_stats
+            and bn.affine and bn.momentum is not None and bn.weight.dtype == torch.float32
+            and pair(pool.kernel_size) == (3, 3) and pair(pool.stride) == (2, 2) and pair(pool.padding) in ((1, 1), (0, 0))
+            and pair(pool.dilation) == (1, 1) and not pool.ceil_mode and not pool.return_indices
+            and y.size(1) % 8 == 0 and 256 % (y.size(1) // 8) == 0 and y.numel() < 2 ** 31)
+
+
+def bn_relu_maxpool(y: torch.Tensor, bn, pool, stats_in: Optional[torch.Tensor] = None):
+    """``pool(relu(bn(y)))`` with the BN apply fused into the pool (forward) and the pool gradient
+    gathered inside the BN backward (:class:`_BNReluMaxPoolFn`); composition otherwise."""
+    if bn_relu_maxpool_supported(y, bn, pool):
+        _need_native("bn_relu_maxpool")
+        p = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
+        return _BNReluMaxPoolFn.apply(y, bn.weight, bn.bias, bn, stats_in, p)
+    a = bn(y, relu=True, stats=stats_in) if _is_fused_bn(bn) else torch.relu(bn(y))
+    return pool(a)
+
+
+# A/B knob: the stem's BN + ReLU + max-pool as one fused pair of passes (1) or as K5 + K7 (0)
+_POOL_BN = os.environ.get("MADNN_POOL_BN", "1") != "0"
 
 
 # ---------------------------------------------------------------------- K13
@@ -810,7 +865,8 @@ __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
     "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "batch_norm_add_bn_relu",
-    "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "bn_relu_maxpool",
+    "bn_relu_maxpool_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

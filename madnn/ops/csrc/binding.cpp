@@ -45,6 +45,13 @@ hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
 int madnn_maxpool_supported(int64_t, int, int);
 hipError_t madnn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+int madnn_pool_bn_supported(int64_t, int);
+int madnn_pool_bn_bwd_rows(int64_t, int);
+hipError_t madnn_pool_bn_fwd(const void*, const float*, const float*, void*, void*, int, int, int, int, int, int, int,
+                             hipStream_t);
+hipError_t madnn_pool_bn_bwd(const void*, const void*, const void*, const float*, const float*, const float*,
+                             const float*, const float*, void*, float*, float*, float*, float*, int, int, int, int, int,
+                             int, int, hipStream_t);
 hipError_t madnn_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int,
                              hipStream_t);
 hipError_t madnn_xent_fwd(const void*, int, const int64_t*, int64_t, int64_t, int64_t, int, int, float*, float*,
@@ -856,6 +863,55 @@ at::Tensor maxpool_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, i
   return dx;
 }
 
+// maxpool 3x3/s2(relu(bn(y))) with the BN apply + ReLU fused into the pool (ResNet stem).
+// y: bf16 NHWC raw BN input; scale/shift from bn_coef.  -> (pooled output, 1-byte argmax map)
+std::tuple<at::Tensor, at::Tensor> pool_bn_fwd(const at::Tensor& y, const at::Tensor& scale, const at::Tensor& shift,
+                                               int64_t p) {
+  check_dev(y, "y");
+  TORCH_CHECK(y.dim() == 4 && y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.scalar_type() == at::kBFloat16,
+              "pool_bn: bf16 NHWC 4-D input");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  TORCH_CHECK(madnn_pool_bn_supported(y.numel(), (int)C) && p >= 0 && p <= 1, "pool_bn: unsupported shape");
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat &&
+                  shift.scalar_type() == at::kFloat && scale.is_contiguous() && shift.is_contiguous(),
+              "pool_bn: fp32 [C] scale/shift");
+  const int64_t Ho = (H + 2 * p - 3) / 2 + 1, Wo = (W + 2 * p - 3) / 2 + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "pool_bn: empty output");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  at::Tensor out = at::empty({N, C, Ho, Wo}, y.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor arg = at::empty({N * Ho * Wo * C}, y.options().dtype(at::kByte));
+  check(madnn_pool_bn_fwd(y.data_ptr(), scale.data_ptr<float>(), shift.data_ptr<float>(), out.data_ptr(),
+                          arg.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)p, cur_stream(y)),
+        "pool_bn_fwd");
+  return {out, arg};
+}
+
+// -> (dy, dw, db)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> pool_bn_bwd(const at::Tensor& dp, const at::Tensor& arg,
+                                                           const at::Tensor& y, const c10::optional<at::Tensor>& w,
+                                                           const at::Tensor& mean, const at::Tensor& invstd,
+                                                           const at::Tensor& scale, const at::Tensor& shift,
+                                                           int64_t p) {
+  check_dev(y, "y");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  const int64_t Ho = (H + 2 * p - 3) / 2 + 1, Wo = (W + 2 * p - 3) / 2 + 1;
+  TORCH_CHECK(dp.dim() == 4 && dp.size(0) == N && dp.size(1) == C && dp.size(2) == Ho && dp.size(3) == Wo,
+              "pool_bn_bwd: gradient shape");
+  TORCH_CHECK(arg.numel() == dp.numel() && arg.scalar_type() == at::kByte, "pool_bn_bwd: argmax map mismatch");
+  at::Tensor dpc = dp.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  auto fo = y.options().dtype(at::kFloat);
+  at::Tensor dy = at::empty_like(y);
+  at::Tensor dw = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
+  at::Tensor ws = at::empty({(int64_t)madnn_pool_bn_bwd_rows(N * H * W, (int)C) * 2 * C}, fo);
+  check(madnn_pool_bn_bwd(dpc.data_ptr(), arg.data_ptr(), y.data_ptr(), optf(w), mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(), dy.data_ptr(),
+                          dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), ws.data_ptr<float>(),
+                          (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, (int)p, cur_stream(y)),
+        "pool_bn_bwd");
+  return {dy, dw, db};
+}
+
 // K11 Linear bias gradient.  dy (and pre): [..., N], row-major contiguous.  Returns
 // (db [N] in bias_dtype, dp) where dp = dy * gelu_tanh'(pre) when pre is given (else empty).
 std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::optional<at::Tensor>& pre,
@@ -1008,6 +1064,10 @@ TORCH_LIBRARY(madnn, m) {
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
+  m.def("pool_bn_fwd(Tensor y, Tensor scale, Tensor shift, int p) -> (Tensor, Tensor)");
+  m.def(
+      "pool_bn_bwd(Tensor dp, Tensor arg, Tensor y, Tensor? w, Tensor mean, Tensor invstd, Tensor scale, Tensor shift, "
+      "int p) -> (Tensor, Tensor, Tensor)");
   m.def("maxpool_bwd(Tensor dy, Tensor arg, int H, int W, int k, int s, int p) -> Tensor");
   m.def("bucket_pack(Tensor[] srcs, Tensor(a!) flat, int[] offsets, float scale) -> ()");
   m.def("bucket_unpack(Tensor(a!)[] dsts, Tensor flat, int[] offsets, float scale) -> ()");
@@ -1043,6 +1103,8 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
   m.impl("maxpool_fwd", maxpool_fwd);
+  m.impl("pool_bn_fwd", pool_bn_fwd);
+  m.impl("pool_bn_bwd", pool_bn_bwd);
   m.impl("bias_grad", bias_grad);
   m.impl("gelu_fwd", gelu_fwd);
   m.impl("attn_fwd", attn_fwd);

@@ -674,4 +674,14 @@ hipError_t madnn_bn_coef(const void* x, int64_t M, int C, float eps, float momen
                      momentum, w, b, save_mean, save_invstd, scale, shift, run_mean, run_var, nbt);
   return hipGetLastError();
 }
+
+// The backward finalize on its own (fused consumers with their own reduction pass: pool.hip)
+hipError_t madnn_bn_bwd_finalize(const float* partial, int G, int C, int pstride, int qoff, int64_t M, const float* w,
+                                 const float* mean, const float* invstd, float* dw, float* db, float* ca, float* cb,
+                                 float* cc, hipStream_t stream) {
+  using namespace madnn;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, partial, G, C,
+                     pstride, qoff, M, w, mean, invstd, dw, db, ca, cb, cc);
+  return hipGetLastError();
+}
 }  // extern "C"

@@ -119,10 +119,14 @@ __device__ __forceinline__ unsigned xcd_block_id(int swz) {
 // latency-bound at ~3 TB/s.  These variants compute every window address up front and
 // issue all loads before the first compare, keeping 9 (forward) / 8 (backward) 16-byte
 // loads in flight per lane.  Same scan order, tie-breaking and NaN rule as above.
-template <int XDT>
+// BNRELU: x is a raw BatchNorm input; every window element is relu(x * sc[c] + sh[c]) (the stem's
+// BN apply + ReLU fused into its max-pool: the normalised stem activation never reaches HBM)
+template <int XDT, bool BNRELU = false>
 __global__ __launch_bounds__(256) void maxpool_k3s2_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                                uint64_t* __restrict__ arg, int N, int H, int W,
-                                                               int C, int Ho, int Wo, int p, int swz) {
+                                                               int C, int Ho, int Wo, int p, int swz,
+                                                               const float* __restrict__ sc = nullptr,
+                                                               const float* __restrict__ sh = nullptr) {
   const unsigned CG = (unsigned)C >> 3;
   const unsigned total = (unsigned)N * Ho * Wo * CG;
   for (unsigned idx = xcd_block_id(swz) * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
@@ -135,6 +139,11 @@ __global__ __launch_bounds__(256) void maxpool_k3s2_fwd_kernel(const void* __res
     const int h0 = oh * 2 - p, w0 = ow * 2 - p;
     float v[9][8];
     bool ok[9];
+    float bs[8], bh[8];
+    if constexpr (BNRELU) {
+      load8<kF32>(sc, cg * 8, bs);
+      load8<kF32>(sh, cg * 8, bh);
+    }
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
 #pragma unroll
@@ -144,6 +153,17 @@ __global__ __launch_bounds__(256) void maxpool_k3s2_fwd_kernel(const void* __res
         ok[q] = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
         if (ok[q]) {
           load8<XDT>(x, ((unsigned)(n * H + h) * W + (unsigned)w) * C + cg * 8, v[q]);
+        }
+      }
+    }
+    if constexpr (BNRELU) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        if (!ok[q]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = v[q][j] * bs[j] + bh[j];
+          v[q][j] = z > 0.f ? z : 0.f;
         }
       }
     }
@@ -228,6 +248,107 @@ __global__ __launch_bounds__(256) void maxpool_k3s2_bwd_kernel(const void* __res
   }
 }
 
+// Backward of maxpool_k3s2(relu(bn(y))) into the BatchNorm input, without materialising the
+// pool's input gradient: each lane gathers d(pool input) for one input pixel x 8 channels exactly
+// as maxpool_k3s2_bwd_kernel does, masks it with the ReLU (recomputed from y) and then
+//   PHASE 0: accumulates the BN backward sums (sum g, sum g*y) -> one [2][C] partial row per
+//            workgroup (the format of bn.hip's backward finalize);
+//   PHASE 1: writes dy = ca*g + cb*y + cc (coefficients from that finalize).
+// A lane's channel group is fixed across its grid-stride walk: 256 % CG == 0 and the stride is a
+// multiple of 256 (host-checked: C / 8 divides 256).
+template <int PHASE>
+__global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const void* __restrict__ dp, const uint64_t* __restrict__ arg,
+                                                          const void* __restrict__ y, const float* __restrict__ sc,
+                                                          const float* __restrict__ sh, const float* __restrict__ ca,
+                                                          const float* __restrict__ cb, const float* __restrict__ cc,
+                                                          void* __restrict__ dy, float* __restrict__ partial, int N,
+                                                          int H, int W, int C, int Ho, int Wo, int p) {
+  __shared__ float slab[256][17];  // PHASE 0: per-lane (8 sums, 8 sums) + pad
+  const unsigned CG = (unsigned)C >> 3;
+  const unsigned total = (unsigned)N * H * W * CG;
+  const unsigned cg = threadIdx.x % CG;
+  float bs[8], bh[8], s0[8], s1[8], k0[8], k1[8], k2[8];
+  load8<kF32>(sc, cg * 8, bs);
+  load8<kF32>(sh, cg * 8, bh);
+  if constexpr (PHASE == 1) {
+    load8<kF32>(ca, cg * 8, k0);
+    load8<kF32>(cb, cg * 8, k1);
+    load8<kF32>(cc, cg * 8, k2);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const unsigned pix = idx / CG;
+    const int w = (int)(pix % (unsigned)W);
+    const unsigned t = pix / (unsigned)W;
+    const int h = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
+    const int oh1 = (h + p) >> 1, ow1 = (w + p) >> 1;
+    uint64_t pk[4];
+    float g[4][8];
+    unsigned pos[4];
+    bool ok[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int oh = oh1 - 1 + i, ow = ow1 - 1 + j;
+        const int dh = h - (oh * 2 - p), dw = w - (ow * 2 - p);
+        const int q = i * 2 + j;
+        ok[q] = oh >= 0 && oh < Ho && ow >= 0 && ow < Wo && dh <= 2 && dw <= 2;
+        pos[q] = (unsigned)(dh * 3 + dw);
+        if (ok[q]) {
+          const unsigned oidx = ((unsigned)(n * Ho + oh) * Wo + ow) * CG + cg;
+          pk[q] = arg[oidx];
+          load8<kBF16>(dp, (int64_t)oidx * 8, g[q]);
+        }
+      }
+    }
+    float yv[8];
+    load8<kBF16>(y, (int64_t)idx * 8, yv);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ok[q]) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (((pk[q] >> (8 * j)) & 0xffu) == pos[q]) ? g[q][j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float z = yv[j] * bs[j] + bh[j];
+      acc[j] = z > 0.f ? acc[j] : 0.f;
+    }
+    if constexpr (PHASE == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s0[j] += acc[j];
+        s1[j] += acc[j] * yv[j];
+      }
+    } else {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = k0[j] * acc[j] + k1[j] * yv[j] + k2[j];
+      store8<kBF16>(dy, (int64_t)idx * 8, o);
+    }
+  }
+  if constexpr (PHASE == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      slab[threadIdx.x][j] = s0[j];
+      slab[threadIdx.x][8 + j] = s1[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+      const int which = c / C, ch = c % C, g8 = ch >> 3, e = ch & 7;
+      float a = 0.f;
+      for (int r = g8; r < 256; r += (int)CG) a += slab[r][which * 8 + e];
+      partial[(int64_t)blockIdx.x * 2 * C + c] = a;
+    }
+  }
+}
+
 }  // namespace madnn
 
 using namespace madnn;
@@ -286,6 +407,53 @@ hipError_t madnn_maxpool_bwd(const void* dy, const void* arg, void* dx, int N, i
     hipLaunchKernelGGL((maxpool_bwd_kernel<XDT>), dim3(grid), dim3(256), 0, stream, dy,
                        static_cast<const uint64_t*>(arg), dx, N, H, W, C, Ho, Wo, k, s, p);
   });
+  return hipGetLastError();
+}
+
+
+int madnn_pool_bn_supported(int64_t numel, int C) {
+  return numel < (1ll << 31) && C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0;
+}
+
+// maxpool_k3s2(relu(y * scale + shift)) (bf16 NHWC): output + 1-byte argmax per element
+hipError_t madnn_pool_bn_fwd(const void* x, const float* scale, const float* shift, void* y, void* arg, int N, int H,
+                             int W, int C, int Ho, int Wo, int p, hipStream_t stream) {
+  if (!madnn_pool_bn_supported((int64_t)N * H * W * C, C) || p > 2) return hipErrorInvalidValue;
+  const int64_t work = (int64_t)N * Ho * Wo * (C / 8);
+  const int grid = stream_grid(work, 256, 16 * kNumCU);
+  hipLaunchKernelGGL((maxpool_k3s2_fwd_kernel<kBF16, true>), dim3(grid), dim3(256), 0, stream, x, y,
+                     static_cast<uint64_t*>(arg), N, H, W, C, Ho, Wo, p, 0, scale, shift);
+  return hipGetLastError();
+}
+
+hipError_t madnn_bn_bwd_finalize(const float* partial, int G, int C, int pstride, int qoff, int64_t M, const float* w,
+                                 const float* mean, const float* invstd, float* dw, float* db, float* ca, float* cb,
+                                 float* cc, hipStream_t stream);
+
+// partial rows the fused backward's reduction writes
+int madnn_pool_bn_bwd_rows(int64_t pixels, int C) {
+  const int64_t work = pixels * (C / 8);
+  return stream_grid(work, 256, 8 * kNumCU);  // gather-latency-bound: 8 workgroups per CU in flight
+}
+
+// dy (and the BN weight/bias grads) from the pool output gradient dp: reduction, finalize, apply.
+// workspace: madnn_pool_bn_bwd_rows * 2 * C floats; coef: 3 * C floats.
+hipError_t madnn_pool_bn_bwd(const void* dp, const void* arg, const void* y, const float* w, const float* mean,
+                             const float* invstd, const float* scale, const float* shift, void* dy, float* dw,
+                             float* db, float* coef, float* workspace, int N, int H, int W, int C, int Ho, int Wo,
+                             int p, hipStream_t stream) {
+  if (!madnn_pool_bn_supported((int64_t)N * H * W * C, C) || p > 2) return hipErrorInvalidValue;
+  const int64_t pixels = (int64_t)N * H * W;
+  const int G = madnn_pool_bn_bwd_rows(pixels, C);
+  const uint64_t* a = static_cast<const uint64_t*>(arg);
+  hipLaunchKernelGGL((pool_bn_bwd_kernel<0>), dim3(G), dim3(256), 0, stream, dp, a, y, scale, shift, nullptr, nullptr,
+                     nullptr, nullptr, workspace, N, H, W, C, Ho, Wo, p);
+  MADNN_HIP_CHECK(hipGetLastError());
+  MADNN_HIP_CHECK(madnn_bn_bwd_finalize(workspace, G, C, 2 * C, C, pixels, w, mean, invstd, dw, db, coef, coef + C,
+                                        coef + 2 * C, stream));
+  const int grid = stream_grid(pixels * (C / 8), 256, 16 * kNumCU);
+  hipLaunchKernelGGL((pool_bn_bwd_kernel<1>), dim3(grid), dim3(256), 0, stream, dp, a, y, scale, shift, coef, coef + C,
+                     coef + 2 * C, dy, nullptr, N, H, W, C, Ho, Wo, p);
   return hipGetLastError();
 }
 

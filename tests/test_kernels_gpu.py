@@ -522,3 +522,44 @@ def test_resnet50_downsample_block_dual_bn_matches_composition(cuda):
         assert rel(p1.grad, p3.grad) <= 1.5 * rel(p2.grad, p3.grad) + 2e-3, n
     for (n, b1), b2 in zip(blk.named_buffers(), blk2.buffers()):
         torch.testing.assert_close(b1.float(), b2.float(), atol=1e-3, rtol=1e-3, msg=n)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 64, 17, 23), (2, 128, 9, 8), (2, 8, 6, 5)])
+@pytest.mark.parametrize("with_stats", [False, True])
+def test_bn_relu_maxpool_fused_matches_fp32(cuda, shape, with_stats):
+    """K7+K5 stem fusion: maxpool3x3/s2(relu(bn(y))) with the BN apply in the pool's loads and the
+    pool gradient gathered inside the BN backward vs fp32 eager: output, running stats, all grads."""
+    from madnn.nn.norm import FusedBatchNorm2d, FusedMaxPool2d
+
+    n, c, h, w = shape
+    torch.manual_seed(11)
+    y = (torch.randn(n, c, h, w, device=cuda) * 1.2 + 0.1).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.requires_grad_(True)
+    bn = FusedBatchNorm2d(c).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(-0.5, 1.5)   # negative scales too: max of the affine is not the affine of the max
+        bn.bias.normal_(0, 0.3)
+    pool = FusedMaxPool2d(3, 2, 1)
+    ref = torch.nn.BatchNorm2d(c).to(cuda)
+    ref.load_state_dict(bn.state_dict())
+    st = None
+    if with_stats:
+        v = y.detach().float().permute(0, 2, 3, 1).reshape(1, -1, c)
+        st = torch.stack([v.sum(1), (v * v).sum(1)], 1).contiguous()
+    assert ops.bn_relu_maxpool_supported(y, bn, pool)
+    out = ops.bn_relu_maxpool(y, bn, pool, st)
+    dp = torch.randn_like(out)
+    out.backward(dp)
+    yr = y.detach().float().requires_grad_(True)
+    outr = torch.nn.functional.max_pool2d(torch.relu(ref(yr)), 3, 2, 1)
+    outr.backward(dp.float())
+    torch.testing.assert_close(out.float(), outr, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+    # bf16 rounding of relu(bn(y)) can move an argmax between near-equal window values, so the
+    # input gradient is compared in norm; the parameter gradients (sums) element-wise
+    rel = ((y.grad.float() - yr.grad).norm() / yr.grad.norm()).item()
+    assert rel < 0.05, rel
+    torch.testing.assert_close(bn.weight.grad, ref.weight.grad, atol=0.2, rtol=0.05)
+    torch.testing.assert_close(bn.bias.grad, ref.bias.grad, atol=0.2, rtol=0.05)
