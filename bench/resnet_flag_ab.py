@@ -20,7 +20,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--flag", default="madnn.models.resnet:_DUAL_BN", help="module:attribute (bool)")
+    ap.add_argument("--flag", default="madnn.models.resnet:_DUAL_BN", help="module:attribute")
+    ap.add_argument("--on", default="true", help="value of the 'on' arm (true/false/int/string)")
+    ap.add_argument("--off", default="false", help="value of the 'off' arm")
     ap.add_argument("--batch", type=int, default=1536)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
@@ -30,6 +32,10 @@ def main():
     from madnn.models import resnet50
     from madnn.optim import FusedSGD
 
+    def val(v):
+        return {"true": True, "false": False}.get(v.lower(), int(v) if v.lstrip("-").isdigit() else v)
+
+    arm_val = {True: val(a.on), False: val(a.off)}
     mod_name, attr = a.flag.split(":")
     mod = importlib.import_module(mod_name)
     madnn.init()
@@ -40,7 +46,7 @@ def main():
     x, y = madnn.data.synthetic_batch("image", a.batch, madnn.device(), dtype=torch.bfloat16, channels_last=True)
 
     def window(on, n):
-        setattr(mod, attr, on)
+        setattr(mod, attr, arm_val[on])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(n):
@@ -55,7 +61,7 @@ def main():
     for w in range(a.windows):
         for on in ((True, False) if w % 2 == 0 else (False, True)):
             res[on].append(window(on, a.steps))
-    out = {"flag": a.flag, "batch": a.batch, "windows": a.windows, "steps": a.steps,
+    out = {"flag": a.flag, "on": a.on, "off": a.off, "batch": a.batch, "windows": a.windows, "steps": a.steps,
            "on_ms": statistics.median(res[True]), "off_ms": statistics.median(res[False]),
            "on_all": res[True], "off_all": res[False]}
     out["on_img_s"] = a.batch / out["on_ms"] * 1e3

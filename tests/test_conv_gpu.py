@@ -165,7 +165,7 @@ def test_conv1x1_fork_accumulates_residual_grad(cuda, cin, cout):
 @pytest.mark.parametrize("shape", [(2, 64, 256, 7, 7), (3, 128, 64, 5, 9), (1, 512, 2048, 3, 3),
                                    (2, 192, 320, 11, 13)])
 @pytest.mark.parametrize("with_stats", [False, True])
-def test_bn_relu_conv1x1_prologue_matches_fp32(cuda, shape, with_stats):
+def test_bn_relu_conv1x1_prologue_matches_fp32(cuda, shape, with_stats, monkeypatch):
     """K9 BatchNorm prologue: conv1x1(relu(bn(y))) with bn's apply inside the operand load vs
     fp32 eager BN + ReLU + conv: output, output statistics, running stats and every gradient."""
     from madnn.nn.norm import FusedBatchNorm2d
@@ -186,6 +186,7 @@ def test_bn_relu_conv1x1_prologue_matches_fp32(cuda, shape, with_stats):
     if with_stats:
         v = y.detach().float().permute(0, 2, 3, 1).reshape(1, -1, cin)
         st = torch.stack([v.sum(1), (v * v).sum(1)], 1).contiguous()
+    monkeypatch.setattr(ops, "_BN_PROLOGUE", True)   # opt-in path (off by default: docs/PERF.md)
     assert ops.bn_relu_conv1x1_supported(y, bn, wt)
     out, part = ops.bn_relu_conv1x1(y, bn, wt, stats_in=st, stats=True)
     dout = _rand(tuple(out.shape), cuda)
@@ -208,7 +209,7 @@ def test_bn_relu_conv1x1_prologue_matches_fp32(cuda, shape, with_stats):
     _close(bn.bias.grad, ref.bias.grad, 6e-2)
 
 
-def test_bottleneck_bn_prologue_matches_unfused(cuda):
+def test_bottleneck_bn_prologue_matches_unfused(cuda, monkeypatch):
     """A ResNet-50 bottleneck with bn2 fused into conv3's prologue vs the same block unfused."""
     import copy
 
@@ -222,6 +223,7 @@ def test_bottleneck_bn_prologue_matches_unfused(cuda):
             m.float()
             torch.nn.init.uniform_(m.weight, 0.5, 1.5)
     blk2 = copy.deepcopy(blk)
+    monkeypatch.setattr(O, "_BN_PROLOGUE", True)
     x = _rand((4, 256, 14, 14), cuda)
     x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
     y1 = blk(x1)
