@@ -90,3 +90,23 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     assert res["n_gpus"] == 4 and res["scaling"] == "weak" and res["value"] > 0
     assert res["config"]["parallelism"] == "pp4" and res["config"]["global_batch"] == 4
     assert res["gpt2_pp"]["microbatches"] == 4 and res["gpt2_pp"]["model"] == "gpt2-medium"
+
+
+def test_bench_py_gpt2_dp2_pp4_interleaved_eight_ranks_cpu():
+    """The 8-GPU layout of the GPT-2 half exactly as the driver's N=8 run builds it: GPT-2 medium,
+    dp2 x pp4, interleaved 1F1B with 2 model chunks per rank (short sequences, CPU/gloo)."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "1",
+           "--device", "cpu", "--model", "gpt2-medium", "--gpt2-batch-per-gpu", "2", "--gpt2-mb", "1",
+           "--seq-len", "16"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    pp = res["gpt2_pp"]
+    assert res["n_gpus"] == 8 and res["value"] > 0
+    assert res["config"]["parallelism"] == "dp2xpp4"
+    assert pp["schedule"] == "interleaved" and pp["virtual_stages"] == 2 and pp["microbatches"] == 8
