@@ -116,6 +116,11 @@ def select(t: torch.Tensor, op: str, group=None) -> Selected:
     if kind == "cpu" and be == "nccl":
         raise RuntimeError("CPU tensor on an RCCL group: use a gloo group for host tensors")
     transport = "rccl" if be == "nccl" else ("gloo-host" if kind == "gpu" else "gloo")
+    if op == "all_reduce" and kind == "gpu":
+        from .oneshot import lookup
+
+        if lookup(t, group) is not None:
+            transport = "xgmi-oneshot"   # K5: small sums over P2P-mapped peer buffers
     if fn is None:
         from .. import runtime as rt
 
@@ -139,6 +144,13 @@ def all_reduce(t: torch.Tensor, op: str = "sum", group=None, async_op: bool = Fa
     if _local(group):
         return None
     _record("all_reduce", group, t)
+    if op == "sum" and not async_op and t.device.type == "cuda":
+        from .oneshot import lookup
+
+        c = lookup(t, group)   # K5 one-shot (MADNN_ONESHOT=1, registered via oneshot.enable_for)
+        if c is not None:
+            c(t)
+            return None
     rop = {"sum": dist.ReduceOp.SUM, "avg": dist.ReduceOp.AVG, "max": dist.ReduceOp.MAX}[op]
     if rop == dist.ReduceOp.AVG and dist.get_backend(group) == "gloo":
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=False)
