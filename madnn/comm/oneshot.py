@@ -118,8 +118,8 @@ def enable_for(group=None, cap_bytes: int = 1 << 20) -> Optional[OneShotAllReduc
     """Register a one-shot communicator for ``group``: with ``MADNN_ONESHOT=1``,
     :func:`madnn.comm.all_reduce` sends sum all-reduces of HIP tensors up to ``cap_bytes`` through
     it (collective: every rank of the group must call this)."""
-    if not (dist.is_initialized() and torch.cuda.is_available() and dist.get_backend(group) == "nccl"):
-        return None
+    if not (dist.is_initialized() and torch.cuda.is_available()):
+        return None   # (any backend: the group only carries the one-time IPC handle exchange)
     c = OneShotAllReduce(group, cap_bytes=cap_bytes)
     _registry[_key(group)] = c
     return c

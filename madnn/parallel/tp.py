@@ -23,6 +23,8 @@ this, A-15; in madnn the TP group is a sub-group of the mesh).
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Optional
 
@@ -403,6 +405,11 @@ def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
             comm.broadcast(p.data, src=0)
     old = {id(p) for p in model.parameters()}
     n = shard_linears(model, groups.tp_group, int(cfg.extra.get("tp_min_params", 1 << 20)))
+    if os.environ.get("MADNN_ONESHOT", "0") == "1" and dev.type == "cuda" and tp > 1:
+        # K5: the row-parallel activation sums (small, latency-bound) over IPC-mapped peer buffers
+        from ..comm import oneshot
+
+        oneshot.enable_for(groups.tp_group, cap_bytes=int(cfg.extra.get("oneshot_cap", 4 << 20)))
     params = [p for p in model.parameters() if p.requires_grad]
     if optimizer is not None:
         keep = {id(q) for q in params}

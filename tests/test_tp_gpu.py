@@ -12,8 +12,13 @@ from dist_utils import run_dist
 pytestmark = pytest.mark.gpu
 
 
-def _w_tp_gpu(rank, world):
+def _w_tp_gpu(rank, world, oneshot=False):
+    import os
+
     import madnn
+    from madnn.comm import oneshot as k5
+
+    os.environ["MADNN_ONESHOT"] = "1" if oneshot else "0"
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.nn import ColumnParallelLinear, RowParallelLinear
     from madnn.optim import FusedAdam
@@ -24,6 +29,10 @@ def _w_tp_gpu(rank, world):
     opt = FusedAdam(m.parameters(), lr=1e-3)
     ropt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=0.0)
     eng, opt = madnn.distribute(m, opt, strategy="tp", tp_size=2, tp_min_params=4096, dtype="float32")
+    from madnn import comm
+    probe = torch.zeros(4 * 64 * 256, device="cuda")
+    sel = comm.select(probe, "all_reduce", mlp_group := eng.h[0].mlp.c_proj.group)
+    assert (sel.transport == "xgmi-oneshot") == oneshot, sel
     mlp = eng.h[0].mlp
     assert isinstance(mlp.c_fc, ColumnParallelLinear) and isinstance(mlp.c_proj, RowParallelLinear)
     assert mlp.c_fc.weight.is_cuda and mlp.c_fc.weight.shape[0] == 512
@@ -41,3 +50,8 @@ def _w_tp_gpu(rank, world):
 
 def test_tp2_gpt_on_device(cuda):
     run_dist(_w_tp_gpu, 2, device="cuda", backend="gloo")
+
+
+def test_tp2_gpt_on_device_oneshot_allreduce(cuda):
+    """The same TP parity with the row-parallel activation sums on the K5 one-shot all-reduce."""
+    run_dist(_w_tp_gpu, 2, True, device="cuda", backend="gloo")
