@@ -8,9 +8,10 @@ Default (the driver's contract) measures BOTH halves of the metric in one run:
 * the primary ``value``: ResNet-50, automatic data parallelism
   (``madnn.distribute``), bf16 compute with fp32 master weights and fp32 BatchNorm,
   channels_last, FusedSGD (momentum 0.9, wd 5e-5) on the hand-written gfx950 kernel,
-  bucketed RCCL all-reduce overlapped with backward; 1536 images per GPU (weak scaling, 60 GB
+  bucketed RCCL all-reduce overlapped with backward; 2048 images per GPU (weak scaling, 80 GB
   of the 288 GB HBM; same-box A/Bs: 10.80k img/s at 512 vs 11.37k at 1024,
-  profiles/r2_resnet_b1024.md; 11.38k at 1024 vs 11.59k at 1536, profiles/r2_resnet_b1536.md);
+  profiles/r2_resnet_b1024.md; 11.38k at 1024 vs 11.59k at 1536, profiles/r2_resnet_b1536.md;
+  12.65k at 1536 vs 12.85k at 2048, profiles/r2_resnet_b2048.md);
 * ``gpt2_pp``: GPT-2 medium (seq 1024, bf16, FusedAdam), pipeline parallel over
   RCCL P2P with the interleaved 1F1B schedule (2 model chunks per rank) -- ``pp2`` at 2
   GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1 GPU (a pipeline needs two
@@ -97,10 +98,11 @@ def bench_resnet(args, world, rank):
     from madnn.models import resnet50
     from madnn.optim import FusedSGD
 
-    # 1536 images per GPU: sized for 288 GB HBM3E (60 GB peak), and large enough that the
+    # 2048 images per GPU: sized for 288 GB HBM3E (80 GB peak), and large enough that the
     # per-step fixed costs (kernel boundaries, MIOpen workspace memsets, the optimizer pass) are
-    # amortised; the shipped find-db holds the tuned solvers for this shape (and for 512 / 1024)
-    per_gpu = args.batch or 1536
+    # amortised (same box: 12650 img/s at 1536 -> 12850 at 2048, profiles/r2_resnet_b2048.md); the
+    # shipped find-db holds the tuned solvers for this shape (and for 512 / 1024 / 1536)
+    per_gpu = args.batch or 2048
     torch.manual_seed(0)
     model = resnet50()
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)

@@ -37,7 +37,20 @@ def main():
 
     arm_val = {True: val(a.on), False: val(a.off)}
     mod_name, attr = a.flag.split(":")
-    mod = importlib.import_module(mod_name)
+    if mod_name == "bn_tune":   # a native BN tunable (madnn_bn_tune key), e.g. bn_tune:2
+        import ctypes
+
+        madnn_mod = importlib.import_module("madnn.ops")
+        madnn_mod.load_kernels()
+        tune = ctypes.CDLL(str(madnn_mod.kernels_path())).madnn_bn_tune
+
+        class _Native:
+            def __setattr__(self, k, v):
+                tune(int(k), int(v))
+
+        mod = _Native()
+    else:
+        mod = importlib.import_module(mod_name)
     madnn.init()
     torch.manual_seed(0)
     m = resnet50()

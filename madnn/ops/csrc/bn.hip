@@ -43,14 +43,19 @@ struct BnGeom {
 //    every workgroup is resident at once, so the whole grid walks the tensor as one front;
 //    above 8 the later workgroups only start when the first ones finish, which splits each
 //    pass into several interleaved sweeps and spoils the reuse order.
+//  hoist: load each lane's per-channel coefficients once per walk when its channels never change
+//    (grid stride a multiple of C); 0 reloads them per chunk (A/B)
 struct BnTune {
   int reverse = 1;
   int wg_per_cu = 8;
+  int hoist = 1;
 };
 inline BnTune& bn_tune() {
   static BnTune t;
   return t;
 }
+// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting
+inline int bn_walk_flags() { return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2); }
 
 // grid-stride walk of [0, total) in 8-element lane chunks, forward or back-to-front; c0 tracks
 // the channel of the chunk without a 64-bit modulo per step
@@ -229,19 +234,29 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
                                                        int reverse, const float* __restrict__ rscale = nullptr,
                                                        const float* __restrict__ rshift = nullptr) {
   static_assert(!RAFF || RES, "a residual BatchNorm needs the residual");
-  for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
-    const int64_t i = w.i;
-    const int c0 = w.c0;
-    float v[8], sc[8], sh[8];
-    load8<XDT>(x, i, v);
+  StripeWalk w(total, C, (reverse & 1) != 0);
+  // When the grid stride is a multiple of C (always, for C dividing 256 x 8), every lane keeps its
+  // channels for the whole walk: the coefficients are loaded once instead of per chunk (they were
+  // 4x the data bytes in vector-memory requests)
+  const bool fixed = (reverse & 2) == 0 && (w.dc == 0 || w.dc == C);
+  float sc[8], sh[8], rs[8], rh[8];
+  auto coef = [&](int c0) {
     load8<kF32>(scale, c0, sc);
     load8<kF32>(shift, c0, sh);
+    if constexpr (RAFF) {
+      load8<kF32>(rscale, c0, rs);
+      load8<kF32>(rshift, c0, rh);
+    }
+  };
+  if (fixed && w.n > 0) coef(w.c0);
+  for (; w.n > 0; w.next()) {
+    const int64_t i = w.i;
+    if (!fixed) coef(w.c0);
+    float v[8];
+    load8<XDT>(x, i, v);
     float r[8];
     if constexpr (RES) load8<XDT>(res, i, r);
     if constexpr (RAFF) {
-      float rs[8], rh[8];
-      load8<kF32>(rscale, c0, rs);
-      load8<kF32>(rshift, c0, rh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) r[j] = r[j] * rs[j] + rh[j];
     }
@@ -423,25 +438,37 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float* __restrict__ rca = nullptr, const float* __restrict__ rcb = nullptr,
     const float* __restrict__ rcc = nullptr) {
   static_assert(!RAFF || (RELU && RES), "a residual BatchNorm comes with the fused residual + ReLU mask");
-  for (StripeWalk w(total, C, reverse != 0); w.n > 0; w.next()) {
+  StripeWalk w(total, C, (reverse & 1) != 0);
+  const bool fixed = (reverse & 2) == 0 && (w.dc == 0 || w.dc == C);  // channels invariant across the walk (see bn_apply_kernel)
+  float a[8], b[8], c[8], sc[8], sh[8], ra[8], rb[8], rc[8];
+  auto coef = [&](int c0) {
+    load8<kF32>(ca, c0, a);
+    load8<kF32>(cb, c0, b);
+    load8<kF32>(cc, c0, c);
+    if constexpr (RELU && !RES) {
+      load8<kF32>(scale, c0, sc);
+      load8<kF32>(shift, c0, sh);
+    }
+    if constexpr (RAFF) {
+      load8<kF32>(rca, c0, ra);
+      load8<kF32>(rcb, c0, rb);
+      load8<kF32>(rcc, c0, rc);
+    }
+  };
+  if (fixed && w.n > 0) coef(w.c0);
+  for (; w.n > 0; w.next()) {
     const int64_t i = w.i;
-    const int c0 = w.c0;
-    float dv[8], xv[8], a[8], b[8], c[8];
+    if (!fixed) coef(w.c0);
+    float dv[8], xv[8];
     load8<XDT>(dy, i, dv);
     load8<XDT>(x, i, xv);
     float rv[8];
     if constexpr (RAFF) load8<XDT>(rin, i, rv);
-    load8<kF32>(ca, c0, a);
-    load8<kF32>(cb, c0, b);
-    load8<kF32>(cc, c0, c);
     if constexpr (RELU && RES) {
       const unsigned bits = mask[i >> 3];
 #pragma unroll
       for (int j = 0; j < 8; ++j) dv[j] = ((bits >> j) & 1u) ? dv[j] : 0.f;
     } else if constexpr (RELU) {
-      float sc[8], sh[8];
-      load8<kF32>(scale, c0, sc);
-      load8<kF32>(shift, c0, sh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float z = xv[j] * sc[j] + sh[j];
@@ -453,11 +480,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     for (int j = 0; j < 8; ++j) o[j] = a[j] * dv[j] + b[j] * xv[j] + c[j];
     store8<XDT>(dx, i, o);
     if constexpr (RAFF) {
-      load8<kF32>(rca, c0, a);
-      load8<kF32>(rcb, c0, b);
-      load8<kF32>(rcc, c0, c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = a[j] * dv[j] + b[j] * rv[j] + c[j];
+      for (int j = 0; j < 8; ++j) o[j] = ra[j] * dv[j] + rb[j] * rv[j] + rc[j];
       store8<XDT>(dres, i, o);
     } else if constexpr (RES) {
       store8<XDT>(dres, i, dv);
@@ -481,10 +505,14 @@ static int bn_grid_rows(int64_t M, int C) {
 
 extern "C" {
 
-// key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU; value < 0 only reads.
+// key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU, 2: coefficient hoisting
+// (0/1); value < 0 only reads.
 // Returns the old value (-1 for an unknown key).
 int madnn_bn_tune(int key, int value) {
-  int* f = key == 0 ? &madnn::bn_tune().reverse : key == 1 ? &madnn::bn_tune().wg_per_cu : nullptr;
+  int* f = key == 0   ? &madnn::bn_tune().reverse
+           : key == 1 ? &madnn::bn_tune().wg_per_cu
+           : key == 2 ? &madnn::bn_tune().hoist
+                      : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
   if (value >= 0) *f = key == 1 ? (value < 1 ? 1 : value) : (value != 0);
@@ -531,7 +559,7 @@ hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, unsigned char* 
   const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, res != nullptr, RELU, RES, {
     hipLaunchKernelGGL((bn_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, x, res, scale, shift, y,
-                       mask, total, C, bn_tune().reverse);
+                       mask, total, C, bn_walk_flags());
   }));
   return hipGetLastError();
 }
@@ -562,7 +590,7 @@ hipError_t madnn_bn_bwd(const void* dy, const void* x, const unsigned char* mask
   const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   MADNN_DISPATCH_DT(xdt, XDT, MADNN_BN_VARIANT(relu, has_res, RELU, RES, {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<XDT, RELU, RES>), dim3(grid), dim3(256), 0, stream, dy, x, mask, scale,
-                       shift, ca, cb, cc, dx, dres, total, C, bn_tune().reverse);
+                       shift, ca, cb, cc, dx, dres, total, C, bn_walk_flags());
   }));
   return hipGetLastError();
 }
@@ -615,7 +643,7 @@ hipError_t madnn_bn_fwd_dual(const void* x, const void* r, void* y, unsigned cha
   const int64_t total = M * C;
   const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   hipLaunchKernelGGL((bn_apply_kernel<kBF16, true, true, true>), dim3(grid), dim3(256), 0, stream, x, r, scale, shift,
-                     y, mask, total, C, bn_tune().reverse, scale_r, shift_r);
+                     y, mask, total, C, bn_walk_flags(), scale_r, shift_r);
   return hipGetLastError();
 }
 
@@ -645,7 +673,7 @@ hipError_t madnn_bn_bwd_dual(const void* dy, const void* x, const void* r, const
   const int64_t total = M * C;
   const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, true, true, true>), dim3(grid), dim3(256), 0, stream, dy, x, mask,
-                     nullptr, nullptr, coef, coef + C, coef + 2 * C, dx, dr, total, C, bn_tune().reverse, r,
+                     nullptr, nullptr, coef, coef + C, coef + 2 * C, dx, dr, total, C, bn_walk_flags(), r,
                      coef + 3 * C, coef + 4 * C, coef + 5 * C);
   return hipGetLastError();
 }
