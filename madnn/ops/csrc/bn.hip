@@ -49,13 +49,16 @@ struct BnTune {
   int reverse = 1;
   int wg_per_cu = 8;
   int hoist = 1;
+  int unroll = 0;  // 1: apply walks handle two chunks per trip (more loads in flight)
 };
 inline BnTune& bn_tune() {
   static BnTune t;
   return t;
 }
-// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting
-inline int bn_walk_flags() { return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2); }
+// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting, bit 2 unroll
+inline int bn_walk_flags() {
+  return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2) | (bn_tune().unroll ? 4 : 0);
+}
 
 // grid-stride walk of [0, total) in 8-element lane chunks, forward or back-to-front; c0 tracks
 // the channel of the chunk without a 64-bit modulo per step
@@ -249,13 +252,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
     }
   };
   if (fixed && w.n > 0) coef(w.c0);
-  for (; w.n > 0; w.next()) {
-    const int64_t i = w.i;
-    if (!fixed) coef(w.c0);
-    float v[8];
-    load8<XDT>(x, i, v);
-    float r[8];
-    if constexpr (RES) load8<XDT>(res, i, r);
+  auto body = [&](int64_t i, float (&v)[8], float (&r)[8]) {
     if constexpr (RAFF) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) r[j] = r[j] * rs[j] + rh[j];
@@ -275,6 +272,31 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
     if constexpr (RELU && RES) {
       if (mask) mask[i >> 3] = (unsigned char)bits;
     }
+  };
+  if (fixed && (reverse & 4)) {  // two chunks per trip: both chunks' loads issued before either store
+    while (w.n >= 2) {
+      const int64_t i0 = w.i;
+      w.next();
+      const int64_t i1 = w.i;
+      w.next();
+      float v0[8], v1[8], r0[8], r1[8];
+      load8<XDT>(x, i0, v0);
+      load8<XDT>(x, i1, v1);
+      if constexpr (RES) {
+        load8<XDT>(res, i0, r0);
+        load8<XDT>(res, i1, r1);
+      }
+      body(i0, v0, r0);
+      body(i1, v1, r1);
+    }
+  }
+  for (; w.n > 0; w.next()) {
+    const int64_t i = w.i;
+    if (!fixed) coef(w.c0);
+    float v[8], r[8];
+    load8<XDT>(x, i, v);
+    if constexpr (RES) load8<XDT>(res, i, r);
+    body(i, v, r);
   }
 }
 
@@ -456,14 +478,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     }
   };
   if (fixed && w.n > 0) coef(w.c0);
-  for (; w.n > 0; w.next()) {
-    const int64_t i = w.i;
-    if (!fixed) coef(w.c0);
-    float dv[8], xv[8];
-    load8<XDT>(dy, i, dv);
-    load8<XDT>(x, i, xv);
-    float rv[8];
-    if constexpr (RAFF) load8<XDT>(rin, i, rv);
+  auto body = [&](int64_t i, float (&dv)[8], const float (&xv)[8], const float (&rv)[8]) {
     if constexpr (RELU && RES) {
       const unsigned bits = mask[i >> 3];
 #pragma unroll
@@ -486,6 +501,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     } else if constexpr (RES) {
       store8<XDT>(dres, i, dv);
     }
+  };
+  if (fixed && (reverse & 4)) {  // two chunks per trip (see bn_apply_kernel)
+    while (w.n >= 2) {
+      const int64_t i0 = w.i;
+      w.next();
+      const int64_t i1 = w.i;
+      w.next();
+      float d0[8], d1[8], x0[8], x1[8], q0[8], q1[8];
+      load8<XDT>(dy, i0, d0);
+      load8<XDT>(dy, i1, d1);
+      load8<XDT>(x, i0, x0);
+      load8<XDT>(x, i1, x1);
+      if constexpr (RAFF) {
+        load8<XDT>(rin, i0, q0);
+        load8<XDT>(rin, i1, q1);
+      }
+      body(i0, d0, x0, q0);
+      body(i1, d1, x1, q1);
+    }
+  }
+  for (; w.n > 0; w.next()) {
+    const int64_t i = w.i;
+    if (!fixed) coef(w.c0);
+    float dv[8], xv[8], rv[8];
+    load8<XDT>(dy, i, dv);
+    load8<XDT>(x, i, xv);
+    if constexpr (RAFF) load8<XDT>(rin, i, rv);
+    body(i, dv, xv, rv);
   }
 }
 
@@ -512,6 +555,7 @@ int madnn_bn_tune(int key, int value) {
   int* f = key == 0   ? &madnn::bn_tune().reverse
            : key == 1 ? &madnn::bn_tune().wg_per_cu
            : key == 2 ? &madnn::bn_tune().hoist
+           : key == 3 ? &madnn::bn_tune().unroll
                       : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;

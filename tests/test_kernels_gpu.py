@@ -563,3 +563,45 @@ def test_bn_relu_maxpool_fused_matches_fp32(cuda, shape, with_stats):
     assert rel < 0.05, rel
     torch.testing.assert_close(bn.weight.grad, ref.weight.grad, atol=0.2, rtol=0.05)
     torch.testing.assert_close(bn.bias.grad, ref.bias.grad, atol=0.2, rtol=0.05)
+
+
+def test_batchnorm_apply_walk_variants_bitwise(cuda):
+    """The BN apply walks (coefficient hoisting on/off, one or two chunks per trip) are pure
+    scheduling changes: outputs and gradients must be bitwise identical across them."""
+    import ctypes
+
+    from madnn.nn.norm import FusedBatchNorm2d
+
+    tune = ctypes.CDLL(str(ops.kernels_path())).madnn_bn_tune
+    torch.manual_seed(12)
+    C = 256
+    x = torch.randn(16, C, 56, 56, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x)
+    dy = torch.randn_like(x)
+    bn, bn_r = FusedBatchNorm2d(C).to(cuda), FusedBatchNorm2d(C).to(cuda)
+    outs = []
+    old = (tune(2, -1), tune(3, -1))
+    try:
+        for hoist, unroll in ((0, 0), (1, 0), (1, 1)):
+            tune(2, hoist)
+            tune(3, unroll)
+            res = []
+            for dual in (False, True):
+                xa, ra = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+                y = ops.batch_norm_add_bn_relu(xa, ra, bn, bn_r) if dual else \
+                    ops.batch_norm_act(xa, bn.weight, bn.bias, None, None, training=True, relu=True, residual=ra)
+                y.backward(dy)
+                res += [y.detach(), xa.grad, ra.grad]
+            outs.append(res)
+    finally:
+        tune(2, old[0])
+        tune(3, old[1])
+    # hoisting is bitwise neutral; the two-chunk walk lets the compiler contract the backward's
+    # a*g + b*x + c differently, so its gradients may differ in the last bf16 place
+    bad = [(v, k, (a.float() - b.float()).abs().max().item())
+           for v, other in enumerate(outs[1:], 1) for k, (a, b) in enumerate(zip(outs[0], other))
+           if not torch.equal(a, b)]
+    assert all(v == 2 and k in (1, 2, 4, 5) for v, k, _ in bad), bad
+    for v, k, d in bad:
+        ref = outs[0][k].float().abs().max().item()
+        assert d <= 2 ** -7 * max(ref, 1.0), (v, k, d, ref)
