@@ -26,8 +26,8 @@ from torch import nn
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
-from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_supported, bn_relu_maxpool,
-                   bn_relu_maxpool_supported)
+from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_supported, bn_relu_conv3x3,
+                   bn_relu_conv3x3_supported, bn_relu_maxpool, bn_relu_maxpool_supported)
 
 # A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
 _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
@@ -88,18 +88,25 @@ class Bottleneck(nn.Module):
                 # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's
                 # passes (forward and backward), its normalised output never written to HBM
                 yd, std = self.downsample[0](xf, stats=True)
-                out = self.bn1(y, relu=True, stats=st)
-                y, st = self.conv2(out, stats=True)
+                y, st = self._bn1_conv2(y, st)
                 y, st = self._bn2_conv3(y, st)
                 return batch_norm_add_bn_relu(y, yd, self.bn3, self.downsample[1], st, std)
             idt = self.downsample(xf)
         else:
             idt = self.downsample(x)
             y, st = self.conv1(x, stats=True)
-        out = self.bn1(y, relu=True, stats=st)
-        y, st = self.conv2(out, stats=True)   # K13 at stride 1: BN statistics from the epilogue
+        y, st = self._bn1_conv2(y, st)   # K13 at stride 1: BN statistics from the epilogue
         y, st = self._bn2_conv3(y, st)
         return self.bn3(y, residual=idt, relu=True, stats=st)   # relu(bn3 + idt): one kernel
+
+    def _bn1_conv2(self, y, st):
+        """conv2(relu(bn1(y))): with conv2 on K13, bn1's backward reduction is taken in conv2's
+        data-grad epilogue (ops.bn_relu_conv3x3); the stride-2 conv2s stay on the module path."""
+        if isinstance(self.bn1, BN) and isinstance(self.conv2, FusedConv2d) and self.conv2._k13(y) \
+                and bn_relu_conv3x3_supported(y, self.bn1, self.conv2.weight):
+            return bn_relu_conv3x3(y, self.bn1, self.conv2.weight, stats_in=st, stats=True)
+        out = self.bn1(y, relu=True, stats=st)
+        return self.conv2(out, stats=True)
 
     def _bn2_conv3(self, y, st):
         """conv3(relu(bn2(y))): on K9 the bn2 apply + ReLU run in conv3's operand prologue

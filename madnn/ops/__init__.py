@@ -788,6 +788,68 @@ class _Conv3x3Fn(torch.autograd.Function):
         return dx, dw, None
 
 
+class _BNReluConv3x3Fn(torch.autograd.Function):
+    """``conv3x3(relu(bn(y)), w)`` in training (ResNet's bn1 -> conv2).  Forward: the K5 BN apply
+    (statistics from y's producer) and K13 with the output statistics.  Backward: K13's data grad
+    also takes bn's backward sums over (d relu(bn(y)), y) in its epilogue, so the BN backward is
+    finalize + apply only -- its reduction pass over two activation-sized tensors disappears."""
+
+    @staticmethod
+    def forward(ctx, y, w, bn_w, bn_b, bn, stats_in, want_stats):
+        a, mean, invstd, scale, shift, _ = torch.ops.madnn.bn_fwd(y, None, bn_w, bn_b, bn.running_mean,
+                                                                  bn.running_var, bn.num_batches_tracked, True,
+                                                                  float(bn.momentum), float(bn.eps), True, stats_in)
+        out, part = torch.ops.madnn.conv3x3_fwd(a, _cl(w), bool(want_stats))
+        ctx.save_for_backward(y, a, w, bn_w, mean, invstd, scale, shift)
+        ctx.mark_non_differentiable(part)
+        return out, part
+
+    @staticmethod
+    def backward(ctx, dout, _dpart):
+        y, a, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        dout = _nhwc(dout.to(y.dtype))
+        wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        da, part = torch.ops.madnn.conv3x3_fwd_bnb(dout, wt, y, scale, shift)
+        if _K13_WGRAD == "k13" or (_K13_WGRAD == "auto" and a.size(3) >= 48):
+            dw = torch.ops.madnn.conv3x3_wgrad(dout, a, w.dtype == torch.bfloat16)
+        else:
+            dw = torch.ops.aten.convolution_backward(dout, a, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                                                     (False, True, False))[1]
+        if dw.stride() != w.stride() or dw.dtype != w.dtype:
+            dw = torch.empty_like(w).copy_(dw)
+        dy, dbw, dbb = torch.ops.madnn.bn_bwd_ext(da, y, bn_w, mean, invstd, scale, shift, part, True)
+        need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
+
+
+def bn_relu_conv3x3_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
+    """Whether :func:`bn_relu_conv3x3` runs fused: training-mode BN with running statistics and an
+    fp32 affine in front of a K13-shaped convolution whose data grad runs on K13."""
+    return (_BN_DGRAD_EPI and isinstance(y, torch.Tensor) and _K13_DGRAD == "k13" and bn.training
+            and bn.track_running_stats and bn.affine and bn.momentum is not None
+            and bn.weight.dtype == torch.float32 and conv3x3_supported(y, w) and y.size(1) == w.size(1)
+            and bn_supported(y, bn.weight))
+
+
+def bn_relu_conv3x3(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[torch.Tensor] = None,
+                    stats: bool = False):
+    """``conv3x3(relu(bn(y)), w)`` with bn's backward reduction taken in K13's data-grad epilogue
+    (:class:`_BNReluConv3x3Fn`); composition of the two modules' paths otherwise."""
+    if bn_relu_conv3x3_supported(y, bn, w):
+        _need_native("bn_relu_conv3x3")
+        out, part = _BNReluConv3x3Fn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
+        return (out, part if part.numel() else None) if stats else out
+    a = bn(y, relu=True, stats=stats_in) if _is_fused_bn(bn) else torch.relu(bn(y))
+    if conv3x3_supported(a, w):
+        return conv3x3(a, w, stats=stats)
+    out = torch.nn.functional.conv2d(a, w, padding=1)
+    return (out, None) if stats else out
+
+
+# A/B knob: bn1's backward reduction in conv2's (K13) data-grad epilogue (1) or its own pass (0)
+_BN_DGRAD_EPI = os.environ.get("MADNN_BN_DGRAD_EPI", "1") != "0"
+
+
 def conv3x3(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False):
     """``conv2d(x, w, stride=1, padding=1)`` of an NHWC bf16 HIP tensor on K13 (see
     :func:`conv3x3_supported`).  ``stats``: also return per-tile channel (sum, sum of squares)
@@ -866,7 +928,7 @@ __all__ = [
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
     "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "batch_norm_add_bn_relu",
     "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "bn_relu_maxpool",
-    "bn_relu_maxpool_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "bn_relu_maxpool_supported", "bn_relu_conv3x3", "bn_relu_conv3x3_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

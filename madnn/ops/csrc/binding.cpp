@@ -87,6 +87,12 @@ int madnn_conv3x3_supported(int, int, int, int);
 int madnn_conv3x3_stat_rows(int64_t);
 hipError_t madnn_conv3x3_fwd(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
 int64_t madnn_conv3x3_wgrad_ws(int, int, int, int, int);
+hipError_t madnn_conv3x3_fwd_bnb(const void*, const void*, void*, float*, const void*, const float*, const float*, int,
+                                 int, int, int, int, hipStream_t);
+hipError_t madnn_bn_bwd_ext(const void*, const void*, void*, int64_t, int, int, const float*, const float*,
+                            const float*, const float*, const float*, float*, float*, float*, const float*, int, float*,
+                            hipStream_t);
+int madnn_bn_prereduce_floats(int);
 hipError_t madnn_conv3x3_wgrad(const void*, const void*, float*, void*, int, int, int, int, int, int, hipStream_t);
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
                             int64_t, int64_t, hipStream_t);
@@ -346,7 +352,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
                     partial->size(1) == 2 && partial->size(2) == C,
                 "bn: partial statistics must be fp32 [rows, 2, C]");
   }
-  at::Tensor ws = at::empty({training && !ext ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C : 1}, fo);
+  at::Tensor ws = at::empty({training && !ext ? (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C
+                                              : (int64_t)madnn_bn_prereduce_floats((int)C)},
+                            fo);
   // training with a fused residual + ReLU: 1-bit ReLU mask for the backward passes
   const bool need_mask = training && relu && res.has_value();
   at::Tensor mask = at::empty({need_mask ? x.numel() / 8 : 0}, x.options().dtype(at::kByte));
@@ -437,7 +445,9 @@ std::vector<at::Tensor> bn_fwd_dual(const at::Tensor& x, const at::Tensor& r, co
   out.push_back(at::empty_like(x));
   out.push_back(at::empty({x.numel() / 8}, x.options().dtype(at::kByte)));
   for (int k = 0; k < 8; ++k) out.push_back(at::empty({C}, fo));
-  at::Tensor ws = at::empty({(int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
+  at::Tensor ws = at::empty({std::max<int64_t>((int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C,
+                                               (int64_t)madnn_bn_prereduce_floats((int)C))},
+                            fo);
   const float* pe = ext(partial);
   const float* pr = ext(partial_r);
   check(madnn_bn_fwd_dual(x.data_ptr(), r.data_ptr(), out[0].data_ptr(), out[1].data_ptr<uint8_t>(), M, (int)C,
@@ -507,7 +517,9 @@ std::vector<at::Tensor> bn_coef(const at::Tensor& x, const c10::optional<at::Ten
                     partial->size(1) == 2 && partial->size(2) == C,
                 "bn: partial statistics must be fp32 [rows, 2, C]");
   }
-  at::Tensor ws = at::empty({ext ? 1 : (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C}, fo);
+  at::Tensor ws = at::empty({ext ? (int64_t)madnn_bn_prereduce_floats((int)C)
+                                : (int64_t)madnn_bn_partial_rows(M, (int)C) * 2 * C},
+                            fo);
   int64_t* nb = nullptr;
   if (nbt.has_value() && nbt->defined()) {
     TORCH_CHECK(nbt->scalar_type() == at::kLong && nbt->is_cuda(), "num_batches_tracked must be an int64 device tensor");
@@ -705,6 +717,63 @@ std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Te
                           W, Ci, Co, cur_stream(x)),
         "conv3x3_fwd");
   return {y, part};
+}
+
+// Data grad (x = output gradient, w = flipped / transposed weight) with the BatchNorm-backward sums of
+// bny (the BN input feeding relu -> this conv) in the epilogue: -> (dx, partial [rows, 2, Co])
+std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_bnb(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bny,
+                                                   const at::Tensor& scale, const at::Tensor& shift) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  check_dev(bny, "bny");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  bny.scalar_type() == at::kBFloat16,
+              "conv3x3: bf16 only");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv3x3: x must be NHWC 4-D");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3: w must be a channels_last [Co, Ci, 3, 3]");
+  const int N = (int)x.size(0), Ci = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Co = (int)w.size(0);
+  TORCH_CHECK(bny.dim() == 4 && bny.size(0) == N && bny.size(1) == Co && bny.size(2) == H && bny.size(3) == W &&
+                  bny.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_fwd_bnb: bny must be the NHWC [N, Co, H, W] BN input");
+  TORCH_CHECK(scale.numel() == Co && shift.numel() == Co && scale.scalar_type() == at::kFloat &&
+                  shift.scalar_type() == at::kFloat && scale.is_contiguous() && shift.is_contiguous(),
+              "conv3x3_fwd_bnb: fp32 [Co] scale / shift");
+  TORCH_CHECK(madnn_conv3x3_supported(H, W, Ci, Co), "conv3x3: unsupported shape Ci=", Ci, " Co=", Co, " W=", W);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor part = at::empty({madnn_conv3x3_stat_rows((int64_t)N * H * W), 2, Co}, x.options().dtype(at::kFloat));
+  check(madnn_conv3x3_fwd_bnb(x.data_ptr(), w.data_ptr(), y.data_ptr(), part.data_ptr<float>(), bny.data_ptr(),
+                              scale.data_ptr<float>(), shift.data_ptr<float>(), N, H, W, Ci, Co, cur_stream(x)),
+        "conv3x3_fwd_bnb");
+  return {y, part};
+}
+
+// BN(+ReLU) backward from externally reduced sums (partial [G, 2, C]): -> (dx, dw, db)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_bwd_ext(const at::Tensor& dy, const at::Tensor& x,
+                                                          const c10::optional<at::Tensor>& w,
+                                                          const at::Tensor& save_mean, const at::Tensor& save_invstd,
+                                                          const at::Tensor& scale, const at::Tensor& shift,
+                                                          const at::Tensor& partial, bool relu) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = bn_rows(x, C);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && dy.strides() == x.strides(),
+              "bn_bwd_ext: bf16 dy / x of one layout");
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.is_contiguous() && partial.dim() == 3 &&
+                  partial.size(1) == 2 && partial.size(2) == C,
+              "bn_bwd_ext: partial must be fp32 [rows, 2, C]");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x), dw = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
+  at::Tensor ws = at::empty({(int64_t)madnn_bn_prereduce_floats((int)C)}, fo);
+  check(madnn_bn_bwd_ext(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, relu ? 1 : 0, optf(w),
+                         save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                         shift.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(),
+                         partial.data_ptr<float>(), (int)partial.size(0), ws.data_ptr<float>(), cur_stream(x)),
+        "bn_bwd_ext");
+  return {dx, dw, db};
 }
 
 // dW [Co, Ci, 3, 3] (channels_last) of y = conv3x3(x, w): dy [N, Co, H, W], x [N, Ci, H, W], both NHWC bf16
@@ -1051,6 +1120,11 @@ TORCH_LIBRARY(madnn, m) {
       "Tensor(c!) dv, bool causal, float scale) -> ()");
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
+  m.def(
+      "conv3x3_fwd_bnb(Tensor x, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
+  m.def(
+      "bn_bwd_ext(Tensor dy, Tensor x, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, Tensor shift, "
+      "Tensor partial, bool relu) -> (Tensor, Tensor, Tensor)");
   m.def("conv1x1_wgrad(Tensor dy, Tensor x, Tensor? scale=None, Tensor? shift=None) -> Tensor");
   m.def(
       "bn_coef(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, "
@@ -1099,6 +1173,8 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("bn_bwd", bn_bwd);
   m.impl("bn_fwd_dual", bn_fwd_dual);
   m.impl("bn_coef", bn_coef);
+  m.impl("conv3x3_fwd_bnb", conv3x3_fwd_bnb);
+  m.impl("bn_bwd_ext", bn_bwd_ext);
   m.impl("bn_bwd_dual", bn_bwd_dual);
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);

@@ -532,6 +532,52 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// Producer epilogues (K13: one row per 256-pixel tile) can hand over 10^4+ partial rows; the
+// finalize kernels walk rows with 32 slices per channel and turn latency-bound there.  Above
+// kPreMinRows the rows are first folded to kPreS rows by a (C/32) x kPreS grid.
+constexpr int kPreS = 64;
+constexpr int kPreMinRows = 1024;
+
+__global__ __launch_bounds__(1024) void partial_prereduce_kernel(const float* __restrict__ partial, int G, int C,
+                                                                 int pstride, int qoff, float* __restrict__ out) {
+  __shared__ float red[2][kFinSlices][33];
+  const int lc = threadIdx.x & 31, ls = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + lc;
+  const int lo = (int)((int64_t)G * blockIdx.y / gridDim.y), hi = (int)((int64_t)G * (blockIdx.y + 1) / gridDim.y);
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int k = lo + ls; k < hi; k += kFinSlices) {
+      s += partial[(int64_t)k * pstride + c];
+      q += partial[(int64_t)k * pstride + qoff + c];
+    }
+  }
+  red[0][ls][lc] = s;
+  red[1][ls][lc] = q;
+  __syncthreads();
+  if (ls == 0 && c < C) {
+    s = q = 0.f;
+    for (int k = 0; k < kFinSlices; ++k) {
+      s += red[0][k][lc];
+      q += red[1][k][lc];
+    }
+    out[((int64_t)blockIdx.y * 2) * C + c] = s;
+    out[((int64_t)blockIdx.y * 2 + 1) * C + c] = q;
+  }
+}
+
+// fold `part` ([G] rows of pstride floats, sums at 0 / qoff) to kPreS rows of [2][C] in `scratch`
+// (kPreS * 2 * C floats) when G is large; updates G / pstride / qoff to describe the result
+inline const float* prereduce(const float* part, int& G, int C, int& pstride, int& qoff, float* scratch,
+                              hipStream_t stream) {
+  if (G < kPreMinRows || scratch == nullptr || scratch == part) return part;
+  hipLaunchKernelGGL(partial_prereduce_kernel, dim3((C + 31) / 32, kPreS), dim3(32 * kFinSlices), 0, stream, part, G,
+                     C, pstride, qoff, scratch);
+  G = kPreS;
+  pstride = 2 * C;
+  qoff = C;
+  return scratch;
+}
+
 static int bn_grid_rows(int64_t M, int C) {
   const BnGeom g = bn_geom(C);
   int64_t iters = (M + g.rpi - 1) / g.rpi;
@@ -567,6 +613,9 @@ int madnn_bn_supported(int C) { return (C % 8 == 0 && C >= 8 && C <= 2048) ? 1 :
 
 int madnn_bn_partial_rows(int64_t M, int C) { return madnn::bn_grid_rows(M, C); }
 
+// scratch floats the producer-partial paths need to fold many partial rows (prereduce)
+int madnn_bn_prereduce_floats(int C) { return madnn::kPreS * 2 * C; }
+
 // Forward. training: compute batch stats (+ running update); else use running stats.
 // ext_partial: [ext_rows][2][C] per-channel (sum, sum of squares) of x already produced by
 // the kernel that wrote x (K9 conv1x1 epilogue); the statistics pass over x is skipped.
@@ -584,8 +633,9 @@ hipError_t madnn_bn_fwd(const void* x, const void* res, void* y, unsigned char* 
   if (training) {
     const float* part = workspace;
     if (ext_partial != nullptr && ext_rows > 0) {
-      part = ext_partial;
       G = ext_rows;
+      int ps = 2 * C, qo = C;
+      part = prereduce(ext_partial, G, C, ps, qo, workspace, stream);
     } else {
       MADNN_DISPATCH_DT(xdt, XDT, {
         hipLaunchKernelGGL((bn_stats_kernel<XDT>), dim3(G), dim3(kBnThreads), lds, stream, x, M, C, workspace);
@@ -674,8 +724,9 @@ hipError_t madnn_bn_fwd_dual(const void* x, const void* r, void* y, unsigned cha
     const float* part = workspace;
     int G = bn_grid_rows(M, C);
     if (ext[k] != nullptr && erows[k] > 0) {
-      part = ext[k];
       G = erows[k];
+      int ps = 2 * C, qo = C;
+      part = prereduce(ext[k], G, C, ps, qo, workspace, stream);
     } else {
       hipLaunchKernelGGL((bn_stats_kernel<kBF16>), dim3(G), dim3(kBnThreads), lds, stream, src[k], M, C, workspace);
       MADNN_HIP_CHECK(hipGetLastError());
@@ -734,8 +785,9 @@ hipError_t madnn_bn_coef(const void* x, int64_t M, int C, float eps, float momen
   int G = bn_grid_rows(M, C);
   const float* part = workspace;
   if (ext_partial != nullptr && ext_rows > 0) {
-    part = ext_partial;
     G = ext_rows;
+    int ps = 2 * C, qo = C;
+    part = prereduce(ext_partial, G, C, ps, qo, workspace, stream);
   } else {
     const BnGeom g = bn_geom(C);
     const size_t lds = g.rpi > 1 ? (size_t)g.rpi * 2 * C * sizeof(float) : 0;
@@ -754,6 +806,34 @@ hipError_t madnn_bn_bwd_finalize(const float* partial, int G, int C, int pstride
   using namespace madnn;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, partial, G, C,
                      pstride, qoff, M, w, mean, invstd, dw, db, ca, cb, cc);
+  return hipGetLastError();
+}
+
+// BatchNorm(+ReLU, no residual) backward whose reduction came from the producer of dy (K13's data-grad
+// epilogue: partial [G][2][C] = (sum g, sum g*x)): finalize + apply only.  coef: 3 * C floats.
+// scratch: madnn_bn_prereduce_floats(C) floats
+hipError_t madnn_bn_bwd_ext(const void* dy, const void* x, void* dx, int64_t M, int C, int relu, const float* w,
+                            const float* save_mean, const float* save_invstd, const float* scale, const float* shift,
+                            float* dw, float* db, float* coef, const float* partial, int G, float* scratch,
+                            hipStream_t stream) {
+  using namespace madnn;
+  if (!madnn_bn_supported(C) || partial == nullptr || G <= 0) return hipErrorInvalidValue;
+  if (M <= 0) return hipSuccess;
+  int ps = 2 * C, qo = C;
+  const float* part = prereduce(partial, G, C, ps, qo, scratch, stream);
+  MADNN_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(32 * kFinSlices), 0, stream, part, G, C, ps,
+                     qo, M, w, save_mean, save_invstd, dw, db, coef, coef + C, coef + 2 * C);
+  MADNN_HIP_CHECK(hipGetLastError());
+  const int64_t total = M * C;
+  const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
+  if (relu) {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, true, false>), dim3(grid), dim3(256), 0, stream, dy, x, nullptr,
+                       scale, shift, coef, coef + C, coef + 2 * C, dx, nullptr, total, C, bn_walk_flags());
+  } else {
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, false, false>), dim3(grid), dim3(256), 0, stream, dy, x, nullptr,
+                       scale, shift, coef, coef + C, coef + 2 * C, dx, nullptr, total, C, bn_walk_flags());
+  }
   return hipGetLastError();
 }
 }  // extern "C"

@@ -49,6 +49,9 @@ struct Args {
   const uint16_t* w;   // [Co][9][Ci] (channels_last weight)
   uint16_t* y;         // [M][Co]
   float* stats;        // [m_tiles][2][Co] or null
+  const uint16_t* bny;  // BNB epilogue: the BatchNorm input y [M][Co] whose backward sums are taken
+  const float* bnsc;    //   its forward scale / shift (ReLU mask = y * sc + sh > 0)
+  const float* bnsh;
   int64_t M;
   int H, W, Ci, Co;
   int halo_px;         // LDS halo capacity in pixels
@@ -79,8 +82,13 @@ __host__ inline size_t conv3x3_lds(int W, int CH) {
   return cap > 32 * 1024 ? cap : 32 * 1024;  // the epilogue's [256][64] bf16 tile reuses the whole image
 }
 
-template <int CH, bool STATS>
+// BNB (data grad of a convolution whose input was relu(bn(y))): the epilogue also accumulates the
+// BatchNorm backward's two sums over its output tile, sum g and sum g*y with g = out * [y*sc+sh > 0]
+// (out = the bf16-rounded input gradient it stores), as the [m_tiles][2][Co] partial rows of
+// bn.hip's backward finalize -- the BN backward then skips its reduction pass over (dx, y).
+template <int CH, bool STATS, bool BNB = false>
 __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(const Args p) {
+  static_assert(!(STATS && BNB), "one statistics epilogue per launch");
   using C = Chunk<CH>;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* halo = smem;                                     // [halo_px][CH]
@@ -222,14 +230,41 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
   }
   __syncthreads();
   const int ch = tid & 7;
-  float ssum[8], ssq[8];
+  float ssum[8], ssq[8], bs[8], bh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  if constexpr (BNB) {  // this thread's 8 channels are fixed for the whole tile
+    const f32x4* sc4 = reinterpret_cast<const f32x4*>(p.bnsc + co0 + 8 * ch);
+    const f32x4* sh4 = reinterpret_cast<const f32x4*>(p.bnsh + co0 + 8 * ch);
+    const f32x4 s0 = sc4[0], s1 = sc4[1], h0 = sh4[0], h1 = sh4[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bs[e] = s0[e];
+      bs[4 + e] = s1[e];
+      bh[e] = h0[e];
+      bh[4 + e] = h1[e];
+    }
+  }
   for (int r = tid >> 3; r < kBJ; r += kThreads / 8) {
     const int64_t m = j0 + r;
     if (m >= p.M) break;
     const u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, ch));
     *reinterpret_cast<u32x4*>(p.y + m * p.Co + co0 + 8 * ch) = v;
+    if constexpr (BNB) {
+      const u32x4 yv = *reinterpret_cast<const u32x4*>(p.bny + m * p.Co + co0 + 8 * ch);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int k = 2 * e + hf;
+          const float g = bf16_to_f32((unsigned short)(hf ? v[e] >> 16 : v[e] & 0xffffu));
+          const float yy = bf16_to_f32((unsigned short)(hf ? yv[e] >> 16 : yv[e] & 0xffffu));
+          const float gm = yy * bs[k] + bh[k] > 0.f ? g : 0.f;
+          ssum[k] += gm;
+          ssq[k] += gm * yy;
+        }
+      }
+    }
     if constexpr (STATS) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -242,7 +277,7 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
       }
     }
   }
-  if constexpr (STATS) {
+  if constexpr (STATS || BNB) {
     __syncthreads();  // the tile image is consumed
     float* red = reinterpret_cast<float*>(smem);  // [32 row groups][2][64], 16-B vector writes
     const int rg = tid >> 3;
@@ -467,6 +502,39 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
     if (stats) hipLaunchKernelGGL((conv3x3_kernel<64, true>), g, b, lds, s, p);
     else hipLaunchKernelGGL((conv3x3_kernel<64, false>), g, b, lds, s, p);
   }
+  return hipGetLastError();
+}
+
+// Data grad with the BatchNorm-backward sums in the epilogue (see BNB): x = the output gradient,
+// w = the flipped / transposed weight, y = dx; partial [ceil(M/256)][2][Co] = (sum g, sum g*bny)
+hipError_t madnn_conv3x3_fwd_bnb(const void* x, const void* w, void* y, float* partial, const void* bny,
+                                 const float* bnsc, const float* bnsh, int N, int H, int W, int Ci, int Co,
+                                 hipStream_t s) {
+  if (!madnn_conv3x3_supported(H, W, Ci, Co) || partial == nullptr || bny == nullptr) return hipErrorInvalidValue;
+  Args p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(y);
+  p.stats = partial;
+  p.bny = static_cast<const uint16_t*>(bny);
+  p.bnsc = bnsc;
+  p.bnsh = bnsh;
+  p.M = (int64_t)N * H * W;
+  if (p.M <= 0) return hipSuccess;
+  p.H = H;
+  p.W = W;
+  p.Ci = Ci;
+  p.Co = Co;
+  const int CH = k13_ch(Ci);
+  p.halo_px = halo_rows_px(W, 1024 / (2 * CH));
+  p.m_tiles = (int)((p.M + kBJ - 1) / kBJ);
+  p.co_tiles = Co / kBI;
+  const int64_t grid = (int64_t)p.m_tiles * p.co_tiles;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  const size_t lds = conv3x3_lds(W, CH);
+  const dim3 g((unsigned)grid), b(kThreads);
+  if (CH == 32) hipLaunchKernelGGL((conv3x3_kernel<32, false, true>), g, b, lds, s, p);
+  else hipLaunchKernelGGL((conv3x3_kernel<64, false, true>), g, b, lds, s, p);
   return hipGetLastError();
 }
 

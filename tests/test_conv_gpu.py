@@ -250,3 +250,44 @@ def test_bottleneck_bn_prologue_matches_unfused(cuda, monkeypatch):
     assert rel(x1.grad, x3.grad) < 0.1   # bf16 end to end through a whole block: ~0.06
     for (n, p1), p2, p3 in zip(blk.named_parameters(), blk2.parameters(), blk3.parameters()):
         assert rel(p1.grad, p3.grad) <= 1.5 * rel(p2.grad, p3.grad) + 2e-3, n
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56), (3, 128, 128, 28, 28), (2, 256, 256, 14, 14),
+                                   (4, 512, 512, 7, 7), (1, 64, 128, 9, 13),
+                                   (96, 64, 64, 56, 56)])   # > 1024 partial rows: the finalize pre-fold
+def test_bn_relu_conv3x3_dgrad_epilogue_matches_fp32(cuda, shape):
+    """K13 data grad with bn's backward sums in the epilogue (bn1 -> conv2): output, output
+    statistics, running stats and every gradient vs fp32 eager BN + ReLU + conv."""
+    from madnn.nn.norm import FusedBatchNorm2d
+
+    n, ci, co, h, w = shape
+    torch.manual_seed(3)
+    y = (_rand((n, ci, h, w), cuda).float() * 1.4 + 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.requires_grad_(True)
+    wt = _rand((co, ci, 3, 3), cuda, (9 * ci) ** -0.5).contiguous(memory_format=torch.channels_last)
+    wt.requires_grad_(True)
+    bn = FusedBatchNorm2d(ci).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(-0.5, 1.5)
+        bn.bias.normal_(0, 0.2)
+    ref = torch.nn.BatchNorm2d(ci).to(cuda)
+    ref.load_state_dict(bn.state_dict())
+    assert ops.bn_relu_conv3x3_supported(y, bn, wt)
+    out, part = ops.bn_relu_conv3x3(y, bn, wt, stats=True)
+    dout = _rand(tuple(out.shape), cuda)
+    out.backward(dout)
+    yr = y.detach().float().requires_grad_(True)
+    wr = wt.detach().float().requires_grad_(True)
+    outr = F.conv2d(torch.relu(ref(yr)), wr, padding=1)
+    outr.backward(dout.float())
+    _close(out.float(), outr, 3e-2)
+    of = out.double().permute(0, 2, 3, 1).reshape(-1, co)
+    torch.testing.assert_close(part.double().sum(0)[0], of.sum(0), atol=1e-2 * of.abs().sum(0).max().item(),
+                               rtol=1e-3)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    _close(wt.grad.float(), wr.grad, 3e-2)
+    rel = ((y.grad.float() - yr.grad).norm() / yr.grad.norm()).item()
+    assert rel < 0.03, rel
+    _close(bn.weight.grad, ref.weight.grad, 6e-2)
+    _close(bn.bias.grad, ref.bias.grad, 6e-2)

@@ -605,3 +605,24 @@ def test_batchnorm_apply_walk_variants_bitwise(cuda):
     for v, k, d in bad:
         ref = outs[0][k].float().abs().max().item()
         assert d <= 2 ** -7 * max(ref, 1.0), (v, k, d, ref)
+
+
+def test_batchnorm_many_producer_partial_rows(cuda):
+    """Producer statistics with thousands of partial rows (K13's one row per 256-pixel tile) are
+    folded before the finalize: running stats and outputs equal the statistics-pass path."""
+    torch.manual_seed(13)
+    C = 64
+    x = (torch.randn(8, C, 64, 96, device=cuda) * 2 + 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
+    v = x.float().permute(0, 2, 3, 1).reshape(-1, C)
+    rows = torch.arange(v.size(0), device=cuda) % 3001   # 3001 uneven row groups
+    part = torch.zeros(3001, 2, C, device=cuda)
+    part[:, 0].index_add_(0, rows, v)
+    part[:, 1].index_add_(0, rows, v * v)
+    w, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    rm1, rv1 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y1 = ops.batch_norm_act(x, w, b, rm1, rv1, training=True, relu=True)
+    y2 = ops.batch_norm_act(x, w, b, rm2, rv2, training=True, relu=True, stats=part)
+    torch.testing.assert_close(rm1, rm2, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rv1, rv2, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(y1.float(), y2.float(), atol=2e-2, rtol=2e-2)
