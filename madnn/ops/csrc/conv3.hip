@@ -228,6 +228,17 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
         *reinterpret_cast<u32x2*>(ot + out_off(pr, ic >> 3) + 8 * ((ic >> 2) & 1)) = u32x2{lo, hi};
       }
   }
+  // BNB: fetch this thread's 8 rows of y now -- the accumulators are dead, so the 8 x 16 B land in
+  // their registers and the loads overlap the barrier and the LDS tile reads below
+  constexpr int kRowsPerThread = kBJ / (kThreads / 8);
+  u32x4 ypre[BNB ? kRowsPerThread : 1];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; ++k) {
+      const int64_t m = j0 + (tid >> 3) + k * (kThreads / 8);
+      ypre[k] = m < p.M ? *reinterpret_cast<const u32x4*>(p.bny + m * p.Co + co0 + 8 * (tid & 7)) : u32x4{0, 0, 0, 0};
+    }
+  }
   __syncthreads();
   const int ch = tid & 7;
   float ssum[8], ssq[8], bs[8], bh[8];
@@ -245,13 +256,15 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
       bh[4 + e] = h1[e];
     }
   }
-  for (int r = tid >> 3; r < kBJ; r += kThreads / 8) {
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; ++k) {
+    const int r = (tid >> 3) + k * (kThreads / 8);
     const int64_t m = j0 + r;
     if (m >= p.M) break;
     const u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, ch));
     *reinterpret_cast<u32x4*>(p.y + m * p.Co + co0 + 8 * ch) = v;
     if constexpr (BNB) {
-      const u32x4 yv = *reinterpret_cast<const u32x4*>(p.bny + m * p.Co + co0 + 8 * ch);
+      const u32x4 yv = ypre[k];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
 #pragma unroll
