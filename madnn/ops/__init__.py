@@ -635,6 +635,45 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
         return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
 
 
+class _BNReluConv1x1EpiFn(torch.autograd.Function):
+    """``conv1x1(relu(bn(y)), w)`` in training with bn's backward reduction taken in the K9 data
+    grad's epilogue (the conv3 shapes whose data grad runs on K9): forward = K5 apply + K9 with the
+    output statistics; backward = K9 data grad (+ bn's sums), the routed weight grad on the stored
+    activation, and bn's backward as finalize + apply only."""
+
+    @staticmethod
+    def forward(ctx, y, w, bn_w, bn_b, bn, stats_in, want_stats):
+        a, mean, invstd, scale, shift, _ = torch.ops.madnn.bn_fwd(y, None, bn_w, bn_b, bn.running_mean,
+                                                                  bn.running_var, bn.num_batches_tracked, True,
+                                                                  float(bn.momentum), float(bn.eps), True, stats_in)
+        fwd, _, wgrad = conv1x1_route(a.size(1), w.size(0))
+        if fwd == "k9":
+            out, part = torch.ops.madnn.conv1x1_fwd(a, w, bool(want_stats))
+        else:
+            out = torch.nn.functional.conv2d(a, w) if a.dim() == 4 else torch.mm(a, w.reshape(w.size(0), -1).t())
+            part = a.new_empty((0, 2, w.size(0)), dtype=torch.float32)
+        ctx.save_for_backward(y, a, w, bn_w, mean, invstd, scale, shift)
+        ctx.wgrad = wgrad
+        ctx.mark_non_differentiable(part)
+        return out, part
+
+    @staticmethod
+    def backward(ctx, dout, _dpart):
+        y, a, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
+        dout = _nhwc(dout.to(y.dtype))
+        da, part = torch.ops.madnn.conv1x1_dgrad_bnb(dout, w, y, scale, shift)
+        if ctx.wgrad == "k9":
+            dw = torch.ops.madnn.conv1x1_wgrad(dout, a).to(w.dtype).view(w.shape)
+        elif a.dim() == 4:
+            dw = torch.ops.aten.convolution_backward(dout, a, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0),
+                                                     (1, 1), False, (0, 0), 1, (False, True, False))[1].view(w.shape)
+        else:
+            dw = torch.mm(dout.t(), a).view(w.shape)
+        dy, dbw, dbb = torch.ops.madnn.bn_bwd_ext(da, y, bn_w, mean, invstd, scale, shift, part, True)
+        need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
+
+
 def bn_relu_conv1x1_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
     """Whether :func:`bn_relu_conv1x1` runs fused: training-mode BN with running statistics and an
     fp32 affine, bf16 NHWC input, K9-shaped weight."""
@@ -644,12 +683,18 @@ def bn_relu_conv1x1_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
 
 def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[torch.Tensor] = None,
                     stats: bool = False):
-    """``conv1x1(relu(bn(y)), w)``: the BatchNorm's apply pass is fused into the convolution's
-    operand load (ResNet's bn2 -> conv3).  ``stats_in``: ``y``'s partial statistics from its
-    producer; ``stats``: also return the output's partial statistics (None if not computed)."""
+    """``conv1x1(relu(bn(y)), w)`` (ResNet's bn2 -> conv3): with ``MADNN_BN_PROLOGUE=1`` the
+    BatchNorm's apply pass is fused into the convolution's operand load; otherwise, when the data
+    grad runs on K9, bn's backward reduction is taken in that kernel's epilogue.  ``stats_in``:
+    ``y``'s partial statistics from its producer; ``stats``: also return the output's partial
+    statistics (None if not computed)."""
     if bn_relu_conv1x1_supported(y, bn, w):
         _need_native("bn_relu_conv1x1")
         out, part = _BNReluConv1x1Fn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
+        return (out, part if part.numel() else None) if stats else out
+    if bn_relu_conv1x1_epi_supported(y, bn, w):
+        _need_native("bn_relu_conv1x1")
+        out, part = _BNReluConv1x1EpiFn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
         return (out, part if part.numel() else None) if stats else out
     a = bn(y, relu=True, stats=stats_in) if _is_fused_bn(bn) else torch.relu(bn(y))
     if conv1x1_supported(a, w):
@@ -664,6 +709,15 @@ def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[
 # on the LDS-store path of a one-k-step-per-tile, write-bound GEMM) and K9's weight grad is 1.1 ms/step
 # slower than MIOpen's on the conv3 shapes; together they eat the 1.5 ms/step bn2 apply pass saved.
 _BN_PROLOGUE = os.environ.get("MADNN_BN_PROLOGUE", "0") != "0"
+
+
+def bn_relu_conv1x1_epi_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
+    """The data-grad-epilogue variant of :func:`bn_relu_conv1x1`: training BN (running stats, fp32
+    affine) in front of a 1x1 convolution whose data grad routes to K9."""
+    return (_BN_DGRAD_EPI and isinstance(y, torch.Tensor) and bn.training and bn.track_running_stats
+            and bn.affine and bn.momentum is not None and bn.weight.dtype == torch.float32
+            and conv1x1_supported(y, w) and bn_supported(y, bn.weight)
+            and conv1x1_route(y.size(1), w.size(0))[1] == "k9")
 
 
 class _BNReluMaxPoolFn(torch.autograd.Function):
@@ -928,7 +982,8 @@ __all__ = [
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
     "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "batch_norm_add_bn_relu",
     "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "bn_relu_maxpool",
-    "bn_relu_maxpool_supported", "bn_relu_conv3x3", "bn_relu_conv3x3_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
+    "bn_relu_maxpool_supported", "bn_relu_conv3x3", "bn_relu_conv3x3_supported",
+    "bn_relu_conv1x1_epi_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
 
 if os.environ.get("MADNN_EAGER_LOAD", "0") == "1":

@@ -72,7 +72,9 @@ int madnn_conv1x1_supported(int64_t, int64_t);
 int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, const float*,
                              const float*, hipStream_t);
-hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, hipStream_t);
+hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, const void*,
+                               const float*, const float*, float*, hipStream_t);
+int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
 hipError_t madnn_bn_coef(const void*, int64_t, int, float, float, const float*, const float*, float*, float*, int64_t*,
@@ -605,9 +607,29 @@ at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::o
     TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad: residual layout");
   }
   check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
-                            cout, cur_stream(dy)),
+                            cout, nullptr, nullptr, nullptr, nullptr, cur_stream(dy)),
         "conv1x1_dgrad");
   return dx;
+}
+
+// dx = dy (*) w^T where dx is d relu(bn(bny)), plus bn's backward sums (sum g, sum g*bny) from the
+// epilogue: -> (dx, partial [rows, 2, Cin])
+std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnb(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& bny,
+                                                     const at::Tensor& scale, const at::Tensor& shift) {
+  const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
+  const int64_t M = conv_rows(dy, cout, "dy");
+  conv_check_w(w, cout, cin);
+  TORCH_CHECK(conv_rows(bny, cin, "bny") == M && bny.dim() == dy.dim(), "conv1x1_dgrad_bnb: bny layout");
+  TORCH_CHECK(scale.numel() == cin && shift.numel() == cin && scale.scalar_type() == at::kFloat &&
+                  shift.scalar_type() == at::kFloat && scale.is_contiguous() && shift.is_contiguous(),
+              "conv1x1_dgrad_bnb: fp32 [Cin] scale / shift");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dx = conv_out_like(dy, cin);
+  at::Tensor part = at::empty({madnn_conv1x1_dgrad_rows(M, cin, cout), 2, cin}, dy.options().dtype(at::kFloat));
+  check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), nullptr, M, cin, cout, bny.data_ptr(),
+                            scale.data_ptr<float>(), shift.data_ptr<float>(), part.data_ptr<float>(), cur_stream(dy)),
+        "conv1x1_dgrad_bnb");
+  return {dx, part};
 }
 
 // fp32 [Cout, Cin] weight gradient
@@ -1120,6 +1142,7 @@ TORCH_LIBRARY(madnn, m) {
       "Tensor(c!) dv, bool causal, float scale) -> ()");
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
+  m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
       "conv3x3_fwd_bnb(Tensor x, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
@@ -1174,6 +1197,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("bn_fwd_dual", bn_fwd_dual);
   m.impl("bn_coef", bn_coef);
   m.impl("conv3x3_fwd_bnb", conv3x3_fwd_bnb);
+  m.impl("conv1x1_dgrad_bnb", conv1x1_dgrad_bnb);
   m.impl("bn_bwd_ext", bn_bwd_ext);
   m.impl("bn_bwd_dual", bn_bwd_dual);
   m.impl("xent_fwd", xent_fwd);

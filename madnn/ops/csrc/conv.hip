@@ -73,6 +73,9 @@ struct GemmArgs {
   float* stats;
   const float* bsc;  // B-operand BatchNorm prologue: relu(b * bsc[c] + bsh[c]) (PRO kernels)
   const float* bsh;
+  const uint16_t* bny;  // BNB epilogue (data grad): BN input y [J][I] whose backward sums are taken,
+  const float* bnsc;    //   with its forward scale / shift (ReLU mask = y * sc + sh > 0)
+  const float* bnsh;
   int64_t lda, ldb, ldo;
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
@@ -168,8 +171,12 @@ struct Stage {
   }
 };
 
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false>
+// BNB (store mode): besides the output D, accumulate per output channel the BatchNorm backward sums
+// sum g and sum g*y, g = D * [y * sc + sh > 0], into the same [groups][2][I] partial rows STATS writes
+// (the data grad of conv3 whose input was relu(bn2(y)): bn2's backward skips its reduction pass).
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false, bool BNB = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
+  static_assert(!(STATS && BNB), "one statistics epilogue per launch");
   constexpr int NI = (BI == 64 && BJ == 64) ? 1 : 2;  // 32-row i blocks per wave
   constexpr int WI = BI / (32 * NI), WJ = 4 / WI, NJ = BJ / (32 * WJ);
   static_assert(WI * WJ == 4 && NJ >= 1, "four waves tile the workgroup");
@@ -215,10 +222,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
 #pragma unroll
     for (int b = 0; b < NJ; ++b) acc[a][b] = zero16();
   // statistics: this thread's 8 output channels (chunk tid % CPR), summed over its rows of every tile
-  float ssum[8], ssq[8];
-  if constexpr (STATS) {
+  float ssum[8], ssq[8], bs[8], bh[8];
+  if constexpr (STATS || BNB) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) ssum[e] = ssq[e] = 0.f;
+  }
+  if constexpr (BNB) {  // this thread's 8 output channels (chunk tid % CPR of the i tile) are fixed
+    const int cc = tid % (BI / 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs[e] = p.bnsc[i0 + 8 * cc + e];
+      bh[e] = p.bnsh[i0 + 8 * cc + e];
+    }
   }
   // byte offset of 16-B chunk c of output row r: rows of 256 B (BI = 128) or 128 B (BI = 64)
   auto out_off = [](int r, int c) {
@@ -300,6 +315,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
               }
             }
             *reinterpret_cast<u32x4*>(out + j * p.ldo + i0 + 8 * c) = v;
+            if constexpr (BNB) {
+              const u32x4 yv = *reinterpret_cast<const u32x4*>(p.bny + j * p.ldo + i0 + 8 * c);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                  const int k = 2 * e + hf;
+                  const float g = bf16_to_f32((unsigned short)(hf ? v[e] >> 16 : v[e] & 0xffffu));
+                  const float yy = bf16_to_f32((unsigned short)(hf ? yv[e] >> 16 : yv[e] & 0xffffu));
+                  const float gm = yy * bs[k] + bh[k] > 0.f ? g : 0.f;
+                  ssum[k] += gm;
+                  ssq[k] += gm * yy;
+                }
+              }
+            }
             if constexpr (STATS) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -338,7 +368,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
     ks = nks;
   }
 
-  if constexpr (STATS) {
+  if constexpr (STATS || BNB) {
     __syncthreads();  // smem is free
     float* red = reinterpret_cast<float*>(smem);  // [RPP][2][BI]
     const int c = tid % CPR, rg = tid / CPR;
@@ -357,9 +387,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   }
 }
 
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false>
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false, bool BNB = false>
 hipError_t launch(const GemmArgs& p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS, PRO>), dim3(grid), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS, PRO, BNB>), dim3(grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
 }
 
@@ -405,6 +435,14 @@ int madnn_conv1x1_stat_rows(int64_t M, int64_t cin, int64_t cout) {
 }
 
 // bsc/bsh (optional, [cin] fp32): x is a raw BatchNorm input, convolved as relu(x * bsc + bsh)
+// partial rows the BNB data grad writes ([rows][2][cin] fp32)
+int madnn_conv1x1_dgrad_rows(int64_t M, int64_t cin, int64_t cout) {
+  if (!madnn_conv1x1_supported(cin, cout) || M <= 0) return 0;
+  GemmArgs p{};
+  plan_persistent(p, M, cin % 128 == 0 ? 128 : 64, cin, cout);
+  return p.j_groups;
+}
+
 hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats, int64_t M, int64_t cin,
                              int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
@@ -444,8 +482,11 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
 }
 
 // dx = dY W (+ res: an accumulated gradient of the same layout, added in the epilogue)
+// bny/bnsc/bnsh/partial (optional, all or none): dx is d relu(bn(bny)); the epilogue also writes bn's
+// backward sums as partial [madnn_conv1x1_dgrad_rows][2][cin] (see BNB)
 hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const void* res, int64_t M, int64_t cin,
-                               int64_t cout, hipStream_t s) {
+                               int64_t cout, const void* bny, const float* bnsc, const float* bnsh, float* partial,
+                               hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -463,6 +504,15 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   const bool wide = cin % 128 == 0;
   plan_persistent(p, M, wide ? 128 : 64, cin, cout);
   const int grid = p.i_tiles * p.j_groups;
+  if (bny != nullptr) {
+    if (bnsc == nullptr || bnsh == nullptr || partial == nullptr || res != nullptr) return hipErrorInvalidValue;
+    p.bny = static_cast<const uint16_t*>(bny);
+    p.bnsc = bnsc;
+    p.bnsh = bnsh;
+    p.stats = partial;
+    return wide ? launch<true, false, 128, 128, kStoreT, false, false, true>(p, grid, s)
+                : launch<true, false, 64, 128, kStoreT, false, false, true>(p, grid, s);
+  }
   return wide ? launch<true, false, 128, 128, kStoreT, false>(p, grid, s)
               : launch<true, false, 64, 128, kStoreT, false>(p, grid, s);
 }

@@ -291,3 +291,40 @@ def test_bn_relu_conv3x3_dgrad_epilogue_matches_fp32(cuda, shape):
     assert rel < 0.03, rel
     _close(bn.weight.grad, ref.weight.grad, 6e-2)
     _close(bn.bias.grad, ref.bias.grad, 6e-2)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 256, 56, 56), (3, 128, 512, 5, 9), (2, 192, 320, 11, 13),
+                                   (4, 64, 64, 16, 16)])
+def test_bn_relu_conv1x1_dgrad_epilogue_matches_fp32(cuda, shape):
+    """K9 data grad with bn's backward sums in the epilogue (bn2 -> conv3 on the K9-routed shapes):
+    output, running stats and every gradient vs fp32 eager BN + ReLU + 1x1 conv."""
+    from madnn.nn.norm import FusedBatchNorm2d
+
+    n, cin, cout, h, w = shape
+    torch.manual_seed(4)
+    y = (_rand((n, cin, h, w), cuda).float() * 1.2 + 0.2).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.requires_grad_(True)
+    wt = _rand((cout, cin, 1, 1), cuda, cin ** -0.5).contiguous(memory_format=torch.channels_last)
+    wt.requires_grad_(True)
+    bn = FusedBatchNorm2d(cin).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(-0.5, 1.5)
+        bn.bias.normal_(0, 0.2)
+    ref = torch.nn.BatchNorm2d(cin).to(cuda)
+    ref.load_state_dict(bn.state_dict())
+    assert not ops.bn_relu_conv1x1_supported(y, bn, wt) and ops.bn_relu_conv1x1_epi_supported(y, bn, wt)
+    out, part = ops.bn_relu_conv1x1(y, bn, wt, stats=True)
+    dout = _rand(tuple(out.shape), cuda)
+    out.backward(dout)
+    yr = y.detach().float().requires_grad_(True)
+    wr = wt.detach().float().requires_grad_(True)
+    outr = F.conv2d(torch.relu(ref(yr)), wr)
+    outr.backward(dout.float())
+    _close(out.float(), outr, 3e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
+    _close(wt.grad.float(), wr.grad, 3e-2)
+    rel = ((y.grad.float() - yr.grad).norm() / yr.grad.norm()).item()
+    assert rel < 0.03, rel
+    _close(bn.weight.grad, ref.weight.grad, 6e-2)
+    _close(bn.bias.grad, ref.bias.grad, 6e-2)
