@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu"])
+    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu", "gelu_bwd_fast"])
     a = ap.parse_args()
     import madnn
     from madnn import ops
@@ -44,6 +44,10 @@ def main():
             ops._LT_KIND["res"] = on
         elif a.switch == "gelu":
             ops.GELU_KERNEL = on
+        elif a.switch == "gelu_bwd_fast":
+            import ctypes
+
+            ctypes.CDLL(str(ops.kernels_path())).madnn_bias_fast_tanh(1 if on else 0)
 
     def window(n):
         torch.cuda.synchronize()

@@ -19,10 +19,20 @@ namespace madnn {
 
 constexpr int kBiasLanes = 256;
 
+// FAST: tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp, as the forward computes it (libm tanhf is ~30
+// VALU per element with range branches: at 32 elements per lane per row step the GELU backward
+// pass was partly VALU-bound instead of HBM-bound)
+template <bool FAST = true>
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
-  const float t = tanhf(k0 * (x + k1 * x2 * x));
+  const float u = k0 * (x + k1 * x2 * x);
+  float t;
+  if constexpr (FAST) {
+    t = 1.f - 2.f / (__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.f);
+  } else {
+    t = tanhf(u);
+  }
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 
@@ -75,7 +85,7 @@ __host__ __device__ inline BiasGeom bias_geom(int N) {
   return {tpr, kBiasLanes / tpr, (lanes + tpr - 1) / tpr};
 }
 
-template <int XDT, bool GELU>
+template <int XDT, bool GELU, bool FAST = true>
 __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
                                                                const void* __restrict__ pre, void* __restrict__ dp,
                                                                int64_t M, int N, float* __restrict__ partial) {
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad(p[u][j]);
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad<FAST>(p[u][j]);
           store8<XDT>(dp, (r + u * step) * N + col, v[u]);
         }
       }
@@ -118,7 +128,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
         float p[8];
         load8<XDT>(pre, r * N + col, p);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad(p[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad<FAST>(p[j]);
         store8<XDT>(dp, r * N + col, v);
       }
 #pragma unroll
@@ -172,12 +182,19 @@ using namespace madnn;
 // (N=1024/3072/4096: 11.6/20.2/23.3 us vs 17.4/24.2/28.6 at 4: fewer partial rows to write and
 // re-read), the GELU variant, which also writes dp, at 4 (36.4/80.9/92.3 us vs 40.6/135/134 at 1).
 static int g_bias_wg_per_cu[2] = {1, 4};
+static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
 
 extern "C" {
 
 int madnn_bias_tune(int gelu, int wg_per_cu) {
   const int old = g_bias_wg_per_cu[gelu ? 1 : 0];
   if (wg_per_cu > 0) g_bias_wg_per_cu[gelu ? 1 : 0] = wg_per_cu;
+  return old;
+}
+
+int madnn_bias_fast_tanh(int on) {
+  const int old = g_bias_fast_tanh;
+  if (on >= 0) g_bias_fast_tanh = on != 0;
   return old;
 }
 
@@ -216,9 +233,12 @@ hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M,
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
+    if (pre && g_bias_fast_tanh) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
                          partial);
+    } else if (pre) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, false>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
+                         N, partial);
     } else {
       hipLaunchKernelGGL((bias_grad_kernel<XDT, false>), grid, dim3(kBiasLanes), 0, stream, dy, nullptr, nullptr,
                          M, N, partial);
