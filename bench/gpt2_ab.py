@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu", "gelu_bwd_fast"])
+    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp"])
     a = ap.parse_args()
     import madnn
     from madnn import ops
@@ -48,6 +48,10 @@ def main():
             import ctypes
 
             ctypes.CDLL(str(ops.kernels_path())).madnn_bias_fast_tanh(1 if on else 0)
+        elif a.switch == "gelu_rcp":
+            import ctypes
+
+            ctypes.CDLL(str(ops.kernels_path())).madnn_gelu_rcp(1 if on else 0)
 
     def window(n):
         torch.cuda.synchronize()

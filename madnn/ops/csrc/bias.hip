@@ -22,14 +22,21 @@ constexpr int kBiasLanes = 256;
 // FAST: tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp, as the forward computes it (libm tanhf is ~30
 // VALU per element with range branches: at 32 elements per lane per row step the GELU backward
 // pass was partly VALU-bound instead of HBM-bound)
-template <bool FAST = true>
+// 1 - 2 / (e + 1): RCP = v_rcp_f32 (1 ulp) instead of the IEEE division sequence
+template <bool RCP>
+__device__ __forceinline__ float tanh_from_exp(float e) {
+  if constexpr (RCP) return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+  else return 1.f - 2.f / (e + 1.f);
+}
+
+template <bool FAST = true, bool RCP = true>
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
   const float u = k0 * (x + k1 * x2 * x);
   float t;
   if constexpr (FAST) {
-    t = 1.f - 2.f / (__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.f);
+    t = tanh_from_exp<RCP>(__builtin_amdgcn_exp2f(2.8853900817779268f * u));
   } else {
     t = tanhf(u);
   }
@@ -39,17 +46,18 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 // y = gelu_tanh(x) with tanh(u) = 1 - 2 / (exp(2u) + 1) on v_exp (x -> +-inf gives +-1 exactly):
 // the standalone GELU forward pass after c_fc (hipBLASLt on gfx950 has no GELU epilogue that also
 // returns the pre-activation the backward needs, bench/lt_probe.py).
+template <bool RCP = true>
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * (x + k1 * x * x * x);
   const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * u);  // exp(2u) = 2^(2u log2 e)
-  const float t = 1.f - 2.f / (e + 1.f);
+  const float t = tanh_from_exp<RCP>(e);
   return 0.5f * x * (1.f + t);
 }
 
 // 8 elements per lane per access (16-byte loads/stores), 4 accesses in flight per lane,
 // grid-stride over the flat tensor.  HBM-bound: reads x, writes y, nothing else.
-template <int DT>
+template <int DT, bool RCP = true>
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                        int64_t n8) {
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh(v[u][j]);
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh<RCP>(v[u][j]);
       store8<DT>(y, (i + u * stride) * 8, v[u]);
     }
   }
@@ -69,7 +77,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
     float v[8];
     load8<DT>(x, i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh<RCP>(v[j]);
     store8<DT>(y, i * 8, v);
   }
 }
@@ -85,7 +93,7 @@ __host__ __device__ inline BiasGeom bias_geom(int N) {
   return {tpr, kBiasLanes / tpr, (lanes + tpr - 1) / tpr};
 }
 
-template <int XDT, bool GELU, bool FAST = true>
+template <int XDT, bool GELU, bool FAST = true, bool RCP = true>
 __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
                                                                const void* __restrict__ pre, void* __restrict__ dp,
                                                                int64_t M, int N, float* __restrict__ partial) {
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad<FAST>(p[u][j]);
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad<FAST, RCP>(p[u][j]);
           store8<XDT>(dp, (r + u * step) * N + col, v[u]);
         }
       }
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
         float p[8];
         load8<XDT>(pre, r * N + col, p);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad<FAST>(p[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad<FAST, RCP>(p[j]);
         store8<XDT>(dp, r * N + col, v);
       }
 #pragma unroll
@@ -183,12 +191,19 @@ using namespace madnn;
 // re-read), the GELU variant, which also writes dp, at 4 (36.4/80.9/92.3 us vs 40.6/135/134 at 1).
 static int g_bias_wg_per_cu[2] = {1, 4};
 static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
+static int g_gelu_rcp = 1;        // A/B knob: v_rcp (1) or the IEEE division (0) in the exp2-based tanh
 
 extern "C" {
 
 int madnn_bias_tune(int gelu, int wg_per_cu) {
   const int old = g_bias_wg_per_cu[gelu ? 1 : 0];
   if (wg_per_cu > 0) g_bias_wg_per_cu[gelu ? 1 : 0] = wg_per_cu;
+  return old;
+}
+
+int madnn_gelu_rcp(int on) {
+  const int old = g_gelu_rcp;
+  if (on >= 0) g_gelu_rcp = on != 0;
   return old;
 }
 
@@ -219,7 +234,8 @@ hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
   MADNN_DISPATCH_DT(dt, DT, {
-    hipLaunchKernelGGL((gelu_fwd_kernel<DT>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
   });
   return hipGetLastError();
 }
@@ -233,9 +249,12 @@ hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M,
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre && g_bias_fast_tanh) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
-                         partial);
+    if (pre && g_bias_fast_tanh && g_gelu_rcp) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
+                         N, partial);
+    } else if (pre && g_bias_fast_tanh) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, false>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
+                         M, N, partial);
     } else if (pre) {
       hipLaunchKernelGGL((bias_grad_kernel<XDT, true, false>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
                          N, partial);
