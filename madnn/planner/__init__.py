@@ -149,6 +149,12 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         example_input = infer_example_input(model)
     dtype = torch_dtype(cfg.dtype)
     measured = False
+    B = global_batch or cfg.extra.get("global_batch")
+    if not B:
+        if not explicit_input:
+            get_logger().warning("madnn planner: no example_input / global_batch given; assuming %d sample(s) per "
+                                 "GPU for microbatch and activation sizing", example_input.shape[0])
+        B = max(example_input.shape[0], 1) * world
     if costs is None:
         costs = estimate(spine, example_input, dtype=dtype, machine=hw)
         import torch.distributed as dist
@@ -156,7 +162,9 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         multi = dist.is_initialized() and dist.get_world_size() > 1
         if _want_measure(cfg) and (not multi or dist.get_rank() == 0):
             try:
-                mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input)
+                per_gpu = max(int(B) // max(world, 1), 1) if (explicit_input or global_batch
+                                                              or cfg.extra.get("global_batch")) else None
+                mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input, per_gpu)
                 costs = measure_layers(spine, example_input, costs, batch=mb, dtype=dtype)
             except Exception as e:  # noqa: BLE001 - the analytic model still plans
                 get_logger().warning("madnn planner: layer measurement failed (%s); using analytic costs", e)
@@ -167,12 +175,6 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
             for c, (f, b, m) in zip(costs, obj[0]):
                 c.fwd_s, c.bwd_s, c.measured = f, b, m
     measured = all(c.measured for c in costs)
-    B = global_batch or cfg.extra.get("global_batch")
-    if not B:
-        if not explicit_input:
-            get_logger().warning("madnn planner: no example_input / global_batch given; assuming %d sample(s) per "
-                                 "GPU for microbatch and activation sizing", example_input.shape[0])
-        B = max(example_input.shape[0], 1) * world
     opt = _opt_kind(optimizer)
     cap = hw.hbm_gb * cfg.mem_headroom * 1e9
     L = len(spine)
@@ -210,12 +212,19 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     return plan
 
 
-def _default_measure_batch(example_input: torch.Tensor) -> int:
-    """Per-layer timing batch: enough work per launch for realistic kernel efficiency."""
+def _default_measure_batch(example_input: torch.Tensor, per_gpu: Optional[int] = None) -> int:
+    """Per-layer timing batch.  Per-sample costs fall steeply with the batch (a ResNet-50 layer at
+    32 images runs at ~1/6 of its batch-2048 efficiency), so when the job's per-GPU batch is known
+    the layers are timed at that batch, capped at 256 images / 32k tokens / 1024 rows to bound the
+    probe's memory and time; otherwise at a small default (~4k tokens, 32 images, 64 rows)."""
     per = int(torch.tensor(example_input.shape[1:]).prod()) if example_input.dim() > 1 else 1
-    if example_input.dtype in (torch.long, torch.int32):  # token ids: ~4k tokens
-        return max(1, min(16, 4096 // max(per, 1)))
-    return 32 if example_input.dim() == 4 else 64
+    if example_input.dtype in (torch.long, torch.int32):  # token ids
+        base, cap = max(1, min(16, 4096 // max(per, 1))), max(1, 32768 // max(per, 1))
+    elif example_input.dim() == 4:
+        base, cap = 32, 256
+    else:
+        base, cap = 64, 1024
+    return max(1, min(int(per_gpu), cap)) if per_gpu else base
 
 
 def _allowed(forced: str, pp: int, dp: int, world: int, pp_stages) -> bool:
