@@ -103,7 +103,8 @@ class Bottleneck(nn.Module):
     def _bn1_conv2(self, y, st):
         """conv2(relu(bn1(y))): with conv2 on K13, bn1's backward reduction is taken in conv2's
         data-grad epilogue (ops.bn_relu_conv3x3); the stride-2 conv2s stay on the module path."""
-        if isinstance(self.bn1, BN) and isinstance(self.conv2, FusedConv2d) and self.conv2._k13(y) \
+        if isinstance(y, torch.Tensor) and isinstance(self.bn1, BN) and isinstance(self.conv2, FusedConv2d) \
+                and self.conv2._k13(y) \
                 and bn_relu_conv3x3_supported(y, self.bn1, self.conv2.weight):
             return bn_relu_conv3x3(y, self.bn1, self.conv2.weight, stats_in=st, stats=True)
         out = self.bn1(y, relu=True, stats=st)
@@ -112,7 +113,8 @@ class Bottleneck(nn.Module):
     def _bn2_conv3(self, y, st):
         """conv3(relu(bn2(y))): on K9 the bn2 apply + ReLU run in conv3's operand prologue
         (forward and weight grad), so relu(bn2(y)) is never written to HBM."""
-        if isinstance(self.bn2, BN) and isinstance(self.conv3, FusedConv2d) and self.conv3._k9(y) \
+        if isinstance(y, torch.Tensor) and isinstance(self.bn2, BN) and isinstance(self.conv3, FusedConv2d) \
+                and self.conv3._k9(y) \
                 and (bn_relu_conv1x1_supported(y, self.bn2, self.conv3.weight)
                      or bn_relu_conv1x1_epi_supported(y, self.bn2, self.conv3.weight)):
             # K9 BN prologue (opt-in) or bn2's backward reduction in conv3's K9 data-grad epilogue

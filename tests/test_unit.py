@@ -217,6 +217,19 @@ def test_fx_spine_composes_to_model():
     torch.testing.assert_close(run_spine(sp, x), m(x))
 
 
+def test_fx_spine_resnet50_bottleneck_fusions():
+    """ResNet-50's bottlenecks (dual downsample BN, bn -> conv fusions) stay fx-traceable: the fused
+    paths are skipped for proxies and the spine still composes to the model."""
+    from madnn.models import resnet50
+    from madnn.planner.trace import _fx_split, run_spine
+
+    m = resnet50(num_classes=7).eval()
+    sp = _fx_split(m)
+    assert sp is not None and sp.source == "fx" and len(sp) > 16
+    x = torch.randn(2, 3, 64, 64)
+    torch.testing.assert_close(run_spine(sp, x), m(x))
+
+
 def test_declared_spine_and_block_list():
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.planner.trace import run_spine, trace
