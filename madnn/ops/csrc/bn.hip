@@ -46,10 +46,11 @@ struct BnGeom {
 //  hoist: load each lane's per-channel coefficients once per walk when its channels never change
 //    (grid stride a multiple of C); 0 reloads them per chunk (A/B)
 //  (re-measured at batch 2048 after the coefficient hoisting, profiles/r2_ab_bn_wg*.json: 4 workgroups
-//  per CU beat 8 by 1.2 % and 16 lost 0.7 %; the reverse walk is neutral there, 0.1 %)
+//  per CU beat 8 by 1.2 % and 16 lost 0.7 %; against 4, 3 gained 1.6 %, 2 gained 1.3 %, 6 lost 0.7 %;
+//  the reverse walk is neutral there, 0.1 %)
 struct BnTune {
   int reverse = 1;
-  int wg_per_cu = 4;
+  int wg_per_cu = 3;
   int hoist = 1;
   int unroll = 0;  // 1: apply walks handle two chunks per trip (more loads in flight)
 };
