@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp"])
+    ap.add_argument("--switch", default="lt_res", choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp", "native"])
+    ap.add_argument("--native", default="", help="FUNC:KEY:ON:OFF -- a native tunable, e.g. madnn_norm_tune:1:4:2")
     a = ap.parse_args()
     import madnn
     from madnn import ops
@@ -48,6 +49,11 @@ def main():
             import ctypes
 
             ctypes.CDLL(str(ops.kernels_path())).madnn_bias_fast_tanh(1 if on else 0)
+        elif a.switch == "native":
+            import ctypes
+
+            fn, key, von, voff = a.native.split(":")
+            getattr(ctypes.CDLL(str(ops.kernels_path())), fn)(int(key), int(von if on else voff))
         elif a.switch == "gelu_rcp":
             import ctypes
 
@@ -70,7 +76,7 @@ def main():
         arm = (w % 2 == 0)
         set_arm(arm)
         res[arm].append(window(a.steps))
-    out = {"switch": a.switch, "batch": a.batch, "on_ms": res[True], "off_ms": res[False],
+    out = {"switch": a.switch, "native": a.native, "batch": a.batch, "on_ms": res[True], "off_ms": res[False],
            "on_median": statistics.median(res[True]), "off_median": statistics.median(res[False]),
            "lt_failed": {str(k): str(v)[:100] for k, v in ops._LT_FAILED.items()}}
     out["gain_pct"] = 100.0 * (out["off_median"] - out["on_median"]) / out["off_median"]

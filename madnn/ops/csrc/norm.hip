@@ -280,7 +280,19 @@ static NormCfg pick_cfg(int H) {
 
 }  // namespace madnn
 
+// launch grids (A/B knobs, madnn_norm_tune): forward workgroups per CU (grid-stride over rows beyond),
+// backward workgroups per CU (each writes one dgamma/dbeta partial row)
+static int g_norm_fwd_wg = 16, g_norm_bwd_wg = 2;
+
 extern "C" {
+
+int madnn_norm_tune(int key, int value) {
+  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : nullptr;
+  if (f == nullptr) return -1;
+  const int old = *f;
+  if (value > 0) *f = value;
+  return old;
+}
 
 int madnn_norm_max_h() { return 16384; }
 
@@ -294,7 +306,7 @@ hipError_t madnn_norm_fwd(const void* x, const void* res, const void* w, const v
     MADNN_NORM_CFG(H, TPR, NC, {
       constexpr int RPB = kNormThreads / TPR;
       int64_t blocks = (rows + RPB - 1) / RPB;
-      const int grid = blocks > 16 * kNumCU ? 16 * kNumCU : (int)blocks;
+      const int grid = blocks > g_norm_fwd_wg * kNumCU ? g_norm_fwd_wg * kNumCU : (int)blocks;
       hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w, b,
                          y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
     });
@@ -308,7 +320,7 @@ int64_t madnn_norm_bwd_workspace(int64_t rows, int H) {
   NormCfg c = pick_cfg(H);
   const int RPB = kNormThreads / c.tpr;
   int64_t blocks = (rows + RPB - 1) / RPB;
-  int64_t G = blocks < 2 * kNumCU ? blocks : 2 * kNumCU;
+  int64_t G = blocks < (int64_t)g_norm_bwd_wg * kNumCU ? blocks : (int64_t)g_norm_bwd_wg * kNumCU;
   if (G < 1) G = 1;
   return G * 2 * (int64_t)H;
 }
