@@ -281,8 +281,10 @@ static NormCfg pick_cfg(int H) {
 }  // namespace madnn
 
 // launch grids (A/B knobs, madnn_norm_tune): forward workgroups per CU (grid-stride over rows beyond),
-// backward workgroups per CU (each writes one dgamma/dbeta partial row)
-static int g_norm_fwd_wg = 16, g_norm_bwd_wg = 2;
+// backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
+// (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
+// +0.5 % over 16 (4: -0.1 %)
+static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4;
 
 extern "C" {
 
