@@ -189,7 +189,9 @@ using namespace madnn;
 // M = 16384 (profiles/r1_linear_ab.json): the plain column sum is fastest at 1 workgroup per CU
 // (N=1024/3072/4096: 11.6/20.2/23.3 us vs 17.4/24.2/28.6 at 4: fewer partial rows to write and
 // re-read), the GELU variant, which also writes dp, at 4 (36.4/80.9/92.3 us vs 40.6/135/134 at 1).
-static int g_bias_wg_per_cu[2] = {1, 4};
+// Round 2, GPT-2 medium at 64 x 1024 (M = 65536; profiles/r2_ab_madnn_bias_tune_*.json): the plain sum at
+// 2 per CU is 1.0 % faster per step than at 1 (4: +0.8 %); the GELU variant stays at 4 (2: +0.1 %, 8: -0.4 %).
+static int g_bias_wg_per_cu[2] = {2, 4};
 static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
 static int g_gelu_rcp = 1;        // A/B knob: v_rcp (1) or the IEEE division (0) in the exp2-based tanh
 
