@@ -37,12 +37,14 @@ def main():
 
     arm_val = {True: val(a.on), False: val(a.off)}
     mod_name, attr = a.flag.split(":")
-    if mod_name == "bn_tune":   # a native BN tunable (madnn_bn_tune key), e.g. bn_tune:2
+    if mod_name == "bn_tune" or mod_name.startswith("native."):
+        # a native tunable: bn_tune:KEY (madnn_bn_tune) or native.FUNC:KEY, e.g. native.madnn_conv1x1_tune:0
         import ctypes
 
         madnn_mod = importlib.import_module("madnn.ops")
         madnn_mod.load_kernels()
-        tune = ctypes.CDLL(str(madnn_mod.kernels_path())).madnn_bn_tune
+        fname = "madnn_bn_tune" if mod_name == "bn_tune" else mod_name[len("native."):]
+        tune = getattr(ctypes.CDLL(str(madnn_mod.kernels_path())), fname)
 
         class _Native:
             def __setattr__(self, k, v):
