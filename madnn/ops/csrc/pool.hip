@@ -411,6 +411,17 @@ hipError_t madnn_maxpool_bwd(const void* dy, const void* arg, void* dx, int N, i
 }
 
 
+// fused stem BN + pool grids, workgroups per CU (A/B knobs, madnn_pool_bn_tune): 0 forward, 1 backward
+// reduction, 2 backward apply
+static int g_pool_bn_wg[3] = {16, 8, 16};
+
+int madnn_pool_bn_tune(int key, int value) {
+  if (key < 0 || key > 2) return -1;
+  const int old = g_pool_bn_wg[key];
+  if (value > 0) g_pool_bn_wg[key] = value;
+  return old;
+}
+
 int madnn_pool_bn_supported(int64_t numel, int C) {
   return numel < (1ll << 31) && C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0;
 }
@@ -420,7 +431,7 @@ hipError_t madnn_pool_bn_fwd(const void* x, const float* scale, const float* shi
                              int W, int C, int Ho, int Wo, int p, hipStream_t stream) {
   if (!madnn_pool_bn_supported((int64_t)N * H * W * C, C) || p > 2) return hipErrorInvalidValue;
   const int64_t work = (int64_t)N * Ho * Wo * (C / 8);
-  const int grid = stream_grid(work, 256, 16 * kNumCU);
+  const int grid = stream_grid(work, 256, g_pool_bn_wg[0] * kNumCU);
   hipLaunchKernelGGL((maxpool_k3s2_fwd_kernel<kBF16, true>), dim3(grid), dim3(256), 0, stream, x, y,
                      static_cast<uint64_t*>(arg), N, H, W, C, Ho, Wo, p, 0, scale, shift);
   return hipGetLastError();
@@ -433,7 +444,7 @@ hipError_t madnn_bn_bwd_finalize(const float* partial, int G, int C, int pstride
 // partial rows the fused backward's reduction writes
 int madnn_pool_bn_bwd_rows(int64_t pixels, int C) {
   const int64_t work = pixels * (C / 8);
-  return stream_grid(work, 256, 8 * kNumCU);  // gather-latency-bound: 8 workgroups per CU in flight
+  return stream_grid(work, 256, g_pool_bn_wg[1] * kNumCU);  // gather-latency-bound: 8 workgroups per CU in flight
 }
 
 // dy (and the BN weight/bias grads) from the pool output gradient dp: reduction, finalize, apply.
@@ -451,7 +462,7 @@ hipError_t madnn_pool_bn_bwd(const void* dp, const void* arg, const void* y, con
   MADNN_HIP_CHECK(hipGetLastError());
   MADNN_HIP_CHECK(madnn_bn_bwd_finalize(workspace, G, C, 2 * C, C, pixels, w, mean, invstd, dw, db, coef, coef + C,
                                         coef + 2 * C, stream));
-  const int grid = stream_grid(pixels * (C / 8), 256, 16 * kNumCU);
+  const int grid = stream_grid(pixels * (C / 8), 256, g_pool_bn_wg[2] * kNumCU);
   hipLaunchKernelGGL((pool_bn_bwd_kernel<1>), dim3(grid), dim3(256), 0, stream, dp, a, y, scale, shift, coef, coef + C,
                      coef + 2 * C, dy, nullptr, N, H, W, C, Ho, Wo, p);
   return hipGetLastError();
