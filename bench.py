@@ -73,6 +73,11 @@ def parse():
                     help="process-group backend override (default: nccl=RCCL on cuda, gloo on cpu); gloo on cuda "
                          "lets tests run several ranks on one GPU, which RCCL refuses")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--std-batch", type=int, default=512,
+                    help="also time ResNet-50 at this standard per-GPU batch (config.std_batch; 0 = skip)")
+    ap.add_argument("--gpt2-timeout", type=float, default=420.0,
+                    help="seconds the GPT-2 phase may take before it is reported as an error (below the 600 s "
+                         "process-group timeout, whose watchdog would abort the process first)")
     ap.add_argument("--miopen-benchmark", type=int, default=0,
                     help="torch.backends.cudnn.benchmark (MIOpen find).  Both modes read the shipped MI355X "
                          "find-db (madnn/tuning/miopen, seeded by madnn.init), so 0 already runs the tuned solvers")
@@ -272,31 +277,93 @@ def main():
             "config": config,
         }
         _release()
+        if args.std_batch and args.std_batch != config["per_gpu_batch"]:
+            # the same measurement at a standard per-GPU batch, so rounds compare like for like
+            sargs = argparse.Namespace(**dict(vars(args), batch=args.std_batch))
+            sdt, sps_step, _ = bench_resnet(sargs, world, rank)
+            sdt = _max_over_ranks(sdt)
+            res["config"]["std_batch"] = {"per_gpu_batch": args.std_batch, "global_batch": sps_step,
+                                          "value": round(sps_step * args.steps / sdt, 2),
+                                          "ms_per_step": round(sdt / args.steps * 1000.0, 3)}
+            _release()
     if args.model in ("all", "gpt2-medium"):
         if args.model == "all":
             import gc
 
             gc.collect()
-        dt, steps, gbatch, info = bench_gpt2(args, world, rank)
-        dt = _max_over_ranks(dt)
-        sps = gbatch * steps / dt
-        g = dict(info, samples_per_s=round(sps, 2), tokens_per_s=round(sps * args.seq_len, 1),
-                 ms_per_step=round(dt / steps * 1000.0, 3), n_gpus=world, scaling="weak",
-                 dtype="bf16" if on_gpu else "fp32", data="synthetic (random tokens, random-init weights)")
+        g = _gpt2_phase(args, world, rank, on_gpu, res)
         if res is None:
-            res = {"metric": METRIC, "value": round(sps, 2), "unit": "samples/s", "n_gpus": world, "steps": steps,
-                   "warmup": info["warmup"], "ms_per_step": g["ms_per_step"], "higher_is_better": True,
-                   "scaling": "weak", "vs_baseline": None, "dtype": g["dtype"], "data": g["data"],
-                   "config": {"model": args.gpt2_config, "global_batch": gbatch, "seq_len": args.seq_len,
-                              "parallelism": info["parallelism"]}}
+            res = {"metric": METRIC, "value": g.get("samples_per_s"), "unit": "samples/s", "n_gpus": world,
+                   "steps": g.get("steps", args.steps), "warmup": g.get("warmup", args.warmup),
+                   "ms_per_step": g.get("ms_per_step"), "higher_is_better": True, "scaling": "weak",
+                   "vs_baseline": None, "dtype": g["dtype"], "data": g["data"],
+                   "config": {"model": args.gpt2_config, "global_batch": g.get("global_batch"),
+                              "seq_len": args.seq_len, "parallelism": g.get("parallelism")}}
         res["gpt2_pp"] = g
+        if "error" in g:
+            # peers may be stuck inside the failed phase: no collective teardown.  Only rank 0
+            # prints; the others wait for its line (its watchdog fires at the latest after
+            # --gpt2-timeout) because a launcher tears the whole job down at the first exit.
+            if rank == 0:
+                _emit(res, rank, args)
+            else:
+                time.sleep(args.gpt2_timeout + 60)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(3)
+    _emit(res, rank, args)
+    madnn.shutdown()
+
+
+def _emit(res, rank, args):
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    madnn.shutdown()
+
+
+def _gpt2_phase(args, world, rank, on_gpu, res):
+    """The GPT-2 half as its own failure domain: an exception, or no result within
+    ``--gpt2-timeout`` seconds (a hang inside a collective), yields ``{"error": ...}`` and the
+    already measured ResNet value is still printed (rank 0's watchdog prints it and ends the
+    process if the phase never returns)."""
+    import threading
+
+    base = {"model": args.gpt2_config, "n_gpus": world, "scaling": "weak", "dtype": "bf16" if on_gpu else "fp32",
+            "data": "synthetic (random tokens, random-init weights)"}
+    strategy, stages, par = gpt2_layout(world)
+    base["parallelism"] = par
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(args.gpt2_timeout):
+            return
+        out = dict(res or {"metric": METRIC, "value": None, "n_gpus": world})
+        out["gpt2_pp"] = dict(base, error=f"timeout: GPT-2 phase did not finish within {args.gpt2_timeout:.0f} s")
+        print(f"bench: rank {rank}: GPT-2 phase timed out after {args.gpt2_timeout:.0f} s", file=sys.stderr,
+              flush=True)
+        _emit(out, rank, args)
+        sys.stdout.flush()
+        os._exit(3)
+
+    wd = threading.Thread(target=watchdog, daemon=True)
+    wd.start()
+    fault = os.environ.get("MADNN_BENCH_GPT2_FAULT")
+    if fault:  # madnn's fault injection (MADNN_FAULT=rank:step:kind), armed for this phase only
+        os.environ["MADNN_FAULT"] = fault
+    try:
+        dt, steps, gbatch, info = bench_gpt2(args, world, rank)
+        dt = _max_over_ranks(dt)
+    except Exception as e:  # noqa: BLE001
+        done.set()
+        print(f"bench: rank {rank}: GPT-2 phase failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        return dict(base, error=f"{type(e).__name__}: {str(e)[:300]}")
+    done.set()
+    sps = gbatch * steps / dt
+    return dict(base, **info, samples_per_s=round(sps, 2), tokens_per_s=round(sps * args.seq_len, 1),
+                ms_per_step=round(dt / steps * 1000.0, 3))
 
 
 if __name__ == "__main__":

@@ -229,8 +229,284 @@ def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_
 
 
 # ----------------------------------------------------------------------------
+# channel layout (shared by build_pipeline and the transport simulation)
+# ----------------------------------------------------------------------------
+def p2p_channel_specs(nstages: int, nchunks: int = 1) -> List[tuple]:
+    """The one-directional channels of one pipeline replica, in creation order, as
+    ``(name at the sender, name at the receiver, sender stage, receiver stage)``: activations
+    on every edge s -> s+1, gradients on every edge s+1 -> s, and with V > 1 the ring edge
+    (activations S-1 -> 0 between chunks, their gradients 0 -> S-1)."""
+    S = nstages
+    specs = [("act_out", "act_in", e, e + 1) for e in range(S - 1)]
+    specs += [("grad_out", "grad_in", e + 1, e) for e in range(S - 1)]
+    if nchunks > 1:
+        specs += [("act_out_wrap", "act_in_wrap", S - 1, 0), ("grad_out_wrap", "grad_in_wrap", 0, S - 1)]
+    return specs
+
+
+def p2p_group_layout(nstages: int, nchunks: int, dp: int, rank_of: Callable[[int, int], int],
+                     layout: str = "pairwise") -> List[tuple]:
+    """The process groups that carry the pipeline channels, in creation order (every rank must
+    call ``new_group`` for all of them, members or not), as ``(ranks, [(replica, spec), ...])``.
+
+    ``pairwise`` (the engine's layout): ONE 2-rank group per channel, i.e. per (edge,
+    direction, replica).  On RCCL with eager initialisation an unbatched send/recv is executed
+    like a collective, in issue order with every other op on its communicator; a group with a
+    single sender and a single receiver is therefore a true FIFO whose pre-posted receives can
+    never block a send of the same rank.  ``shared`` (round-2 layout, kept only so the transport
+    tests can show that it deadlocks): one S-rank group per channel kind and replica, where an
+    interior rank's sends queue behind its own pre-posted receives."""
+    specs = p2p_channel_specs(nstages, nchunks)
+    out = []
+    if layout == "pairwise":
+        for d in range(dp):
+            for sp in specs:
+                out.append(((rank_of(d, sp[2]), rank_of(d, sp[3])), [(d, sp)]))
+    elif layout == "shared":
+        kinds = ["act", "grad"] + (["act_wrap", "grad_wrap"] if nchunks > 1 else [])
+        for kind in kinds:
+            for d in range(dp):
+                carried = [(d, sp) for sp in specs if sp[0].replace("_out", "") == kind]
+                out.append((tuple(rank_of(d, s) for s in range(nstages)), carried))
+    else:
+        raise ValueError(f"unknown pipeline channel layout {layout!r}")
+    return out
+
+
+def recv_plan(order, vstages: List[int], nvirtual: int) -> List[tuple]:
+    """Every receive one pipeline rank makes in a step, in issue order: ``("act", c, m)`` before
+    the forward of virtual stage c*S+rank (unless it is the first), ``("grad", c, m)`` before the
+    backward of every virtual stage but the last.  The engine pre-posts exactly this list."""
+    out = []
+    for op, c, m in order:
+        vs = vstages[c]
+        if op == "F" and vs > 0:
+            out.append(("act", c, m))
+        elif op == "B" and vs < nvirtual - 1:
+            out.append(("grad", c, m))
+    return out
+
+
+def _chan_names(stage: int, nstages: int):
+    """This rank's channel names: (act in, act out, grad in, grad out)."""
+    return ("act_in" if stage > 0 else "act_in_wrap", "act_out" if stage < nstages - 1 else "act_out_wrap",
+            "grad_in" if stage < nstages - 1 else "grad_in_wrap", "grad_out" if stage > 0 else "grad_out_wrap")
+
+
+def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, layout: str = "pairwise",
+                       prepost: bool = True, t_fwd: float = 1.0, t_bwd: float = 2.0, t_p2p: float = 0.0) -> dict:
+    """Replay one training step of every pipeline rank against the COMMUNICATORS
+    :func:`p2p_group_layout` builds, with RCCL's eager-initialisation semantics.
+
+    Model: each rank has a compute stream and one stream per communicator it belongs to; all of
+    a rank's operations on one communicator execute in issue order (unbatched P2P is serialised
+    like a collective).  The host issues, in program order, the receives of :func:`recv_plan`
+    (all up front when ``prepost``; otherwise each right before its consumer, preceded by the
+    shape header that the first step of a new input signature exchanges with a host-blocking
+    receive), every forward/backward on the compute stream (waiting on its receive), and each
+    send on its channel's communicator right after its producer.  A send completes only
+    together with the matching receive at the head of the peer's stream (rendezvous, the
+    conservative reading of RCCL's P2P protocol).  Raises RuntimeError on a deadlock or when a
+    receive would be matched with a message meant for another receive; otherwise returns
+    ``{"makespan", "bubble", "communicators"}``."""
+    S, M, V = nstages, nmicro, nchunks
+    SV = S * V
+    groups = p2p_group_layout(S, V, 1, lambda d, s: s, layout)
+    comm_of: Dict[tuple, int] = {}
+    for gi, (_ranks, carried) in enumerate(groups):
+        for _d, (n_src, n_dst, a, b) in carried:
+            comm_of[(a, n_src)] = gi
+            comm_of[(b, n_dst)] = gi
+    ops: List[dict] = []           # every op: kind C/S/R, rank, stream, deps, payload
+
+    def new(kind_, rank, stream, **kw):
+        ops.append(dict(kind=kind_, rank=rank, stream=stream, done=None, **kw))
+        return len(ops) - 1
+
+    programs = []                  # per rank: list of ("issue", op id) / ("hostwait", op id)
+    for s in range(S):
+        order = native_runtime.pipeline_order(kind, s, S, M, V)
+        vst = [virtual_stage(c, s, S) for c in range(V)]
+        a_in, a_out, g_in, g_out = _chan_names(s, S)
+        prog = []
+        recv_id: Dict[tuple, int] = {}
+        met_in, met_out = set(), set()
+
+        def post(key, s=s, a_in=a_in, g_in=g_in, vst=vst, recv_id=recv_id, prog=prog):
+            k, c, m = key
+            name = a_in if k == "act" else g_in
+            peer = (s - 1) % S if k == "act" else (s + 1) % S
+            msg = (k, vst[c], m)
+            recv_id[key] = new("R", s, ("comm", comm_of[(s, name)]), peer=peer, msg=msg)
+            prog.append(("issue", recv_id[key]))
+
+        if prepost:
+            for key in recv_plan(order, vst, SV):
+                post(key)
+        for op, c, m in order:
+            vs = vst[c]
+            dep = None
+            if op == "F" and vs > 0 or op == "B" and vs < SV - 1:
+                key = ("act" if op == "F" else "grad", c, m)
+                if not prepost:
+                    if op == "F" and c not in met_in:   # shape header, host-blocking
+                        met_in.add(c)
+                        h = new("R", s, ("comm", comm_of[(s, a_in)]), peer=(s - 1) % S, msg=("hdr", vs, c))
+                        prog.append(("issue", h))
+                        prog.append(("hostwait", h))
+                    post(key)
+                dep = recv_id[key]
+            cid = new("C", s, ("compute",), dep=dep, dur=t_fwd if op == "F" else t_bwd)
+            prog.append(("issue", cid))
+            if op == "F" and vs < SV - 1:
+                if not prepost and c not in met_out:
+                    met_out.add(c)
+                    prog.append(("issue", new("S", s, ("comm", comm_of[(s, a_out)]), peer=(s + 1) % S,
+                                              msg=("hdr", vs + 1, (vs + 1) // S), dep=cid)))
+                prog.append(("issue", new("S", s, ("comm", comm_of[(s, a_out)]), peer=(s + 1) % S,
+                                          msg=("act", vs + 1, m), dep=cid)))
+            elif op == "B" and vs > 0:
+                prog.append(("issue", new("S", s, ("comm", comm_of[(s, g_out)]), peer=(s - 1) % S,
+                                          msg=("grad", vs - 1, m), dep=cid)))
+        programs.append(prog)
+
+    pc = [0] * S
+    queues: Dict[tuple, list] = {}   # (rank, stream) -> op ids in issue order (FIFO)
+    free: Dict[tuple, float] = {}
+    busy = [0.0] * S
+    remaining = len(ops)
+
+    def head(rank, stream):
+        q = queues.get((rank, stream))
+        return q[0] if q else None
+
+    while remaining:
+        progressed = False
+        for s in range(S):               # the host issues until it reaches an unfinished wait
+            prog = programs[s]
+            while pc[s] < len(prog):
+                what, oid = prog[pc[s]]
+                if what == "hostwait":
+                    if ops[oid]["done"] is None:
+                        break
+                else:
+                    queues.setdefault((s, ops[oid]["stream"]), []).append(oid)
+                pc[s] += 1
+                progressed = True
+        for (s, stream), q in list(queues.items()):
+            while q:
+                o = ops[q[0]]
+                if o["kind"] == "C":
+                    if o["dep"] is not None and ops[o["dep"]]["done"] is None:
+                        break
+                    start = max(free.get((s, stream), 0.0), ops[o["dep"]]["done"] if o["dep"] is not None else 0.0)
+                    o["done"] = start + o["dur"]
+                    busy[s] += o["dur"]
+                elif o["kind"] == "S":
+                    if ops[o["dep"]]["done"] is None:
+                        break
+                    ph = head(o["peer"], stream)
+                    if ph is None or ops[ph]["kind"] != "R" or ops[ph]["peer"] != s:
+                        break
+                    r = ops[ph]
+                    if r["msg"] != o["msg"]:
+                        raise RuntimeError(f"transport {layout} {kind} S={S} M={M} V={V}: rank {o['peer']} "
+                                           f"receives {o['msg']} where it expects {r['msg']}")
+                    start = max(free.get((s, stream), 0.0), free.get((o["peer"], stream), 0.0),
+                                ops[o["dep"]]["done"])
+                    o["done"] = r["done"] = start + t_p2p
+                    free[(o["peer"], stream)] = r["done"]
+                    queues[(o["peer"], stream)].pop(0)
+                    remaining -= 1
+                else:
+                    break                # a receive completes with its matching send
+                free[(s, stream)] = o["done"]
+                q.pop(0)
+                remaining -= 1
+                progressed = True
+        if not progressed:
+            stuck = {}
+            for (s, stream), q in queues.items():
+                if q:
+                    o = ops[q[0]]
+                    stuck.setdefault(s, []).append((stream, o["kind"], o.get("msg")))
+            raise RuntimeError(f"pipeline transport {layout} {kind} S={S} M={M} V={V} deadlocks; "
+                               f"stream heads: {stuck}")
+    makespan = max(o["done"] for o in ops)
+    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan if makespan else 0.0,
+            "communicators": len(groups)}
+
+
+# ----------------------------------------------------------------------------
 # transport
 # ----------------------------------------------------------------------------
+class _SerialWork:
+    """Completion handle of an op run by :class:`_SerialComm` (wait() raises on a timeout)."""
+
+    __slots__ = ("event", "error", "timeout")
+
+    def __init__(self, timeout):
+        import threading
+
+        self.event = threading.Event()
+        self.error = None
+        self.timeout = timeout
+
+    def wait(self):
+        if not self.event.wait(self.timeout):
+            raise RuntimeError(f"emulated RCCL P2P: operation not complete after {self.timeout:.0f} s "
+                               "(the communicator's FIFO is blocked: transport deadlock)")
+        if self.error is not None:
+            raise self.error
+        return True
+
+
+class _SerialComm:
+    """CPU test double of an eagerly initialised RCCL communicator: every point-to-point
+    operation on the group runs to completion, one at a time, in issue order, on one worker
+    thread (``MADNN_EMULATE_RCCL_P2P=1`` on gloo).  Gloo alone completes sends and receives of
+    different peers independently, which hides the serialisation RCCL imposes."""
+
+    _by_group: Dict[int, "_SerialComm"] = {}
+
+    def __init__(self, timeout):
+        import queue
+        import threading
+
+        self.q = queue.Queue()
+        self.timeout = timeout
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    @classmethod
+    def of(cls, group, timeout):
+        c = cls._by_group.get(id(group))
+        if c is None:
+            c = cls._by_group[id(group)] = cls(timeout)
+        return c
+
+    def _run(self):
+        while True:
+            fn, work = self.q.get()
+            try:
+                fn().wait()
+            except Exception as e:  # noqa: BLE001
+                work.error = e
+            work.event.set()
+
+    def submit(self, fn) -> _SerialWork:
+        w = _SerialWork(self.timeout)
+        self.q.put((fn, w))
+        return w
+
+
+def _emulated_p2p_timeout() -> Optional[float]:
+    import os
+
+    v = os.environ.get("MADNN_EMULATE_RCCL_P2P", "")
+    if v in ("", "0"):
+        return None
+    return float(os.environ.get("MADNN_EMULATE_RCCL_P2P_TIMEOUT", "60"))
 class _Pending:
     """A posted receive; ``get()`` orders the consumer after it (RCCL: a stream wait, no
     host block) and returns the tensor on the compute device."""
@@ -248,12 +524,15 @@ class _Pending:
 class Channel:
     """One-directional point-to-point FIFO between two pipeline ranks.
 
-    Each direction of each pipeline edge gets its OWN process group, hence its own RCCL
-    communicator and internal HIP stream, so a channel only ever carries messages one way
-    and in one order: receives can be posted ahead of time (the transfer then runs as soon
-    as the peer's send is enqueued, overlapping this rank's compute) and sends are never
-    waited on before the end of the step.  On a gloo group HIP tensors are staged through
-    host memory (tests run several ranks on one GPU that way; RCCL refuses that)."""
+    Its process group has exactly two ranks, the sender and the receiver
+    (:func:`p2p_group_layout`), so its RCCL communicator -- which executes unbatched
+    send/recv in issue order on its own HIP stream -- only ever carries messages one way and
+    in one order: receives can be posted ahead of time (the transfer runs as soon as the
+    peer's send is enqueued, overlapping this rank's compute) and sends are never waited on
+    before the end of the step.  On a gloo group HIP tensors are staged through host memory
+    (tests run several ranks on one GPU that way; RCCL refuses that); with
+    ``MADNN_EMULATE_RCCL_P2P=1`` gloo ops run through :class:`_SerialComm`, which imposes
+    RCCL's per-communicator serialisation on the CPU tests."""
 
     def __init__(self, group, src: int, dst: int, device, name: str = ""):
         self.group, self.src, self.dst, self.name = group, src, dst, name
@@ -261,23 +540,35 @@ class Channel:
         backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
         self.staged = backend == "gloo" and self.device.type == "cuda"
         self.buf_device = torch.device("cpu") if self.staged else self.device
+        t = _emulated_p2p_timeout() if backend == "gloo" else None
+        self.serial = _SerialComm.of(group, t) if t is not None else None
         self._sends = []
         self.bytes = 0
         self.messages = 0
+
+    def _isend(self, t):
+        if self.serial is not None:
+            return self.serial.submit(lambda: dist.isend(t, self.dst, group=self.group))
+        return dist.isend(t, self.dst, group=self.group)
+
+    def _irecv(self, buf):
+        if self.serial is not None:
+            return self.serial.submit(lambda: dist.irecv(buf, self.src, group=self.group))
+        return dist.irecv(buf, self.src, group=self.group)
 
     def send(self, t: torch.Tensor) -> None:
         t = t.detach().contiguous()
         if self.staged:
             t = t.cpu()
         comm._record("send", self.group, t)
-        self._sends.append((dist.isend(t, self.dst, group=self.group), t))
+        self._sends.append((self._isend(t), t))
         self.bytes += t.numel() * t.element_size()
         self.messages += 1
 
     def post_recv(self, shape, dtype) -> _Pending:
         buf = torch.empty(shape, dtype=dtype, device=self.buf_device)
         comm._record("recv", self.group, buf)
-        return _Pending(dist.irecv(buf, self.src, group=self.group), buf, self.device, self.staged)
+        return _Pending(self._irecv(buf), buf, self.device, self.staged)
 
     def send_meta(self, t: torch.Tensor) -> None:
         hdr = torch.zeros(10, dtype=torch.int64)
@@ -383,22 +674,10 @@ class PipelineEngine:
         RCCL builds a two-rank communicator on a pair's first send/recv and that build is a
         blocking rendezvous of the two ranks.  Doing it lazily inside the schedule would turn
         the first message of every channel into a synchronous handshake (the schedule is only
-        proven deadlock-free for non-blocking sends); here every rank walks the pipeline edges
-        in one global order -- channel kind, then edge index, the ring edge S-1 -> 0 last --
-        so the handshakes form a chain that always completes."""
-        order = ["act_out", "act_in", "grad_out", "grad_in", "act_out_wrap", "act_in_wrap", "grad_out_wrap",
-                 "grad_in_wrap"]
-        S = self.nstages
-
-        def edge(name):  # (kind, edge index) of this rank's end of the channel
-            kind = name.replace("_in", "").replace("_out", "")
-            if kind == "act":
-                return kind, (self.stage if name == "act_out" else self.stage - 1)
-            if kind == "grad":
-                return kind, (self.stage - 1 if name == "grad_out" else self.stage)
-            return kind, S - 1
-        ranked = sorted(self.channels, key=lambda n: (["act", "grad", "act_wrap", "grad_wrap"].index(edge(n)[0]),
-                                                      edge(n)[1], order.index(n)))
+        proven deadlock-free for non-blocking sends); here every rank walks its channels in
+        the global group-creation order (then edge index inside a group), so the handshakes
+        form a chain that always completes."""
+        ranked = sorted(self.channels, key=lambda n: getattr(self.channels[n], "warm_key", (0, 0)))
         for name in ranked:
             ch = self.channels[name]
             t = torch.zeros(1, device=ch.buf_device)
@@ -422,15 +701,15 @@ class PipelineEngine:
         return self.channels["grad_out" if self.stage > 0 else "grad_out_wrap"]
 
     def _prepost(self):
-        """Post every receive of the step, per channel in consumption order."""
-        S, SV = self.nstages, self.nstages * self.V
+        """Post every receive of the step (:func:`recv_plan`, the order
+        :func:`simulate_transport` proves deadlock-free on the channel groups)."""
         q = {}
-        for op, c, m in self.order:
-            vs = self._vs[c]
-            if op == "F" and vs > 0:
-                q[("act", c, m)] = self._act_in(c).post_recv(*self._in_meta[c])
-            elif op == "B" and vs < SV - 1:
-                q[("grad", c, m)] = self._grad_in(c).post_recv(*self._out_meta[c])
+        for key in recv_plan(self.order, self._vs, self.nstages * self.V):
+            k, c, _m = key
+            if k == "act":
+                q[key] = self._act_in(c).post_recv(*self._in_meta[c])
+            else:
+                q[key] = self._grad_in(c).post_recv(*self._out_meta[c])
         self.stats["prefetched_recvs"] += len(q)
         return q
 
@@ -723,38 +1002,27 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
             if rt.get_rank() in ranks:
                 tied_local.append((by_name[name], grp, ranks[0]))
 
-    # one-directional FIFO channels: a process group per direction per pipeline edge kind
+    # one-directional FIFO channels, one 2-rank process group each (p2p_group_layout); every
+    # rank creates every group in the same order
+    import os
+
+    layout = os.environ.get("MADNN_PP_P2P_LAYOUT", "pairwise")
     channels: Dict[str, Channel] = {}
     p2p_groups = []  # every channel group this rank belongs to (also those it sends nothing on)
-    kinds = ["act", "grad"] + (["act_wrap", "grad_wrap"] if V > 1 else [])
-    for kind in kinds:
-        for d in range(plan.dp):
-            ranks = [mesh.rank_of(d, s, 0) for s in range(S)]
-            grp = dist.new_group(ranks) if dist.is_initialized() else None
-            if rt.get_rank() not in ranks:
-                continue
-            p2p_groups.append(grp)
-            me = ranks[stage]
-            if kind == "act":
-                if stage > 0:
-                    channels["act_in"] = Channel(grp, ranks[stage - 1], me, dev, "act_in")
-                if stage < S - 1:
-                    channels["act_out"] = Channel(grp, me, ranks[stage + 1], dev, "act_out")
-            elif kind == "grad":
-                if stage < S - 1:
-                    channels["grad_in"] = Channel(grp, ranks[stage + 1], me, dev, "grad_in")
-                if stage > 0:
-                    channels["grad_out"] = Channel(grp, me, ranks[stage - 1], dev, "grad_out")
-            elif kind == "act_wrap":
-                if stage == 0:
-                    channels["act_in_wrap"] = Channel(grp, ranks[S - 1], me, dev, "act_in_wrap")
-                if stage == S - 1:
-                    channels["act_out_wrap"] = Channel(grp, me, ranks[0], dev, "act_out_wrap")
-            else:
-                if stage == S - 1:
-                    channels["grad_in_wrap"] = Channel(grp, ranks[0], me, dev, "grad_in_wrap")
-                if stage == 0:
-                    channels["grad_out_wrap"] = Channel(grp, me, ranks[S - 1], dev, "grad_out_wrap")
+    me = rt.get_rank()
+    for gidx, (ranks, carried) in enumerate(p2p_group_layout(S, V, plan.dp, lambda d, s: mesh.rank_of(d, s, 0),
+                                                             layout)):
+        grp = dist.new_group(list(ranks)) if dist.is_initialized() else None
+        if me not in ranks:
+            continue
+        p2p_groups.append(grp)
+        for d, (n_src, n_dst, a, b) in carried:
+            src, dst = mesh.rank_of(d, a, 0), mesh.rank_of(d, b, 0)
+            for name, mine in ((n_src, src), (n_dst, dst)):
+                if mine == me:
+                    ch = Channel(grp, src, dst, dev, name)
+                    ch.warm_key = (gidx, min(a, b))
+                    channels[name] = ch
 
     dtype, dtype_of, cl = prepare_model(stage_mod, cfg, dev)
     stage_params = [p for p in stage_mod.parameters() if p.requires_grad]

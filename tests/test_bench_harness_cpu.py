@@ -92,21 +92,65 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     assert res["gpt2_pp"]["microbatches"] == 4 and res["gpt2_pp"]["model"] == "gpt2-medium"
 
 
-def test_bench_py_gpt2_dp2_pp4_interleaved_eight_ranks_cpu():
-    """The 8-GPU layout of the GPT-2 half exactly as the driver's N=8 run builds it: GPT-2 medium,
-    dp2 x pp4, interleaved 1F1B with 2 model chunks per rank (short sequences, CPU/gloo)."""
+def _gpt2_8rank(extra_env=None, timeout=900):
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "1",
            "--device", "cpu", "--model", "gpt2-medium", "--gpt2-batch-per-gpu", "2", "--gpt2-mb", "1",
            "--seq-len", "16"]
-    env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING")
-    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING", **(extra_env or {}))
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
+
+
+def test_bench_py_gpt2_dp2_pp4_interleaved_eight_ranks_emulated_rccl():
+    """The 8-GPU layout of the GPT-2 half exactly as the driver's N=8 run builds it: GPT-2 medium,
+    dp2 x pp4, interleaved 1F1B with 2 model chunks per rank (short sequences, CPU/gloo) -- with
+    every pipeline group's point-to-point ops serialised in issue order, as eagerly initialised
+    RCCL communicators execute them (``MADNN_EMULATE_RCCL_P2P``)."""
+    out = _gpt2_8rank({"MADNN_EMULATE_RCCL_P2P": "1", "MADNN_EMULATE_RCCL_P2P_TIMEOUT": "120"})
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     res = json.loads(lines[0])
     pp = res["gpt2_pp"]
-    assert res["n_gpus"] == 8 and res["value"] > 0
+    assert res["n_gpus"] == 8 and res["value"] > 0 and "error" not in pp
     assert res["config"]["parallelism"] == "dp2xpp4"
     assert pp["schedule"] == "interleaved" and pp["virtual_stages"] == 2 and pp["microbatches"] == 8
+
+
+def test_bench_py_gpt2_shared_groups_deadlock_under_emulated_rccl():
+    """Regression check of the emulation itself: the round-2 channel layout (one 4-rank group per
+    channel kind) deadlocks at the first step with pre-posted receives, which bench.py reports as
+    a GPT-2 error instead of hanging."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1",
+           "--device", "cpu", "--model", "gpt2-medium", "--gpt2-config", "gpt2-tiny", "--gpt2-batch-per-gpu", "4",
+           "--seq-len", "16", "--microbatches", "16", "--schedule", "1f1b"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING", MADNN_EMULATE_RCCL_P2P="1",
+               MADNN_EMULATE_RCCL_P2P_TIMEOUT="15", MADNN_PP_P2P_LAYOUT="shared")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode != 0
+    assert "transport deadlock" in out.stderr or "timed out" in out.stderr, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "error" in json.loads(lines[0])["gpt2_pp"], out.stdout
+
+
+def test_bench_py_reports_resnet_when_gpt2_phase_fails():
+    """The two halves are separate failure domains: a fault in the GPT-2 phase still prints the
+    measured ResNet value (plus the standard-batch number) and exits non-zero."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--device", "cpu", "--batch", "4", "--std-batch", "2", "--image-size", "32", "--gpt2-config", "gpt2-tiny",
+           "--seq-len", "16", "--gpt2-batch-per-gpu", "2", "--gpt2-mb", "1", "--gpt2-timeout", "60"]
+    for fault in ("1:1:raise", "1:1:hang"):
+        env = dict(os.environ, OMP_NUM_THREADS="2", MADNN_LOG_LEVEL="WARNING", MADNN_BENCH_GPT2_FAULT=fault)
+        out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+        assert out.returncode != 0, fault
+        lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        assert len(lines) == 1, (fault, out.stdout, out.stderr[-2000:])
+        res = json.loads(lines[0])
+        assert res["value"] > 0 and res["config"]["parallelism"] == "dp2"
+        assert res["config"]["std_batch"]["per_gpu_batch"] == 2 and res["config"]["std_batch"]["value"] > 0
+        assert "error" in res["gpt2_pp"] and res["gpt2_pp"]["parallelism"] == "pp2", fault

@@ -122,6 +122,16 @@ def test_pp_interleaved_parity(S, M, V):
     run_dist(_w_pp, S, "gpt8" if S * V > 6 else "gpt", "interleaved", 1, M, 2, None, V)
 
 
+@pytest.mark.parametrize("schedule,dp,M,V", [("1f1b", 1, 8, None), ("interleaved", 1, 8, 2), ("gpipe", 1, 4, None)])
+def test_pp_4stages_parity_under_emulated_rccl(monkeypatch, schedule, dp, M, V):
+    """Same parity check with every channel group's P2P ops serialised in issue order, as
+    eagerly initialised RCCL communicators run them (3 steps: the 2nd and 3rd pre-post every
+    receive of the step)."""
+    monkeypatch.setenv("MADNN_EMULATE_RCCL_P2P", "1")
+    monkeypatch.setenv("MADNN_EMULATE_RCCL_P2P_TIMEOUT", "60")
+    run_dist(_w_pp, 4, "gpt8" if V else "gpt", schedule, dp, M, 3, None, V)
+
+
 def test_pp_clip_grad_norm_is_global_and_tied_counted_once():
     """clip_grad_norm_ + step with tied weights across stages: the tied sum is
     applied once, and the clip coefficient uses the whole model's norm."""

@@ -106,6 +106,53 @@ def test_pipeline_orders_deadlock_free_and_fifo(kind, V, S, M):
         assert r["bubble"] == pytest.approx((S - 1) / (M + S - 1), abs=1e-9)
 
 
+@pytest.mark.parametrize("S,V,dp", [(2, 1, 1), (4, 1, 2), (4, 2, 2), (8, 2, 1), (2, 3, 4)])
+def test_every_pipeline_p2p_group_has_two_ranks(S, V, dp):
+    """Each channel (edge, direction, replica) owns a 2-rank group: one sender, one receiver."""
+    from madnn.parallel.pp import p2p_channel_specs, p2p_group_layout
+
+    groups = p2p_group_layout(S, V, dp, lambda d, s: d * S + s)
+    assert len(groups) == dp * len(p2p_channel_specs(S, V)) == dp * (2 * (S - 1) + (2 if V > 1 else 0))
+    for ranks, carried in groups:
+        assert len(ranks) == 2 and len(set(ranks)) == 2 and len(carried) == 1
+        d, (_, _, a, b) = carried[0]
+        assert ranks == (d * S + a, d * S + b)
+    # every rank sends on exactly the channels it needs: interior stages 2 out + 2 in
+    for r in range(S * dp):
+        outs = [g for g, _ in groups if g[0] == r]
+        ins = [g for g, _ in groups if g[1] == r]
+        assert len(outs) == len(ins)
+
+
+@pytest.mark.parametrize("S", [2, 4, 8])
+@pytest.mark.parametrize("kind,V", [("gpipe", 1), ("1f1b", 1), ("interleaved", 2)])
+@pytest.mark.parametrize("M", [8, 16, 32])
+def test_pipeline_transport_serialised_per_communicator(S, kind, V, M):
+    """RCCL eager-init semantics (ops of one communicator execute in issue order, a send
+    completes only with its receive): the engine's 2-rank channel groups never deadlock, with
+    every receive of the step pre-posted (steady state) or posted just in time behind a
+    host-blocking shape header (first step of an input signature)."""
+    from madnn.parallel.pp import simulate_schedule, simulate_transport
+
+    for prepost in (True, False):
+        r = simulate_transport(kind, S, M, V, "pairwise", prepost)
+        assert r["communicators"] == 2 * (S - 1) + (2 if V > 1 else 0)
+        # with free transfers the transport adds no bubble over the compute-only schedule
+        assert r["bubble"] == pytest.approx(simulate_schedule(kind, S, M, V)["bubble"], abs=1e-9)
+
+
+@pytest.mark.parametrize("kind,V,S,M", [("1f1b", 1, 4, 16), ("interleaved", 2, 4, 16), ("1f1b", 1, 8, 32),
+                                        ("1f1b", 1, 3, 4)])
+def test_shared_pipeline_groups_deadlock_on_rccl(kind, V, S, M):
+    """Regression for the round-2 layout (one S-rank group per channel kind): an interior rank's
+    send queues behind its own pre-posted receives and the step deadlocks for S >= 3."""
+    from madnn.parallel.pp import simulate_transport
+
+    with pytest.raises(RuntimeError, match="deadlocks"):
+        simulate_transport(kind, S, M, V, "shared", True)
+    simulate_transport("1f1b", 2, M, 1, "shared", True)  # one sender + one receiver per group: fine
+
+
 def test_interleaving_shrinks_the_bubble():
     from madnn.parallel.pp import pipeline_bubble
 
