@@ -78,45 +78,53 @@ def device_kind(t: torch.Tensor) -> str:
 
 
 class Selected:
-    """What :func:`select` chose for one tensor: the bound collective and the path label
-    ``(device kind, transport)`` -- ``("gpu", "rccl")``, ``("gpu", "gloo-host")`` or
-    ``("cpu", "gloo")`` -- mirroring the reference's ``collectiveSelector[dev][topo][sync]``
-    table lookup (datamodule.lua:199-208)."""
+    """What :func:`select` chose for one tensor: the bound collective, its mode and the path
+    label ``(device kind, transport)`` -- ``("gpu", "rccl")``, ``("gpu", "xgmi-oneshot")``,
+    ``("gpu", "gloo-host")`` or ``("cpu", "gloo")`` -- mirroring the reference's
+    ``collectiveSelector[dev][topo][sync|async][op]`` table lookup (datamodule.lua:199-208).
+    A ``sync`` selection returns when the result may be used (RCCL: stream-ordered); an
+    ``async`` one returns a work handle whose ``wait()`` orders the consumer after it."""
 
-    __slots__ = ("fn", "device", "transport", "op")
+    __slots__ = ("fn", "device", "transport", "op", "mode")
 
-    def __init__(self, fn, device, transport, op):
-        self.fn, self.device, self.transport, self.op = fn, device, transport, op
+    def __init__(self, fn, device, transport, op, mode="sync"):
+        self.fn, self.device, self.transport, self.op, self.mode = fn, device, transport, op, mode
 
     def __call__(self, *args, **kwargs):
+        if self.mode == "async" and self.op not in ("send", "recv", "barrier"):
+            kwargs.setdefault("async_op", True)
         return self.fn(*args, **kwargs)
 
     def __repr__(self):
-        return f"Selected({self.op}, {self.device}/{self.transport})"
+        return f"Selected({self.op}, {self.mode}, {self.device}/{self.transport})"
 
 
-def select(t: torch.Tensor, op: str, group=None) -> Selected:
+def select(t: torch.Tensor, op: str, group=None, mode: str = "sync") -> Selected:
     """Collective selector (R9): the implementation for ``op`` on ``t`` over ``group``.
 
-    The reference keys on [cpu|gpu][singlenode|multinode][sync][op]; on one MI355X node the
-    topology axis collapses (all 8 GPUs are xGMI peers) and the transport follows from the
-    tensor's device and the group's backend: HIP tensors on an RCCL ("nccl") group travel
-    over xGMI; HIP tensors on a gloo group (several ranks sharing one GPU in tests) are
-    staged through host memory by gloo; host tensors go to gloo.  A host tensor on an RCCL
-    group is refused (RCCL cannot move it).  Without a process group the returned callable
-    is the local no-op of every collective."""
+    The reference keys on [cpu|gpu][singlenode|multinode][sync|async][op]; on one MI355X node
+    the topology axis collapses (all 8 GPUs are xGMI peers) and the transport follows from the
+    tensor's device, the group's backend and the mode: HIP tensors on an RCCL ("nccl") group
+    travel over xGMI -- small sync sums through the K5 one-shot kernel when registered, an
+    async sum always through RCCL (the one-shot kernel is stream-ordered only); HIP tensors on
+    a gloo group (several ranks sharing one GPU in tests) are staged through host memory by
+    gloo; host tensors go to gloo.  A host tensor on an RCCL group is refused (RCCL cannot
+    move it).  Without a process group the returned callable is the local no-op of every
+    collective."""
     if op not in _OPS:
         raise KeyError(f"unknown collective {op!r}")
+    if mode not in ("sync", "async"):
+        raise KeyError(f"unknown collective mode {mode!r} (sync | async)")
     fn = {"all_reduce": all_reduce, "broadcast": broadcast, "all_gather": all_gather_into,
           "reduce_scatter": reduce_scatter, "send": send, "recv": recv, "barrier": None}[op]
     kind = device_kind(t)
     if not dist.is_initialized():
-        return Selected(fn or (lambda *a, **k: None), kind, "local", op)
+        return Selected(fn or (lambda *a, **k: None), kind, "local", op, mode)
     be = dist.get_backend(group)
     if kind == "cpu" and be == "nccl":
         raise RuntimeError("CPU tensor on an RCCL group: use a gloo group for host tensors")
     transport = "rccl" if be == "nccl" else ("gloo-host" if kind == "gpu" else "gloo")
-    if op == "all_reduce" and kind == "gpu":
+    if op == "all_reduce" and kind == "gpu" and mode == "sync":
         from .oneshot import lookup
 
         if lookup(t, group) is not None:
@@ -125,7 +133,28 @@ def select(t: torch.Tensor, op: str, group=None) -> Selected:
         from .. import runtime as rt
 
         fn = lambda *a, **k: rt.barrier(group)  # noqa: E731
-    return Selected(fn, kind, transport, op)
+    return Selected(fn, kind, transport, op, mode)
+
+
+def selector_table(group=None) -> dict:
+    """The whole selection table for ``group`` in the reference's shape,
+    ``{dev: {topology: {sync|async: {op: transport}}}}`` (one node: topology ``singlenode``)."""
+    out = {}
+    devs = [("cpu", torch.zeros(1))]
+    if torch.cuda.is_available():
+        devs.append(("gpu", torch.zeros(1, device="cuda")))
+    for dev, t in devs:
+        modes = {}
+        for mode in ("sync", "async"):
+            row = {}
+            for op in _OPS:
+                try:
+                    row[op] = select(t, op, group, mode).transport
+                except RuntimeError:
+                    row[op] = None
+            modes[mode] = row
+        out[dev] = {"singlenode": modes}
+    return out
 
 
 def _local(group) -> bool:

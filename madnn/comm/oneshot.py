@@ -8,7 +8,12 @@ every peer, wait for the peers' flags, sum the W staged inputs read straight ove
 
     comm = OneShotAllReduce(group, cap_bytes=8 << 20)
     comm(t)                      # in-place sum over the group (fp32 or bf16 HIP tensor)
-    comm.check()                 # raises if a peer never arrived (the kernel's bounded wait)
+    comm.check()                 # synchronise; raise if a peer never arrived (bounded wait)
+
+A wait that times out leaves this rank's own input in the output, so the error must be loud: the
+kernel records it in a pinned host word that every later call (and :func:`poll_all`, run by the
+engines' per-step robustness hook) reads without synchronising, raising ``OneShotTimeout`` at
+the latest one optimizer step after the failed call.
 
 ``madnn.comm.all_reduce`` routes small HIP tensors through a registered communicator when
 ``MADNN_ONESHOT=1`` (:func:`enable_for`); RCCL stays the default until the one-shot path is
@@ -49,6 +54,10 @@ def _native():
         lib.madnn_oneshot_max_peers.restype = I
         _lib["h"] = lib
     return _lib["h"]
+
+
+class OneShotTimeout(RuntimeError):
+    pass
 
 
 class OneShotAllReduce:
@@ -93,6 +102,7 @@ class OneShotAllReduce:
     def __call__(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         if not self.supports(t):
             raise ValueError("one-shot all-reduce: contiguous fp32/bf16 tensor on this device within cap")
+        self.poll()
         out = t if out is None else out
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = _native().madnn_oneshot_allreduce(self.id, t.data_ptr(), out.data_ptr(), t.numel(),
@@ -101,12 +111,20 @@ class OneShotAllReduce:
             raise RuntimeError(f"madnn_oneshot_allreduce failed (hipError {rc})")
         return out
 
+    def _raise_if(self, err: int) -> None:
+        if err != 0:
+            raise OneShotTimeout("one-shot all-reduce: a peer never published its input within the bounded "
+                                 "wait; the affected output holds only this rank's partial sum"
+                                 if err > 0 else "one-shot all-reduce: error word unreadable")
+
+    def poll(self) -> None:
+        """Raise if a FINISHED call's wait timed out (host read of the pinned error word, no sync)."""
+        if getattr(self, "id", 0) > 0:
+            self._raise_if(_native().madnn_oneshot_error(self.id, 1))
+
     def check(self) -> None:
         """Synchronise and raise if any call's wait for a peer timed out since the last check."""
-        err = _native().madnn_oneshot_error(self.id, 1)
-        if err != 0:
-            raise RuntimeError("one-shot all-reduce: a peer never published its input (timed out)"
-                               if err > 0 else "one-shot all-reduce: error word unreadable")
+        self._raise_if(_native().madnn_oneshot_error(self.id, 3))
 
     def close(self) -> None:
         if getattr(self, "id", 0) > 0:
@@ -123,6 +141,12 @@ def enable_for(group=None, cap_bytes: int = 1 << 20) -> Optional[OneShotAllReduc
     c = OneShotAllReduce(group, cap_bytes=cap_bytes)
     _registry[_key(group)] = c
     return c
+
+
+def poll_all() -> None:
+    """Lazy error check of every registered communicator (engines call it once per step)."""
+    for c in list(_registry.values()):
+        c.poll()
 
 
 def _key(group):

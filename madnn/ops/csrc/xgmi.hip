@@ -13,7 +13,9 @@
 //      peer's flag array (system-scope release after a system-scope fence);
 //   3. block b waits until its own flag[r][b] >= e for every rank r (system-scope acquire),
 //      bounded: after `spin_limit` polls it records a timeout in *err and gives up on the
-//      wait, so a missing peer can never leave the kernel running;
+//      wait, so a missing peer can never leave the kernel running.  *err lives in pinned host
+//      memory: the host reads it without synchronising (madnn_oneshot_error), so the Python
+//      side raises at the next call / optimizer step instead of training on a partial sum;
 //   4. block b sums chunk b of all W staging buffers (fp32 accumulation) into the output.
 // Reuse safety: the staging half written at epoch e+1 was last read at epoch e-1; a rank only
 // starts epoch e+1 after its epoch-e kernel saw every peer's epoch-e flag for that chunk, which
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void oneshot_kernel(const Args a) {
   }
   __syncthreads();
   if (timed_out) {
-    if (threadIdx.x == 0) atomicOr(a.err, 1);
+    if (threadIdx.x == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -159,7 +161,8 @@ struct Ctx {
   int64_t cap = 0;  // bytes per staging half
   void* stage = nullptr;
   unsigned* flag = nullptr;
-  int* err = nullptr;
+  int* err = nullptr;      // pinned host word (host view)
+  int* err_dev = nullptr;  // its device-side address
   Peers peers{};
   bool opened = false;
   unsigned epoch = 0;
@@ -199,8 +202,11 @@ int madnn_oneshot_create(int64_t cap, int world, int rank, int device, unsigned 
     e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c.flag), kMaxPeers * kMaxBlocks * sizeof(unsigned),
                               hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(c.flag, 0, kMaxPeers * kMaxBlocks * sizeof(unsigned));
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c.err), sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c.err, 0, sizeof(int));
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c.err), sizeof(int), hipHostMallocMapped);
+  if (e == hipSuccess) {
+    *reinterpret_cast<volatile int*>(c.err) = 0;
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c.err_dev), c.err, 0);
+  }
   hipIpcMemHandle_t hs, hf;
   if (e == hipSuccess) e = hipIpcGetMemHandle(&hs, c.stage);
   if (e == hipSuccess) e = hipIpcGetMemHandle(&hf, c.flag);
@@ -208,7 +214,7 @@ int madnn_oneshot_create(int64_t cap, int world, int rank, int device, unsigned 
   if (e != hipSuccess) {
     if (c.stage) (void)hipFree(c.stage);
     if (c.flag) (void)hipFree(c.flag);
-    if (c.err) (void)hipFree(c.err);
+    if (c.err) (void)hipHostFree(c.err);
     return -(int)e;
   }
   std::memcpy(handles, &hs, sizeof(hs));
@@ -264,7 +270,7 @@ int madnn_oneshot_allreduce(int id, const void* in, void* out, int64_t n, int dt
     a.peers = c.peers;
     a.rank = c.rank;
     a.world = c.world;
-    a.err = c.err;
+    a.err = c.err_dev;
     a.half = c.cap / esz;
     a.epoch = ++c.epoch;
   }
@@ -282,14 +288,17 @@ int madnn_oneshot_allreduce(int id, const void* in, void* out, int64_t n, int dt
   return (int)hipGetLastError();
 }
 
-// error word of the context (1 = a wait timed out); reading it synchronises the device
-int madnn_oneshot_error(int id, int reset) {
+// error word of the context (1 = a wait timed out).  flags bit 0: clear it after reading;
+// bit 1: synchronise the device first (otherwise the word reflects the kernels that have
+// finished so far -- a plain host read of pinned memory, no stall)
+int madnn_oneshot_error(int id, int flags) {
   std::lock_guard<std::mutex> g(mu());
   auto it = ctxs().find(id);
   if (it == ctxs().end()) return -1;
-  int v = 0;
-  if (hipMemcpy(&v, it->second.err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (reset && v) (void)hipMemset(it->second.err, 0, sizeof(int));
+  if ((flags & 2) && hipDeviceSynchronize() != hipSuccess) return -1;
+  volatile int* w = it->second.err;
+  const int v = *w;
+  if ((flags & 1) && v) *w = 0;
   return v;
 }
 
@@ -307,7 +316,7 @@ int madnn_oneshot_destroy(int id) {
   }
   (void)hipFree(c.stage);
   (void)hipFree(c.flag);
-  (void)hipFree(c.err);
+  (void)hipHostFree(c.err);
   ctxs().erase(it);
   return 0;
 }

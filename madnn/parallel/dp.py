@@ -49,12 +49,17 @@ def robustness_tick(step: int, group=None) -> None:
 
     * ``MADNN_FAULT=rank:step:kind`` fault injection (``utils.fault``), used by the tests that
       prove a hung or crashed rank becomes a process-group timeout and a launcher teardown;
+    * the K5 one-shot all-reduce's error word (a timed-out peer wait raises, never trains on);
     * with ``check_collectives`` on (``Config.check_collectives`` / ``MADNN_CHECK_COLLECTIVES=1``),
       every ``MADNN_CHECK_EVERY`` (default 50) steps all ranks compare the running fingerprint
       of their collective sequence and raise on divergence."""
     from ..utils.fault import maybe_fail
 
     maybe_fail(step)
+    from ..comm import oneshot
+
+    if oneshot._registry:
+        oneshot.poll_all()   # a K5 call whose peer wait timed out raises here (ADVICE r2)
     if comm.order_check_enabled():
         every = comm.check_every()
         if every > 0 and step % every == 0:
@@ -143,6 +148,7 @@ class DataParallel(nn.Module):
                     comm.broadcast(b, src=self.src_rank, group=self.group)
 
     def _install_hooks(self):
+        self._next_launch = 0
         for bk in self.space.buckets:
             bk.pending = len(bk.params)
             for p in bk.params:
@@ -165,10 +171,24 @@ class DataParallel(nn.Module):
                     self._rearm()
                 torch.autograd.Variable._execution_engine.queue_callback(self._on_backward_end)
             bk.pending -= 1
-            if bk.pending == 0 and not bk.launched:
-                self._launch(bk)
+            if bk.pending == 0:
+                self._launch_ready()
 
         return hook
+
+    def _launch_ready(self):
+        """Launch every ready bucket in INDEX order (torch DDP's rule): collectives on one
+        communicator must be issued in the same order on every rank, and replicas whose
+        gradients become ready in different orders (data-dependent branches, parameters unused
+        on one rank) would otherwise issue their bucket all-reduces in different orders."""
+        bks = self.space.buckets
+        while self._next_launch < len(bks):
+            bk = bks[self._next_launch]
+            if bk.pending > 0 and not bk.launched:
+                return
+            if not bk.launched:
+                self._launch(bk)
+            self._next_launch += 1
 
     # ------------------------------------------------------------ reduction
     def _launch(self, bk: FlatBucket):
@@ -212,10 +232,11 @@ class DataParallel(nn.Module):
             self._ev["bwd_end"].record()
         for bk in self.space.buckets:
             if not bk.launched:
-                if not self.find_unused:
+                if bk.pending > 0 and not self.find_unused:
                     raise RuntimeError(f"bucket {bk.index} had parameters without gradients; "
                                        "set find_unused=True")
                 self._launch(bk)
+        self._next_launch = len(self.space.buckets)
         self._needs_finalize = True
 
     def _wait_works(self, record_end: bool = False):
@@ -237,6 +258,7 @@ class DataParallel(nn.Module):
                 bk.work = None
             bk.launched = False
             bk.pending = len(bk.params)
+        self._next_launch = 0
         return cur
 
     def _rearm(self):
@@ -299,9 +321,9 @@ class DataParallel(nn.Module):
 
     def _maybe_relayout(self):
         """After the first step: if the buckets did not fill in the order backward produced
-        gradients, re-lay them in the observed order (every rank observes the same autograd
-        order, so layouts stay identical across replicas)."""
-        seen = self._observe
+        gradients, re-lay them in the observed order (the source rank's observation, broadcast
+        by :meth:`_agree_on_order`, so layouts stay identical across replicas)."""
+        seen = self._agree_on_order(self._observe)
         self._observe = None
         if not seen or self.space.layout_is_contiguous(seen):
             return
@@ -320,6 +342,29 @@ class DataParallel(nn.Module):
         self._install_hooks()
         self.rebuilt = True
         get_logger().info("madnn dp: re-laid %d buckets in the observed gradient order", len(self.space.buckets))
+
+    def _agree_on_order(self, seen):
+        """The gradient order every replica re-lays its buckets by: this group's source rank's
+        observation, broadcast as indices into the (rank-independent) parameter registration
+        order.  Ranks may observe different orders (data-dependent branches, parameters unused
+        on one rank only); buckets built from different orders would all-reduce unrelated
+        slices, so -- as torch DDP does with its rebuilt buckets -- one rank decides."""
+        canon = [p for g in self.space._groups for p in g if p.requires_grad]
+        if comm._local(self.group) or self.world <= 1:
+            return seen
+        idx_of = {id(p): i for i, p in enumerate(canon)}
+        order, used = [], set()
+        for i in seen or ():
+            k = idx_of.get(i)
+            if k is not None and k not in used:
+                used.add(k)
+                order.append(k)
+        dev = self.space.buckets[0].master.device if self.space.buckets else torch.device("cpu")
+        t = torch.full((len(canon),), -1, dtype=torch.int64, device=dev)
+        if order:
+            t[:len(order)] = torch.tensor(order, dtype=torch.int64, device=dev)
+        comm.broadcast(t, src=self.src_rank, group=self.group)
+        return [id(canon[k]) for k in t.tolist() if k >= 0]
 
     @torch.no_grad()
     def average_parameters(self):

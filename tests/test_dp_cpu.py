@@ -304,6 +304,49 @@ def test_buckets_relaid_in_observed_order():
     run_dist(_w_relayout, 2)
 
 
+class _RankOrdered(torch.nn.Module):
+    """Rank 0 runs a then b, rank 1 b then a: the two replicas OBSERVE opposite gradient orders."""
+
+    def __init__(self, rank):
+        super().__init__()
+        self.rank = rank
+        self.a = torch.nn.Linear(16, 16)
+        self.b = torch.nn.Linear(16, 16)
+        self.head = torch.nn.Linear(16, 4)
+
+    def forward(self, x):
+        h = self.b(torch.tanh(self.a(x))) if self.rank == 0 else self.a(torch.tanh(self.b(x)))
+        return self.head(h)
+
+
+def _w_relayout_disagree(rank, world):
+    """replicas re-lay their buckets by ONE agreed order (the source rank's), so the
+    bucket all-reduces keep summing matching slices and the weights stay identical."""
+    import madnn
+    from madnn.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = _RankOrdered(rank)
+    opt = FusedSGD(m.parameters(), lr=0.1)
+    dm, opt = madnn.distribute(m, opt, strategy="dp", bucket_mb=300 * 4 / 2**20)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(3):
+        x, y = torch.randn(4, 16, generator=g), torch.randint(0, 4, (4,), generator=g)
+        F.cross_entropy(dm(x), y).backward()
+        opt.step()
+    names = {id(p): n for n, p in m.named_parameters()}
+    layout = [[names[id(p)] for p in bk.params] for bk in dm.space.buckets]
+    objs = [None] * world
+    dist.all_gather_object(objs, layout)
+    assert objs[0] == objs[1], objs
+    for p in m.parameters():
+        _check_same_across_ranks(p.detach())
+
+
+def test_relayout_agrees_across_ranks():
+    run_dist(_w_relayout_disagree, 2)
+
+
 def test_grad_sink_writes_in_place_cpu():
     """ops.linear's backward writes the weight gradient straight into the bucket slot and
     autograd adopts that view as p.grad (no copy); the reducer then skips it when packing."""

@@ -54,3 +54,36 @@ def test_oneshot_world_one_and_timeout_flag(cuda):
     c.check()
     assert not c.supports(torch.randn(1 << 15, device=cuda))   # beyond cap
     c.close()
+
+
+def _w_absent_peer(rank, world):
+    """Rank 1 arrives long after rank 0's bounded wait expired: rank 0's output holds only its own
+    input, and its next call raises instead of training on."""
+    import time
+
+    from madnn.comm.oneshot import OneShotAllReduce, OneShotTimeout
+
+    c = OneShotAllReduce(None, cap_bytes=1 << 16, spin_limit=1 << 12)
+    x = torch.full((4096,), float(rank + 1), device="cuda")
+    if rank == 1:
+        time.sleep(3.0)
+    c(x)
+    torch.cuda.synchronize()
+    if rank == 0:
+        assert bool((x == 1.0).all()), "timed-out wait must leave the local input (no partial peer data)"
+        raised = False
+        try:
+            c(torch.ones(8, device="cuda"))
+        except OneShotTimeout:
+            raised = True
+        assert raised, "the next call must raise after a timed-out peer wait"
+    else:
+        c.check()   # rank 0's flag for this epoch was already there: rank 1 completed normally
+    dist.barrier()
+    c.close()
+
+
+def test_oneshot_absent_peer_raises(cuda):
+    from dist_utils import run_dist
+
+    run_dist(_w_absent_peer, 2, device="cuda", backend="gloo")

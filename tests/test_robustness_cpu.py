@@ -80,7 +80,15 @@ def _w_selector_and_sync(rank, world):
     from madnn.models import MLP
 
     sel = comm.select(torch.zeros(2), "all_reduce")
-    assert (sel.device, sel.transport) == ("cpu", "gloo")
+    assert (sel.device, sel.transport, sel.mode) == ("cpu", "gloo", "sync")
+    asel = comm.select(torch.zeros(2), "all_reduce", mode="async")
+    t = torch.full((3,), float(rank + 1))
+    work = asel(t, "sum")
+    assert work is not None and work.wait()   # the async row returns a work handle
+    torch.testing.assert_close(t, torch.full((3,), 3.0))
+    table = comm.selector_table()
+    assert table["cpu"]["singlenode"]["async"]["all_reduce"] == "gloo"
+    assert set(table["cpu"]["singlenode"]) == {"sync", "async"}
     torch.manual_seed(rank)  # different replicas
     m = MLP(8, 16, 4)
     for p in m.parameters():
