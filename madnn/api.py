@@ -245,9 +245,9 @@ def _after_plain_step(engine: DataParallel):
 # Reference-compatible surface
 # --------------------------------------------------------------------------
 def _flat_collective(tensors, op: str, group=None, src: int = 0, scale: float = 1.0) -> int:
-    """One collective per (device, dtype) class of ``tensors``: K4 pack into an fp32 flat
-    buffer, the collective chosen by the selector (R9), K4 unpack with ``scale`` fused.
-    Returns the number of collectives issued."""
+    """One collective per (device, dtype) class of ``tensors``: K4 pack into a flat buffer of
+    the class's own dtype (a bf16 model moves bf16 bytes), the collective chosen by the
+    selector (R9), K4 unpack with ``scale`` fused.  Returns the number of collectives issued."""
     classes = {}
     for t in tensors:
         if t is not None:
@@ -258,7 +258,7 @@ def _flat_collective(tensors, op: str, group=None, src: int = 0, scale: float = 
         for t in ts:
             offs.append(n)
             n += (t.numel() + 15) // 16 * 16
-        flat = torch.zeros(n, dtype=torch.float64 if dt == torch.float64 else torch.float32, device=dev)
+        flat = torch.zeros(n, dtype=dt if dt.is_floating_point else torch.float32, device=dev)
         ops.bucket_pack(ts, flat, offs, 1.0)
         coll = comm.select(flat, op, group)
         if op == "broadcast":
@@ -283,7 +283,23 @@ def synchronize_model(model: nn.Module, group=None, params: bool = True, grads: 
         model = model.module
     with torch.no_grad():
         if params:
-            _flat_collective(list(model.parameters()), "all_reduce", group, scale=1.0 / world)
+            # parameters homed in a flat space (a fused optimizer's) are averaged through their
+            # fp32 masters -- one all-reduce per bucket, no pack -- and the compute copies are
+            # re-derived; the rest go through the dtype-class flat collective
+            plain, spaces = [], {}
+            for p in model.parameters():
+                home = getattr(p, "_madnn_home", None)
+                if home is not None and id(p) in home.param_info:
+                    spaces[id(home)] = home
+                else:
+                    plain.append(p)
+            for sp in spaces.values():
+                for bk in sp.buckets:
+                    coll = comm.select(bk.master, "all_reduce", group)
+                    coll(bk.master, "sum", group=group)
+                    bk.master.mul_(1.0 / world)
+                sp.sync_model_from_master()
+            _flat_collective(plain, "all_reduce", group, scale=1.0 / world)
         if grads:
             _flat_collective([p.grad for p in model.parameters()], "all_reduce", group, scale=1.0 / world)
 
@@ -392,16 +408,25 @@ def parallelize(data, targets, model: nn.Module, size: Optional[int] = None, syn
 
 class Trainer:
     """Minibatch SGD trainer with the reference trainer's knobs and hooks (R8,
-    datamodule.lua:117-184): ``learning_rate``, ``learning_rate_decay``
-    (lr / (1 + epoch * decay)), ``max_iteration`` (epochs), ``shuffle``,
-    ``on_example`` (after every minibatch; reference ``hookExample``) and
-    ``on_iteration`` (after every epoch; ``hookIteration``).  Synchronisation
-    is whatever the model carries: a ``parallelize`` periodic hook, a
-    ``distribute`` engine, or nothing.
+    datamodule.lua:117-184): ``learning_rate``, ``learning_rate_decay``, ``max_iteration``
+    (epochs), ``shuffle``, ``on_example`` (after every minibatch; reference ``hookExample``) and
+    ``on_iteration`` (after every epoch; ``hookIteration``).  Synchronisation is whatever the
+    model carries: a ``parallelize`` periodic hook, a ``distribute`` engine, or nothing.
+
+    Reference fidelity:
+
+    * the default optimizer is :class:`madnn.optim.FusedSGD` over a flat parameter space -- the
+      K1 kernel, one launch per bucket, standing in for the reference's fused
+      gradient-into-weight ``accUpdateGradParameters`` (datamodule.lua:142);
+    * learning-rate schedule exactly as the reference's (datamodule.lua:176-177): the first
+      epoch runs at ``learning_rate``; the counter is incremented BEFORE the decay is applied,
+      so epoch k >= 2 (1-based) runs at ``learning_rate / (1 + k * decay)``;
+    * ``shuffle=True`` draws ONE permutation before the first epoch and keeps it, as the
+      reference does (datamodule.lua:123); ``shuffle="epoch"`` redraws it every epoch.
     """
 
     def __init__(self, model: nn.Module, criterion: Callable, optimizer=None, *, learning_rate: float = 0.01,
-                 learning_rate_decay: float = 0.0, max_iteration: int = 25, shuffle: bool = True,
+                 learning_rate_decay: float = 0.0, max_iteration: int = 25, shuffle=True,
                  batch_size: int = 32, on_example: Optional[Callable] = None,
                  on_iteration: Optional[Callable] = None, verbose: bool = True, device=None,
                  metrics_path: Optional[str] = None):
@@ -411,8 +436,14 @@ class Trainer:
         self.on_example, self.on_iteration, self.verbose = on_example, on_iteration, verbose
         self.device = device
         if optimizer is None:
-            optimizer = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=learning_rate)
+            from .optim import FusedSGD
+
+            optimizer = FusedSGD([p for p in model.parameters() if p.requires_grad], lr=learning_rate)
         self.optimizer = optimizer
+        self.epoch = 0          # completed epochs (checkpointed with the trainer state)
+        self.cursor = 0         # samples of the current epoch already trained on
+        self._partial = (0.0, 0)
+        self._order = None
         self.history = []
         self.global_step = 0
         self.meter = None
@@ -423,18 +454,43 @@ class Trainer:
                                    samples_per_step=batch_size, path=metrics_path)
 
     def _lr(self, epoch: int) -> float:
-        return self.learning_rate / (1.0 + epoch * self.learning_rate_decay)
+        """Learning rate of 0-based ``epoch`` (reference: 1-based iteration i uses lr for i = 1,
+        lr / (1 + i * decay) for i >= 2)."""
+        if epoch == 0:
+            return self.learning_rate
+        return self.learning_rate / (1.0 + (epoch + 1) * self.learning_rate_decay)
+
+    def _perm(self, n: int):
+        if not self.shuffle:
+            return torch.arange(n)
+        if self.shuffle == "epoch" or self._order is None or len(self._order) != n:
+            self._order = torch.randperm(n)
+        return self._order
+
+    def state_dict(self) -> dict:
+        """Resume state (no optimizer: ``madnn.ckpt`` stores that by parameter name): epoch,
+        position inside it, step counter, the permutation, the partial epoch error."""
+        return {"epoch": self.epoch, "cursor": self.cursor, "global_step": self.global_step,
+                "history": list(self.history), "order": None if self._order is None else self._order.tolist(),
+                "partial": list(self._partial)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.epoch, self.global_step = int(sd["epoch"]), int(sd["global_step"])
+        self.cursor = int(sd.get("cursor", 0))
+        self.history = list(sd.get("history", []))
+        self._order = torch.tensor(sd["order"]) if sd.get("order") is not None else None
+        self._partial = tuple(sd.get("partial", (0.0, 0)))
 
     def train(self, data, targets) -> list:
         n = len(data)
         log = get_logger()
-        for epoch in range(self.max_iteration):
+        for epoch in range(self.epoch, self.max_iteration):
             lr = self._lr(epoch)
             for g in self.optimizer.param_groups:
                 g["lr"] = lr
-            order = torch.randperm(n) if self.shuffle else torch.arange(n)
-            tot, cnt = 0.0, 0
-            for s in range(0, n, self.batch_size):
+            order = self._perm(n) if self.cursor == 0 or self._order is None else self._order
+            tot, cnt = self._partial if self.cursor else (0.0, 0)
+            for s in range(self.cursor, n, self.batch_size):
                 idx = order[s:s + self.batch_size]
                 x, y = data[idx], targets[idx]
                 if self.device is not None:
@@ -458,6 +514,8 @@ class Trainer:
                     self.meter.stop(loss, epoch=epoch + 1, lr=lr)
                 tot += float(loss.detach()) * len(idx)
                 cnt += len(idx)
+                self.cursor = s + len(idx)
+                self._partial = (tot, cnt)
                 if self.on_example is not None:
                     self.on_example(self, (x, y))
             err = tot / max(cnt, 1)
@@ -467,6 +525,8 @@ class Trainer:
                 ps.sync()  # end-of-epoch sync (reference counter == size branch, fixed to every epoch: A-4)
             if self.verbose:
                 log.info("# current error = %.6f (epoch %d, lr %.5g)", err, epoch + 1, lr)
+            self.epoch = epoch + 1
+            self.cursor, self._partial = 0, (0.0, 0)
             if self.on_iteration is not None:
                 self.on_iteration(self, epoch, err)
         if self.verbose:

@@ -11,7 +11,10 @@ object.  madnn's format::
                                        UN-WRAPPED single-device parameter names
     <dir>/optim-<shard>.pt             optimizer state per parameter name (plain
                                        tensors only: loads with weights_only=True)
-    <dir>/rng-rank<r>.pt               per-rank RNG states
+    <dir>/state-<coords>.pt            per-rank resume state keyed by MESH coordinates
+                                       (e.g. ``dp1-pp0-tp0``): RNG, data-sampler
+                                       cursor, trainer epoch/position, the
+                                       ``parallelize`` auto-sync counter
 
 One shard per pipeline stage, written by that stage's DP-rank 0.  Because keys
 are the original model's names, ``consolidate()`` merges the shards into one
@@ -176,8 +179,46 @@ def _shard_id(engine) -> Optional[int]:
     return 0 if rt.get_rank() == 0 else None
 
 
-def save(path: str, engine, optimizer=None, step: int = 0, extra: Optional[dict] = None) -> None:
-    """Collective: every rank calls it; DP-rank 0 of every stage writes its shard."""
+def _coords(engine) -> dict:
+    """This rank's mesh coordinates {"dp", "pp", "tp"} under ``engine``'s placement."""
+    g = getattr(engine, "groups", None)
+    if g is None and hasattr(engine, "module"):
+        g = getattr(engine.module, "groups", None)
+    if g is not None:
+        return {"dp": g.dp_idx, "pp": g.pp_idx, "tp": g.tp_idx}
+    return {"dp": rt.get_rank(), "pp": 0, "tp": 0}
+
+
+def _coord_name(c: dict) -> str:
+    return f"dp{c['dp']}-pp{c['pp']}-tp{c['tp']}"
+
+
+def _periodic_sync(engine):
+    from ..parallel.dp import DataParallel
+
+    module = engine.module if isinstance(engine, DataParallel) else engine
+    return getattr(module, "_madnn_sync", None) if isinstance(module, nn.Module) else None
+
+
+def _resume_state(engine, sampler, trainer) -> dict:
+    out = {"rng_cpu": torch.get_rng_state()}
+    if torch.cuda.is_available():
+        out["rng_cuda"] = torch.cuda.get_rng_state()
+    ps = _periodic_sync(engine)
+    if ps is not None:
+        out["sync"] = {"counter": ps.counter, "period": ps.period, "backwards": ps.backwards, "syncs": ps.syncs}
+    if sampler is not None:
+        out["sampler"] = sampler.state_dict()
+    if trainer is not None:
+        out["trainer"] = trainer.state_dict()
+    return out
+
+
+def save(path: str, engine, optimizer=None, step: int = 0, extra: Optional[dict] = None, sampler=None,
+         trainer=None) -> None:
+    """Collective: every rank calls it; DP-rank 0 of every stage writes its shard, and every rank
+    writes its resume state (RNG, ``sampler`` cursor, ``trainer`` position, the auto-sync
+    counter of a ``parallelize``-d model) under its mesh coordinates."""
     save_file, _ = _st()
     os.makedirs(path, exist_ok=True)
     state = _named_state(engine)          # collective for TP gathers: all ranks
@@ -191,19 +232,45 @@ def save(path: str, engine, optimizer=None, step: int = 0, extra: Optional[dict]
             for k, v in st.items():
                 flat[f"{name}::{k}"] = v
         torch.save(flat, os.path.join(path, f"optim-{shard:05d}.pt"))
-    rng = {"cpu": torch.get_rng_state()}
-    if torch.cuda.is_available():
-        rng["cuda"] = torch.cuda.get_rng_state()
-    torch.save(rng, os.path.join(path, f"rng-rank{rt.get_rank()}.pt"))
+    coords = _coords(engine)
+    torch.save(_resume_state(engine, sampler, trainer), os.path.join(path, f"state-{_coord_name(coords)}.pt"))
     rt.barrier()
     if rt.get_rank() == 0:
         meta = {"format": FORMAT, "time": time.time(), "step": int(step), "world": rt.get_world_size(),
                 "torch": torch.__version__, "plan": _plan_meta(engine), "extra": extra or {},
-                "aliases": aliases,
+                "aliases": aliases, "mesh": _mesh_meta(engine), "optim_groups": _group_hparams(optimizer),
                 "shards": sorted(f for f in os.listdir(path) if f.startswith("model-"))}
         with open(os.path.join(path, "madnn_meta.json"), "w") as f:
             json.dump(meta, f, indent=2)
     rt.barrier()
+
+
+def _group_hparams(optimizer) -> list:
+    """JSON-able hyper-parameters of every optimizer param group (lr, momentum, betas, ...)."""
+    if optimizer is None:
+        return []
+    out = []
+    for g in optimizer.param_groups:
+        d = {}
+        for k, v in g.items():
+            if k == "params":
+                continue
+            if isinstance(v, (int, float, bool, str)) or v is None:
+                d[k] = v
+            elif isinstance(v, (tuple, list)) and all(isinstance(x, (int, float)) for x in v):
+                d[k] = list(v)
+        out.append(d)
+    return out
+
+
+def _mesh_meta(engine) -> dict:
+    g = getattr(engine, "groups", None)
+    if g is None and hasattr(engine, "module"):
+        g = getattr(engine.module, "groups", None)
+    if g is not None:
+        m = g.mesh
+        return {"dp": m.dp, "pp": m.pp, "tp": m.tp}
+    return {"dp": rt.get_world_size(), "pp": 1, "tp": 1}
 
 
 def _plan_meta(engine) -> dict:
@@ -247,8 +314,12 @@ def _optim_all(path: str) -> Dict[str, Dict[str, torch.Tensor]]:
     return out
 
 
-def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
-    """Restore weights (and optimizer state) into any placement, by parameter name."""
+def load(path: str, engine, optimizer=None, strict: bool = True, sampler=None, trainer=None) -> dict:
+    """Restore weights (and optimizer state) into any placement, by parameter name; plus this
+    rank's resume state (RNG, sampler cursor, trainer position, auto-sync counter).  The resume
+    state is looked up by mesh coordinates; at a different placement a rank takes the state of
+    the saved coordinates it maps onto (dp index modulo the saved dp size), which keeps the
+    data position but cannot reproduce per-rank random streams bit for bit."""
     from ..parallel.dp import DataParallel
     from ..parallel.pp import PipelineEngine
 
@@ -302,13 +373,43 @@ def load(path: str, engine, optimizer=None, strict: bool = True) -> dict:
                                     for kk, v in ost[n].items()}
                 k += 1
         sd["state"] = new_state
+        saved = meta.get("optim_groups") or []
+        if len(saved) == len(sd["param_groups"]):
+            for g, h in zip(sd["param_groups"], saved):
+                for k, v in h.items():
+                    g[k] = tuple(v) if isinstance(g.get(k), tuple) else v
         optimizer.load_state_dict(sd)
     if isinstance(engine, DataParallel):
         engine._steps = int(meta.get("plan", {}).get("steps", engine._steps))
-    rng_file = os.path.join(path, f"rng-rank{rt.get_rank()}.pt")
-    if os.path.exists(rng_file):
-        rng = torch.load(rng_file, weights_only=True)
-        torch.set_rng_state(rng["cpu"])
-        if "cuda" in rng and torch.cuda.is_available():
-            torch.cuda.set_rng_state(rng["cuda"])
+    st = _load_resume_state(path, engine, meta)
+    if st is not None:
+        torch.set_rng_state(st["rng_cpu"])
+        if "rng_cuda" in st and torch.cuda.is_available():
+            torch.cuda.set_rng_state(st["rng_cuda"])
+        ps = _periodic_sync(engine)
+        if ps is not None and "sync" in st:
+            ps.counter = int(st["sync"]["counter"])
+            ps.backwards = int(st["sync"]["backwards"])
+            ps.syncs = int(st["sync"]["syncs"])
+        if sampler is not None and "sampler" in st:
+            sampler.load_state_dict(st["sampler"])
+        if trainer is not None and "trainer" in st:
+            trainer.load_state_dict(st["trainer"])
     return meta
+
+
+def _load_resume_state(path: str, engine, meta: dict) -> Optional[dict]:
+    c = _coords(engine)
+    f = os.path.join(path, f"state-{_coord_name(c)}.pt")
+    if not os.path.exists(f):
+        saved = meta.get("mesh") or {"dp": meta.get("world", 1), "pp": 1, "tp": 1}
+        c = {"dp": c["dp"] % max(int(saved["dp"]), 1), "pp": min(c["pp"], int(saved["pp"]) - 1),
+             "tp": c["tp"] % max(int(saved["tp"]), 1)}
+        f = os.path.join(path, f"state-{_coord_name(c)}.pt")
+    if not os.path.exists(f):
+        legacy = os.path.join(path, f"rng-rank{rt.get_rank()}.pt")   # round-2 checkpoints
+        if not os.path.exists(legacy):
+            return None
+        rng = torch.load(legacy, weights_only=True)
+        return {"rng_cpu": rng["cpu"], **({"rng_cuda": rng["cuda"]} if "cuda" in rng else {})}
+    return torch.load(f, weights_only=True)

@@ -51,7 +51,7 @@ class Config:
     # pipeline parallel
     pp_stages: Optional[int] = None
     microbatches: Optional[int] = None
-    schedule: str = "1f1b"               # gpipe | 1f1b | interleaved
+    schedule: str = "auto"               # auto (the planner prices all) | gpipe | 1f1b | interleaved
     virtual_stages: Optional[int] = None  # model chunks per rank for schedule="interleaved" (None => 2)
     # tensor parallel
     tp_size: int = 1
@@ -101,7 +101,7 @@ class Config:
             raise ValueError(f"unknown strategy {self.strategy!r}")
         if self.sync not in ("grads", "params", "manual"):
             raise ValueError(f"unknown sync mode {self.sync!r}")
-        if self.schedule not in ("gpipe", "1f1b", "interleaved"):
+        if self.schedule not in ("auto", "gpipe", "1f1b", "interleaved"):
             raise ValueError(f"unknown pipeline schedule {self.schedule!r}")
         if self.remainder not in ("drop", "last", "pad"):
             raise ValueError(f"unknown remainder policy {self.remainder!r}")

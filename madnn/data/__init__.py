@@ -105,7 +105,12 @@ def synthetic_batch(kind: str, batch: int, device, dtype=torch.bfloat16, **kw):
 
 
 class DistributedSampler(torch.utils.data.Sampler):
-    """Contiguous-stripe sampler with per-epoch shuffling inside the shard."""
+    """Contiguous-stripe sampler with per-epoch shuffling inside the shard.
+
+    Resumable: it counts the indices it has handed out this epoch (``cursor``); after
+    :meth:`load_state_dict` the next iteration continues mid-epoch exactly where the saved
+    one stopped (same permutation: it is a function of seed + epoch only).  Restored at a
+    different world size the position is carried over in GLOBAL samples consumed."""
 
     def __init__(self, n: int, rank: Optional[int] = None, world: Optional[int] = None, shuffle: bool = True,
                  remainder: str = "drop", seed: int = 0):
@@ -114,9 +119,25 @@ class DistributedSampler(torch.utils.data.Sampler):
         self.world = rt.get_world_size() if world is None else world
         self.shuffle, self.remainder, self.seed = shuffle, remainder, seed
         self.epoch = 0
+        self.cursor = 0          # indices of this epoch already yielded
 
     def set_epoch(self, e: int):
+        if e != self.epoch:
+            self.cursor = 0
         self.epoch = e
+
+    def state_dict(self) -> dict:
+        return {"n": self.n, "epoch": self.epoch, "cursor": self.cursor, "seed": self.seed, "world": self.world,
+                "shuffle": self.shuffle, "remainder": self.remainder}
+
+    def load_state_dict(self, sd: dict) -> None:
+        if int(sd["n"]) != self.n:
+            raise ValueError(f"sampler state is for a dataset of {sd['n']} samples, not {self.n}")
+        self.epoch, self.seed = int(sd["epoch"]), int(sd["seed"])
+        cur = int(sd["cursor"])
+        if int(sd.get("world", self.world)) != self.world:
+            cur = cur * int(sd["world"]) // self.world   # same global position
+        self.cursor = min(cur, len(self))
 
     def _indices(self):
         if self.remainder == "pad":
@@ -131,7 +152,11 @@ class DistributedSampler(torch.utils.data.Sampler):
             g = torch.Generator().manual_seed(self.seed + self.epoch)
             perm = torch.randperm(len(idx), generator=g).tolist()
             idx = [idx[i] for i in perm]
-        return iter(idx)
+        start = self.cursor if self.cursor < len(idx) else 0
+        self.cursor = start
+        for i in idx[start:]:
+            self.cursor += 1
+            yield i
 
     def __len__(self):
         return len(self._indices())

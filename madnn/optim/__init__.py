@@ -123,6 +123,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
             return out[0]
         sq = ops.grad_norm(flats, max_norm=0.0)[0:1].double().square()
         for p in skip:
+            if id(p) not in self.space.param_info:
+                continue  # not optimised by this optimizer: contributes no gradient here
             bk, off, _ = self.space.param_info[id(p)]
             i = self.space.buckets.index(bk)
             sq -= flats[i][off:off + p.numel()].double().square().sum()
@@ -220,7 +222,9 @@ class _FlatOptimizer(torch.optim.Optimizer):
                 if key != "params":
                     g[key] = v
         if self.space is None:
-            self._pending_load = sd
+            # the flat state needs the space; hyper-parameters are applied NOW (a later
+            # g["lr"] = ... must not be undone when the space binds at the first step)
+            self._pending_load = {"state": sd["state"], "param_groups": []}
             return
         idx = self._param_index()
         for bk in self.space.buckets:

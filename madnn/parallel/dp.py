@@ -376,6 +376,17 @@ class DataParallel(nn.Module):
             bk.master.mul_(1.0 / self.world)
         self.space.sync_model_from_master()
 
+    def __getattr__(self, name):
+        """Attributes the engine does not have resolve on the wrapped module (``eng.h[0]``,
+        ``eng.loss_fn`` of a model), so a distributed model reads like the original."""
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            mods = self.__dict__.get("_modules", {})
+            if "module" in mods and name != "module":
+                return getattr(mods["module"], name)
+            raise
+
     # -------------------------------------------------------------- forward
     def forward(self, *args, **kwargs):
         if self._needs_finalize and self.comm_stream is not None:

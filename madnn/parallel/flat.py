@@ -141,6 +141,7 @@ class FlatParamSpace:
                     model[off:off + n].copy_(obk.model[ooff:ooff + n])
                 self.param_info[id(p)] = (bk, off, cl)
                 p.data = _phys_view(model[off:off + n], p.shape, cl)
+                p._madnn_home = self
             bk.master, bk.model = master, model
             if on_bucket is not None:
                 on_bucket(bk, old)
@@ -201,6 +202,7 @@ class FlatParamSpace:
         for p, off in zip(bk.params, bk.offsets):
             cl = self.param_info[id(p)][2]
             p.data = _phys_view(model[off:off + p.numel()], p.shape, cl)
+            p._madnn_home = self  # the space whose fp32 master is this parameter's true value
             # an existing p.grad stays valid: pack_grads re-layouts it if its strides differ
         bk.model = model
         bk.master = master

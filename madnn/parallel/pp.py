@@ -946,7 +946,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     schedule = getattr(plan, "schedule", None) or cfg.schedule
     if V > 1:
         schedule = "interleaved"
-    elif schedule == "interleaved":
+    elif schedule in ("interleaved", "auto", "none"):
         schedule = "1f1b"
     if len(plan.bounds) != S * V + 1:
         raise ValueError(f"plan has {len(plan.bounds) - 1} pipeline chunks, expected {S} x {V}")

@@ -58,13 +58,19 @@ def _rank(group) -> int:
 
 
 def _gather_last(x: torch.Tensor, group) -> torch.Tensor:
+    """Concatenate the ranks' shards along the LAST dim.  RCCL gathers rank-major ([W, ..., k]);
+    the last-dim layout interleaves the ranks inside every row, so exactly one re-layout pass
+    (a strided copy of the [W, rows, k] buffer into [rows, W, k]) produces the output -- no
+    per-rank views and no cat."""
     w = _world(group)
     if w == 1:
         return x
     x = x.contiguous()
     buf = torch.empty((w,) + tuple(x.shape), dtype=x.dtype, device=x.device)
     comm.all_gather_into(buf.view(w * x.shape[0], *x.shape[1:]) if x.dim() > 0 else buf, x, group=group)
-    return torch.cat(list(buf.unbind(0)), dim=-1)
+    if x.dim() == 0:
+        return buf
+    return buf.movedim(0, -2).reshape(*x.shape[:-1], w * x.shape[-1])
 
 
 def _shard_last(x: torch.Tensor, group) -> torch.Tensor:
@@ -400,9 +406,10 @@ def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
     groups = rt.ProcessGroups(rt.Mesh(dp=world // tp, pp=1, tp=tp))
     dev = rt.device()
     model.to(dev)
-    with torch.no_grad():  # identical replicas before sharding
-        for p in model.parameters():
-            comm.broadcast(p.data, src=0)
+    with torch.no_grad():  # identical replicas before sharding: one bucketed broadcast per dtype
+        from ..api import _flat_collective
+
+        _flat_collective([p.data for p in model.parameters()], "broadcast", None, src=0)
     old = {id(p) for p in model.parameters()}
     n = shard_linears(model, groups.tp_group, int(cfg.extra.get("tp_min_params", 1 << 20)))
     if os.environ.get("MADNN_ONESHOT", "0") == "1" and dev.type == "cuda" and tp > 1:
@@ -427,13 +434,13 @@ def apply_tensor_parallel(model: nn.Module, optimizer, cfg):
                 groups_o = [{"params": new_params}]
         optimizer = type(optimizer)(groups_o, **optimizer.defaults)
     get_logger().info("madnn tp: sharded %d Linear layers, mesh dp=%d x tp=%d", n, world // tp, tp)
-    if world // tp > 1:
-        engine, optimizer = _distribute_dp(model, optimizer, cfg, dev, group=groups.dp_group,
-                                           src_rank=groups.dp_ranks[0])
-        engine.groups = groups
-        engine._norm_spec = tp_norm_spec(model, groups.tp_group)
-        return engine, optimizer
-    model.groups = groups
+    # ALWAYS through the flat-space engine, also without a DP axis (its group is then a
+    # singleton: no collectives): bf16 compute copies with fp32 masters, the fused optimizer
+    # over flat buckets and input casting apply to TP exactly as to DP
+    engine, optimizer = _distribute_dp(model, optimizer, cfg, dev, group=groups.dp_group,
+                                       src_rank=groups.dp_ranks[0])
+    engine.groups = groups
+    engine._norm_spec = tp_norm_spec(model, groups.tp_group)
     if optimizer is not None and hasattr(optimizer, "norm_spec"):
-        optimizer.norm_spec = tp_norm_spec(model, groups.tp_group)
-    return model, optimizer
+        optimizer.norm_spec = engine._norm_spec
+    return engine, optimizer

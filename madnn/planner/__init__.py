@@ -46,7 +46,7 @@ from torch import nn
 from ..config import Config, torch_dtype
 from ..ops import native_runtime
 from ..utils.logging import get_logger
-from .cost import LayerCost, divisors, estimate, measure_layers, stage_estimate
+from .cost import LayerCost, divisors, estimate, measure_chain, measure_layers, param_state_bytes, stage_estimate
 from .hw import Machine, load
 from .trace import Spine, find_block_list, trace
 
@@ -155,25 +155,31 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
             get_logger().warning("madnn planner: no example_input / global_batch given; assuming %d sample(s) per "
                                  "GPU for microbatch and activation sizing", example_input.shape[0])
         B = max(example_input.shape[0], 1) * world
+    calib = None
     if costs is None:
         costs = estimate(spine, example_input, dtype=dtype, machine=hw)
         import torch.distributed as dist
 
         multi = dist.is_initialized() and dist.get_world_size() > 1
-        if _want_measure(cfg) and (not multi or dist.get_rank() == 0):
+        ok = 1
+        if _want_measure(cfg):
             try:
                 per_gpu = max(int(B) // max(world, 1), 1) if (explicit_input or global_batch
                                                               or cfg.extra.get("global_batch")) else None
                 mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input, per_gpu)
+                # every rank times its share of the distinct layers (all-gathered inside)
                 costs = measure_layers(spine, example_input, costs, batch=mb, dtype=dtype)
+                calib = _calibrate_chain(spine, example_input, costs, mb, dtype, cfg, hw)
             except Exception as e:  # noqa: BLE001 - the analytic model still plans
                 get_logger().warning("madnn planner: layer measurement failed (%s); using analytic costs", e)
+                ok = 0
         if multi:
             # every rank must choose the SAME placement: rank 0's (measured) costs are the plan input
-            obj = [[(c.fwd_s, c.bwd_s, c.measured) for c in costs]]
+            obj = [[(c.fwd_s, c.bwd_s, c.fixed_s, c.measured) for c in costs], calib]
             dist.broadcast_object_list(obj, src=0)
-            for c, (f, b, m) in zip(costs, obj[0]):
-                c.fwd_s, c.bwd_s, c.measured = f, b, m
+            for c, (f, b, fx, m) in zip(costs, obj[0]):
+                c.fwd_s, c.bwd_s, c.fixed_s, c.measured = f, b, fx, m
+            calib = obj[1]
     measured = all(c.measured for c in costs)
     opt = _opt_kind(optimizer)
     cap = hw.hbm_gb * cfg.mem_headroom * 1e9
@@ -187,9 +193,10 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         if not _allowed(forced, pp, dp, world, cfg.pp_stages):
             continue
         for ckpt_mode in ([False, True] if cfg.checkpointing == "auto" else [cfg.checkpointing == "all"]):
-            c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode)
-            if c is not None:
-                cands.append(c)
+            for schedule, V, M in pp_variants(pp, max(B // dp, 1), L, cfg):
+                c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode, schedule, V, M)
+                if c is not None:
+                    cands.append(c)
     if forced in ("auto", "tp") and world > 1:
         for tp in divisors(world):
             if tp == 1 or (forced == "tp" and cfg.tp_size > 1 and tp != cfg.tp_size):
@@ -206,6 +213,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     plan = Plan(best["strategy"], best["dp"], best["pp"], best["bounds"], best["M"], ck, best["step_s"],
                 best["mem_list"], spine, costs, cands, B, schedule=best.get("schedule", "1f1b"),
                 virtual=best.get("V", 1), tp=best.get("tp", 1), measured=measured)
+    plan.calibration = calib
     log = get_logger()
     log.info("madnn plan: %s", plan.describe())
     log.info("madnn plan candidates (world=%d, global batch %d):\n%s", world, B, plan.table())
@@ -215,13 +223,13 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
 def _default_measure_batch(example_input: torch.Tensor, per_gpu: Optional[int] = None) -> int:
     """Per-layer timing batch.  Per-sample costs fall steeply with the batch (a ResNet-50 layer at
     32 images runs at ~1/6 of its batch-2048 efficiency), so when the job's per-GPU batch is known
-    the layers are timed at that batch, capped at 256 images / 32k tokens / 1024 rows to bound the
+    the layers are timed at that batch, capped at 2048 images / 64k tokens / 1024 rows to bound the
     probe's memory and time; otherwise at a small default (~4k tokens, 32 images, 64 rows)."""
     per = int(torch.tensor(example_input.shape[1:]).prod()) if example_input.dim() > 1 else 1
     if example_input.dtype in (torch.long, torch.int32):  # token ids
-        base, cap = max(1, min(16, 4096 // max(per, 1))), max(1, 32768 // max(per, 1))
+        base, cap = max(1, min(16, 4096 // max(per, 1))), max(1, 65536 // max(per, 1))
     elif example_input.dim() == 4:
-        base, cap = 32, 256
+        base, cap = 32, 2048
     else:
         base, cap = 64, 1024
     return max(1, min(int(per_gpu), cap)) if per_gpu else base
@@ -276,41 +284,98 @@ def _chunk_ranks(pp: int, V: int):
     return [[c * pp + r for c in range(V)] for r in range(pp)]
 
 
-def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt):
+def pp_variants(pp: int, per_replica: int, L: int, cfg: Config):
+    """The pipeline schedules the planner prices for ``pp`` stages: GPipe, 1F1B and interleaved
+    1F1B with V in {2, 4} model chunks per rank, each at every microbatch count M in
+    {pp, 2pp, 4pp, 8pp, 16pp} that divides the replica's batch (interleaving also needs
+    M % pp == 0 and pp*V <= layers).  An explicit ``cfg.schedule`` / ``cfg.microbatches`` /
+    ``cfg.virtual_stages`` narrows the search to it.  ``pp == 1`` yields the single DP variant."""
+    if pp == 1:
+        yield "none", 1, 1
+        return
+    scheds = ["gpipe", "1f1b", "interleaved"] if cfg.schedule in (None, "auto") else [cfg.schedule]
+    if cfg.microbatches:
+        ms = [max(1, min(int(cfg.microbatches), per_replica))]
+    else:
+        ms = sorted({m for m in (pp, 2 * pp, 4 * pp, 8 * pp, 16 * pp) if m <= per_replica and per_replica % m == 0})
+        if not ms:  # a tiny batch: as many microbatches as it splits into evenly
+            ms = [max(d for d in divisors(per_replica) if d <= pp)]
+    for sched in scheds:
+        if sched == "interleaved":
+            vs = [int(cfg.virtual_stages)] if cfg.virtual_stages else [2, 4]
+            for V in vs:
+                if V < 2 or pp * V > L:
+                    continue
+                for M in ms:
+                    if M % pp == 0:
+                        yield "interleaved", V, M
+        else:
+            for M in ms:
+                yield sched, 1, M
+
+
+def optimizer_s(params: float, opt: str, hw: Machine) -> float:
+    """The fused optimizer pass over ``params`` parameters: an HBM stream of the fp32 master,
+    the reduced gradient, the state and the bf16 compute copy (Adam ~28 B, SGD ~20 B per
+    parameter) at the profile's streaming bandwidth."""
+    per = 28.0 if opt == "adam" else 20.0
+    return params * per / (hw.hbm_tbps * 1e12)
+
+
+def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw: Machine):
+    """Scale the per-layer costs so their sum matches ONE timing of the whole spine at the
+    measurement batch (isolated layer timings miss what neighbouring layers do to each other).
+    Skipped for models whose weights would take more than a quarter of HBM.  Returns
+    ``{"ratio", "chain_s", "layers_s", "batch"}`` or None."""
+    if not cfg.extra.get("calibrate_chain", True):
+        return None
+    nparams = sum(c.params for c in costs)
+    need = nparams * 6 + sum(c.act_bytes for c in costs) * batch   # weights + grads, saved activations
+    if need > 0.5 * hw.hbm_gb * 1e9:
+        return None
+    t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype)
+    if not t:
+        return None
+    import torch.distributed as dist
+
+    if dist.is_initialized() and dist.get_world_size() > 1:  # every GPU timed it: average
+        v = torch.tensor([t], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(v)
+        t = float(v) / dist.get_world_size()
+    layers = sum(c.call_s(batch) for c in costs)
+    if layers <= 0:
+        return None
+    r = t / layers
+    for c in costs:
+        c.fwd_s *= r
+        c.bwd_s *= r
+        c.fixed_s *= r
+    return {"ratio": r, "chain_s": t, "layers_s": layers, "batch": batch}
+
+
+def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="none", V=1, M=1):
     from ..parallel.pp import pipeline_bubble, simulate_schedule
 
     L = len(costs)
     per_replica = max(B // dp, 1)
-    V = 1
-    schedule = cfg.schedule if pp > 1 else "none"
     if pp == 1:
-        M = 1
-    else:
-        M = cfg.microbatches or min(4 * pp, per_replica)
-        M = max(1, min(M, per_replica))
-        if schedule == "interleaved":
-            V = max(int(cfg.virtual_stages or 2), 1)
-            while V > 1 and pp * V > L:
-                V -= 1
-            M = M // pp * pp
-            if V == 1 or M < pp:
-                V, schedule = 1, "1f1b"
-                M = max(1, min(cfg.microbatches or min(4 * pp, per_replica), per_replica))
+        schedule, V, M = "none", 1, 1
     mb = per_replica / M
     rfac = 1.0 + (1.0 / 3.0 if ckpt else 0.0)
     nst = pp * V
     mems = [stage_estimate(costs, i, i + 1, opt, ckpt).param_bytes + stage_estimate(costs, i, i + 1, opt, ckpt)
             .act_bytes_per_sample * mb * (pp if pp > 1 else 1) for i in range(L)]
-    times = [c.time_s * rfac for c in costs]
+    times = [c.call_s(mb) * rfac for c in costs]
     try:
         bounds, _ = native_runtime.partition(times, nst, mems, cap / V if cap > 0 else 0.0)
     except ValueError:
         bounds, _ = native_runtime.partition(times, nst)
     chunk_est = [stage_estimate(costs, bounds[v], bounds[v + 1], opt, ckpt) for v in range(nst)]
     ranks = _chunk_ranks(pp, V)
-    rank_t = [sum(chunk_est[v].time_per_sample_s for v in vs) * mb for vs in ranks]
+    # per-rank time of ONE microbatch through its chunks: fixed per-call cost + per-sample slope
+    rank_t = [sum(times[i] for v in vs for i in range(bounds[v], bounds[v + 1])) for vs in ranks]
     if pp > 1:
-        inflight = simulate_schedule(schedule, pp, M, V)["peak_inflight"] if schedule != "none" else [1] * pp
+        inflight = simulate_schedule(schedule, pp, M, V)["peak_inflight"]
         if schedule == "gpipe":
             inflight = [M * V] * pp
     else:
@@ -322,12 +387,14 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt):
         mem_list.append((pbytes + act_per_chunk * inflight[r]) / 1e9)
     rb = _reduce_bytes(cfg)
     bucket_bytes = _bucket_bytes(cfg, costs, rb)
+    rank_params = [sum(chunk_est[v].params for v in vs) for vs in ranks]
+    opt_s = max(optimizer_s(p, opt, hw) for p in rank_params)
     if pp == 1:
         compute = rank_t[0]
         bubble = 0.0
-        bwd = [c.bwd_s * rfac * per_replica for c in costs]
+        bwd = [(c.bwd_s * per_replica + c.fixed_s * 2.0 / 3.0) * rfac for c in costs]
         comm_s = dp_exposed_s(bwd, [c.params * rb for c in costs], dp, hw, bucket_bytes)
-        step = compute + comm_s
+        step = compute + comm_s + opt_s
     else:
         bubble = pipeline_bubble(schedule, pp, M, V)
         compute = M * max(rank_t)
@@ -337,15 +404,15 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt):
             worst = 0.0
             for vs in ranks:
                 idx = [i for v in vs for i in range(bounds[v], bounds[v + 1])]
-                bwd = [costs[i].bwd_s * rfac * mb for i in idx]
+                bwd = [(costs[i].bwd_s * mb + costs[i].fixed_s * 2.0 / 3.0) * rfac for i in idx]
                 worst = max(worst, dp_exposed_s(bwd, [costs[i].params * rb for i in idx], dp, hw, bucket_bytes))
             comm_s += worst
-        step = compute / max(1.0 - bubble, 1e-3) + comm_s
+        step = compute / max(1.0 - bubble, 1e-3) + comm_s + opt_s
     fits = max(mem_list) * 1e9 <= cap
     strategy = "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp")
     return {"strategy": strategy, "dp": dp, "pp": pp, "tp": 1, "M": M, "V": V, "schedule": schedule,
             "ckpt": ckpt, "bounds": bounds, "step_s": step, "compute_s": compute, "comm_s": comm_s,
-            "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits}
+            "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits, "opt_s": opt_s}
 
 
 def _tp_linears(layer: nn.Module, tp: int, min_params: int, in_shape, in_dtype):
@@ -398,7 +465,7 @@ def _tp_candidate(spine: Spine, costs, dp, tp, B, cfg, hw: Machine, opt, cap, ex
         lin = _tp_linears(layer, tp, min_params, in_shape, in_dtype)
         gflops = sum(2.0 * a * b * t for a, b, t in lin)
         g = min(gflops / c.flops, 1.0) if c.flops > 0 else 0.0
-        compute += c.time_s * per_replica * ((1 - g) + g / tp)
+        compute += c.time_s * per_replica * ((1 - g) + g / tp) + c.fixed_s
         for a, b, tokens in lin:
             sharded_params += a * b
             nb_out = tokens * b * 2.0 * per_replica
@@ -417,7 +484,7 @@ def _tp_candidate(spine: Spine, costs, dp, tp, B, cfg, hw: Machine, opt, cap, ex
         bwd = [c.bwd_s * per_replica for c in costs]
         grad_dp = dp_exposed_s(bwd, [c.params * _reduce_bytes(cfg) / tp for c in costs], dp, hw,
                                _bucket_bytes(cfg, costs, _reduce_bytes(cfg)))
-    step = compute + comm + grad_dp
+    step = compute + comm + grad_dp + optimizer_s(local_params, opt, hw)
     return {"strategy": "tp", "dp": dp, "pp": 1, "tp": tp, "M": 1, "V": 1, "schedule": "none", "ckpt": False,
             "bounds": [0, len(costs)], "step_s": step, "compute_s": compute, "comm_s": comm + grad_dp,
             "bubble": 0.0, "mem_gb": mem, "mem_list": [mem], "fits": mem * 1e9 <= cap}

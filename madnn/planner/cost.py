@@ -39,10 +39,17 @@ class LayerCost:
     fwd_s: float = 0.0          # per-sample forward time estimate (or measurement)
     bwd_s: float = 0.0
     measured: bool = False
+    fixed_s: float = 0.0        # per-CALL fwd+bwd cost independent of the batch (launches, small-batch
+    #                             under-occupancy): one microbatch of n samples takes fixed_s + n * time_s
+    nops: int = 0               # ops dispatched by one forward (launch-count proxy)
 
     @property
     def time_s(self) -> float:
         return self.fwd_s + self.bwd_s
+
+    def call_s(self, n: float) -> float:
+        """fwd+bwd seconds of one call on ``n`` samples."""
+        return self.fixed_s + n * self.time_s
 
 
 class _BytesMode(TorchDispatchMode):
@@ -51,12 +58,14 @@ class _BytesMode(TorchDispatchMode):
     def __init__(self):
         super().__init__()
         self.bytes = 0
+        self.ops = 0
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = getattr(func, "__name__", "")
         if not any(v in name for v in ("view", "alias", "expand", "as_strided", "permute", "transpose", "detach",
                                        "t.default", "unsqueeze", "squeeze", "slice", "select", "split")):
+            self.ops += 1
             for t in (out if isinstance(out, (list, tuple)) else (out,)):
                 if isinstance(t, torch.Tensor):
                     self.bytes += t.numel() * t.element_size()
@@ -143,9 +152,11 @@ def estimate(spine: Spine, example_input: torch.Tensor, dtype: Optional[torch.dt
         out_b = y.numel() * y.element_size() / batch
         eff_flops = hw.bf16_tflops * 1e12 if (dtype in (torch.bfloat16, torch.float16)) else hw.fp32_tflops * 1e12
         fwd = flops / eff_flops + 2.0 * act / (hw.hbm_tbps * 1e12)  # write + one re-read of every output
+        # forward launches + ~2x as many in backward
+        fixed = 3.0 * bm.ops * hw.kernel_launch_us * 1e-6
         costs.append(LayerCost(name=name, params=own, shared_params=shared, flops=flops, act_bytes=act,
                                out_bytes=out_b, out_shape=tuple(y.shape[1:]), out_dtype=y.dtype,
-                               fwd_s=fwd, bwd_s=2.0 * fwd))
+                               fwd_s=fwd, bwd_s=2.0 * fwd, fixed_s=fixed, nops=bm.ops))
         x = y
     return costs
 
@@ -216,67 +227,149 @@ def _replica(layer: nn.Module, device, dtype):
     return rep, cl
 
 
+def _layer_input(i, layer_costs, example_input, b, dtype, dev):
+    if i == 0:
+        idx = torch.arange(b) % max(example_input.shape[0], 1)
+        x = example_input[idx].to(dev)
+        if x.is_floating_point():
+            x = x.to(dtype or x.dtype)
+        return x
+    prev = layer_costs[i - 1]
+    odt = prev.out_dtype or dtype
+    if odt is not None and not odt.is_floating_point:
+        return torch.zeros((b,) + tuple(prev.out_shape), dtype=odt, device=dev)
+    return torch.randn((b,) + tuple(prev.out_shape), dtype=odt, device=dev)
+
+
+def _time_call(fn, xin, iters: int):
+    """(fwd ms, bwd ms) of ``fn(xin)`` averaged over ``iters`` after two warm-up calls."""
+    for _ in range(2):
+        y = fn(xin)
+        if y.requires_grad:
+            y.backward(torch.ones_like(y))
+    start, mid, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    fw = bw = 0.0
+    for _ in range(iters):
+        start.record()
+        y = fn(xin)
+        mid.record()
+        if y.requires_grad:
+            y.backward(torch.ones_like(y))
+        end.record()
+        end.synchronize()
+        fw += start.elapsed_time(mid)
+        bw += mid.elapsed_time(end)
+    return fw / iters, bw / iters
+
+
 def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: Optional[int] = None,
                    dtype: Optional[torch.dtype] = torch.bfloat16, iters: int = 3,
-                   device: Optional[torch.device] = None) -> List[LayerCost]:
+                   device: Optional[torch.device] = None, group=None, two_point: bool = True) -> List[LayerCost]:
     """Replace the analytic times of ``costs`` with HIP-event timings on this GPU.
 
     Every DISTINCT layer (:func:`layer_signature` + input shape) is copied once onto the
-    device -- a meta-device layer is materialised -- and its forward and forward+backward
-    are timed at ``batch`` samples (default: the example input's batch), so a 24-block
-    transformer costs three measurements and an 8B model never needs to exist whole.  The
-    input of layer i is a random tensor of layer i-1's analytic output shape.  Returns
-    ``costs`` unchanged without a GPU.  This is the working version of the reference's
-    dead ``comm_speed`` probe (datamodule.lua:280-303)."""
+    device -- a meta-device layer is materialised -- and its forward and forward+backward are
+    timed at ``batch`` samples and (``two_point``) at a quarter of it, giving a per-call fixed
+    cost and a per-sample slope (``LayerCost.fixed_s`` / ``time_s``): the planner needs both to
+    price small pipeline microbatches, whose GEMMs run far below the large-batch rate.  A
+    24-block transformer costs three measurements and an 8B model never needs to exist whole.
+
+    With a process group (``group``) of W > 1 ranks the distinct layers are dealt round-robin:
+    every rank times its share on its own GPU concurrently and the results are all-gathered,
+    so no rank idles while one GPU times the whole model.  Returns ``costs`` unchanged without
+    a GPU.  This is the working version of the reference's dead ``comm_speed`` probe
+    (datamodule.lua:280-303)."""
     if not torch.cuda.is_available():
         return costs
+    import torch.distributed as dist
+
     dev = device or torch.device("cuda", torch.cuda.current_device())
     b = int(batch or max(example_input.shape[0], 1))
-    cache = {}
-    for i, (layer, c) in enumerate(zip(spine.layers, costs)):
+    b2 = max(b // 4, 1) if two_point and b >= 4 else None
+    keys, first = [], {}
+    for i, layer in enumerate(spine.layers):
         if i == 0:
             in_key = ("input", tuple(example_input.shape[1:]), str(example_input.dtype))
         else:
             in_key = (tuple(costs[i - 1].out_shape), str(costs[i - 1].out_dtype))
         key = (layer_signature(layer), in_key)
-        if key not in cache:
-            rep, cl = _replica(layer, dev, dtype)
-            if i == 0:
-                idx = torch.arange(b) % max(example_input.shape[0], 1)
-                x = example_input[idx].to(dev)
-                if x.is_floating_point():
-                    x = x.to(dtype or x.dtype)
-            else:
-                odt = costs[i - 1].out_dtype or dtype
-                if odt is not None and not odt.is_floating_point:
-                    x = torch.zeros((b,) + tuple(costs[i - 1].out_shape), dtype=odt, device=dev)
-                else:
-                    x = torch.randn((b,) + tuple(costs[i - 1].out_shape), dtype=odt, device=dev)
+        keys.append(key)
+        first.setdefault(key, i)
+    distinct = sorted(first, key=lambda k: first[k])
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    me, world = (dist.get_rank(group), dist.get_world_size(group)) if multi else (0, 1)
+    mine = {}
+    for j, key in enumerate(distinct):
+        if j % world != me:
+            continue
+        i = first[key]
+        rep, cl = _replica(spine.layers[i], dev, dtype)
+        res = []
+        for n in ([b] + ([b2] if b2 else [])):
+            x = _layer_input(i, costs, example_input, n, dtype, dev)
             if cl and x.dim() == 4:
                 x = x.contiguous(memory_format=torch.channels_last)
-            xin = x.detach().requires_grad_(x.is_floating_point())
-            for _ in range(2):
-                y = rep(xin)
-                if y.requires_grad:
-                    y.backward(torch.ones_like(y))
-            start, mid, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            fw = bw = 0.0
-            for _ in range(iters):
-                start.record()
-                y = rep(xin)
-                mid.record()
-                if y.requires_grad:
-                    y.backward(torch.ones_like(y))
-                end.record()
-                end.synchronize()
-                fw += start.elapsed_time(mid)
-                bw += mid.elapsed_time(end)
-            cache[key] = (fw / iters / 1e3 / b, bw / iters / 1e3 / b)
-            del rep, xin, y
-        c.fwd_s, c.bwd_s = cache[key]
+            # the model input needs no gradient (a conv stem's data grad is a large, slow pass the
+            # training step never runs); every later layer's input does
+            xin = x.detach().requires_grad_(x.is_floating_point() and i > 0)
+            res.append((n,) + _time_call(rep, xin, iters))
+            del x, xin
+        for p in rep.parameters():
+            p.grad = None
+        del rep
+        mine[j] = res
+    if multi:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine, group=group)
+        for g in gathered:
+            mine.update(g)
+    fitted = {}
+    for j, key in enumerate(distinct):
+        res = mine[j]
+        (n1, f1, k1) = res[0]
+        fwd_ps, bwd_ps, fixed = f1 / n1, k1 / n1, 0.0
+        if len(res) > 1:
+            (n2, f2, k2) = res[1]
+            # t(n) = fixed + n * slope through the two points (slope from the large batch when
+            # the small one is not slower per call, i.e. launch-bound noise)
+            slope_f = max((f1 - f2) / (n1 - n2), 0.0) if n1 != n2 else f1 / n1
+            slope_b = max((k1 - k2) / (n1 - n2), 0.0) if n1 != n2 else k1 / n1
+            if slope_f + slope_b > 0:
+                fixed = max((f1 + k1) - n1 * (slope_f + slope_b), 0.0)
+                fwd_ps, bwd_ps = slope_f, slope_b
+        fitted[key] = (fwd_ps / 1e3, bwd_ps / 1e3, fixed / 1e3)
+    for key, c in zip(keys, costs):
+        c.fwd_s, c.bwd_s, c.fixed_s = fitted[key]
         c.measured = True
     torch.cuda.empty_cache()
     return costs
+
+
+def measure_chain(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: int,
+                  dtype: Optional[torch.dtype] = torch.bfloat16, iters: int = 3,
+                  device: Optional[torch.device] = None) -> Optional[float]:
+    """fwd+bwd seconds of the WHOLE spine, layer after layer as the model runs them, at
+    ``batch`` samples -- the one-step calibration of the per-layer sum (isolated layer timings
+    miss the cache/launch interplay between neighbours).  None without a GPU."""
+    if not torch.cuda.is_available():
+        return None
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    reps = [_replica(layer, dev, dtype) for layer in spine.layers]
+    cl = any(c for _, c in reps)
+
+    def chain(x):
+        for rep, _ in reps:
+            x = rep(x)
+        return x
+
+    x = _layer_input(0, costs, example_input, batch, dtype, dev)
+    if cl and x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    xin = x.detach()  # the model input: no data gradient, as in the training step
+    fw, bw = _time_call(chain, xin, iters)
+    del reps, x, xin
+    torch.cuda.empty_cache()
+    return (fw + bw) / 1e3
 
 
 def param_state_bytes(params: int, optimizer: str = "adam", compute_bytes: int = 2) -> float:

@@ -115,3 +115,121 @@ def test_pp_checkpoint_restores_into_dp(tmp_path):
     assert os.path.exists(os.path.join(path, "model-00000.safetensors"))
     assert os.path.exists(os.path.join(path, "model-00001.safetensors"))
     run_dist(_w_load_into_dp, 2, path)
+
+
+# ------------------------------------------------------------- resume-exact training state
+class _DropNet(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(12, 32)
+        self.drop = torch.nn.Dropout(0.3)   # consumes the CPU RNG: resume must restore it
+        self.b = torch.nn.Linear(32, 5)
+
+    def forward(self, x):
+        return self.b(self.drop(torch.relu(self.a(x))))
+
+
+def _w_mid_epoch(rank, world, path, phase):
+    """Phase "save": one epoch + 3 steps, checkpoint mid-epoch, 5 more steps (losses kept).
+    Phase "resume": a fresh replica (other init) loads the checkpoint and must reproduce those
+    5 losses bitwise: weights, momentum, sampler cursor (same shard permutation, mid-epoch) and
+    the dropout RNG all come back.  Phase "replan": the same checkpoint at another world size."""
+    import madnn
+    from madnn import ckpt
+    from madnn.data import DistributedSampler
+    from madnn.optim import FusedSGD
+
+    g = torch.Generator().manual_seed(3)
+    data, labels = torch.randn(64, 12, generator=g), torch.randint(0, 5, (64,), generator=g)
+    torch.manual_seed(0 if phase == "save" else 99)
+    model = _DropNet()
+    opt = FusedSGD(model.parameters(), lr=0.05, momentum=0.9)
+    eng, opt = madnn.distribute(model, opt, strategy="dp")
+    sampler = DistributedSampler(len(data), shuffle=True, seed=7)
+    torch.manual_seed(1000 + rank)
+
+    def batches():
+        while True:
+            it = iter(sampler)
+            while True:
+                idx = [i for _, i in zip(range(4), it)]
+                if len(idx) < 4:
+                    break
+                yield idx
+            sampler.set_epoch(sampler.epoch + 1)
+
+    def step(idx):
+        loss = F.cross_entropy(eng(data[idx]), labels[idx])
+        loss.backward()
+        opt.step()
+        return loss.detach().clone()
+
+    mine = os.path.join(path, f"losses-{rank}.pt")
+    if phase == "save":
+        gen = batches()
+        for _ in range(len(sampler) // 4 + 3):
+            step(next(gen))
+        assert sampler.epoch == 1 and sampler.cursor == 12
+        ckpt.save(path, eng, opt, step=11, sampler=sampler)
+        losses = torch.stack([step(next(gen)) for _ in range(5)])
+        torch.save(losses, mine)
+        return
+    meta = ckpt.load(path, eng, opt, sampler=sampler)
+    assert meta["step"] == 11
+    gen = batches()
+    losses = torch.stack([step(next(gen)) for _ in range(5 if phase == "resume" else 2)])
+    if phase == "resume":
+        want = torch.load(mine, weights_only=True)
+        assert torch.equal(losses, want), (losses, want)
+    else:
+        assert sampler.epoch == 1 and torch.isfinite(losses).all()
+
+
+def test_mid_epoch_resume_is_bitwise_and_replans(tmp_path):
+    path = str(tmp_path / "mid")
+    run_dist(_w_mid_epoch, 2, path, "save")
+    assert os.path.exists(os.path.join(path, "state-dp1-pp0-tp0.pt"))
+    run_dist(_w_mid_epoch, 2, path, "resume")
+    run_dist(_w_mid_epoch, 4, path, "replan")
+
+
+def _w_trainer_resume(rank, world, path, phase):
+    """parallelize() + Trainer (reference path): the periodic-sync counter, the trainer's
+    epoch / position / permutation and the weights resume mid-epoch; finishing training from the
+    checkpoint ends on bitwise the same weights as the uninterrupted run."""
+    import madnn
+    from madnn import ckpt
+
+    g = torch.Generator().manual_seed(5)
+    data, targets = torch.randn(41, 12, generator=g), torch.randint(0, 5, (41,), generator=g)
+    torch.manual_seed(0 if phase == "save" else 42)
+    model = torch.nn.Sequential(torch.nn.Linear(12, 16), torch.nn.Tanh(), torch.nn.Linear(16, 5))
+    d, t, _ = madnn.parallelize(data, targets, model, sync_every=3, verbose=False)
+    torch.manual_seed(7)
+
+    def hook(tr, _batch):
+        if phase == "save" and tr.global_step == 6:
+            ckpt.save(path, model, tr.optimizer, step=tr.global_step, trainer=tr)
+
+    tr = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.2, learning_rate_decay=0.05,
+                       max_iteration=3, batch_size=6, verbose=False, on_example=hook)
+    if phase == "resume":
+        ckpt.load(path, model, tr.optimizer, trainer=tr)
+        # 20 samples per rank, batches of 6: step 6 is the 2nd step of epoch 2 (0-based epoch 1)
+        assert tr.global_step == 6 and tr.epoch == 1 and tr.cursor == 12
+        assert model._madnn_sync.counter == 20 + 12   # samples seen, the reference's sync unit
+    tr.train(d, t)
+    out = torch.cat([p.detach().flatten() for p in model.parameters()])
+    f = os.path.join(path, f"final-{rank}.pt")
+    if phase == "save":
+        torch.save({"w": out, "syncs": model._madnn_sync.syncs, "counter": model._madnn_sync.counter}, f)
+    else:
+        want = torch.load(f, weights_only=True)
+        assert torch.equal(out, want["w"])
+        assert model._madnn_sync.counter == want["counter"]
+
+
+def test_parallelize_trainer_resume_mid_epoch(tmp_path):
+    path = str(tmp_path / "tr")
+    run_dist(_w_trainer_resume, 2, path, "save")
+    run_dist(_w_trainer_resume, 2, path, "resume")

@@ -202,10 +202,18 @@ def _w_parallelize(rank, world, sync_every):
     torch.testing.assert_close(d, data[rank * size:(rank + 1) * size])  # contiguous stripe, remainder dropped
     if sync_every is None:
         assert model._madnn_sync.period == 1  # heuristic: local size < 1000
-    trainer = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.5, max_iteration=6,
-                            batch_size=16, verbose=False)
+    lrs = []
+    trainer = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.5, learning_rate_decay=0.1,
+                            max_iteration=6, batch_size=16, verbose=False,
+                            on_iteration=lambda tr, ep, err: lrs.append(tr.optimizer.param_groups[0]["lr"]))
+    from madnn.optim import FusedSGD
+
+    assert isinstance(trainer.optimizer, FusedSGD)  # the reference's fused accUpdateGradParameters
     hist = trainer.train(d, t)
     assert hist[-1] < hist[0]
+    assert trainer.optimizer.space is not None and len(trainer.optimizer.space.buckets) >= 1
+    # reference schedule (datamodule.lua:176-177): epoch 1 at lr, epoch k >= 2 at lr / (1 + k * decay)
+    assert lrs == pytest.approx([0.5] + [0.5 / (1 + k * 0.1) for k in range(2, 7)])
     if sync_every == -1:
         madnn.synchronize_model(model)
     for p in model.parameters():

@@ -28,7 +28,11 @@ def _w_tp_gpu(rank, world, oneshot=False):
     ref = copy.deepcopy(m).cuda()
     opt = FusedAdam(m.parameters(), lr=1e-3)
     ropt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=0.0)
-    eng, opt = madnn.distribute(m, opt, strategy="tp", tp_size=2, tp_min_params=4096, dtype="float32")
+    # default dtype: bf16 compute copies with fp32 masters (the TP-only path goes through the
+    # flat-space engine like DP), tracked against an fp32 eager copy
+    eng, opt = madnn.distribute(m, opt, strategy="tp", tp_size=2, tp_min_params=4096)
+    assert eng.h[0].mlp.c_fc.weight.dtype == torch.bfloat16
+    assert all(bk.master.dtype == torch.float32 for bk in eng.space.buckets)
     from madnn import comm
     probe = torch.zeros(4 * 64 * 256, device="cuda")
     sel = comm.select(probe, "all_reduce", mlp_group := eng.h[0].mlp.c_proj.group)
@@ -45,7 +49,7 @@ def _w_tp_gpu(rank, world, oneshot=False):
         rl.backward()
         ropt.step()
         ropt.zero_grad()
-        assert abs(float(loss) - float(rl)) < 1e-3 * float(rl), (float(loss), float(rl))
+        assert abs(float(loss) - float(rl)) < 2e-2 * float(rl), (float(loss), float(rl))
 
 
 def test_tp2_gpt_on_device(cuda):

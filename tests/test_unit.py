@@ -340,11 +340,37 @@ def test_planner_interleaved_plan_shape():
     ex = torch.zeros(1, 1024, dtype=torch.long)
     p = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, schedule="interleaved", global_batch=64), 4,
                    example_input=ex)
-    assert p.virtual == 2 and p.schedule == "interleaved" and len(p.bounds) == 4 * 2 + 1
+    assert p.virtual in (2, 4) and p.schedule == "interleaved" and len(p.bounds) == 4 * p.virtual + 1
     assert p.microbatches % 4 == 0
-    q = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, global_batch=64), 4, example_input=ex)
+    q = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, schedule="1f1b", global_batch=64), 4,
+                   example_input=ex)
     # same work, smaller bubble
     assert p.est_step_s < q.est_step_s
+    v2 = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, schedule="interleaved", virtual_stages=2,
+                                       microbatches=16, global_batch=64), 4, example_input=ex)
+    assert (v2.virtual, v2.microbatches) == (2, 16)
+
+
+def test_planner_searches_schedules_and_microbatches():
+    """schedule="auto" (the default): every PP row of the table is one (schedule, V, M) variant --
+    GPipe, 1F1B and interleaved with 2 and 4 chunks at several microbatch counts -- and the
+    chosen one is the cheapest feasible row."""
+    from madnn.models.gpt2 import GPT2, gpt2_config
+    from madnn.planner import plan_model
+
+    with torch.device("meta"):
+        m = GPT2(gpt2_config("gpt2-medium"))
+    ex = torch.zeros(1, 1024, dtype=torch.long)
+    p = plan_model(m, Config.from_env(strategy="pp", pp_stages=4, global_batch=64), 4, example_input=ex)
+    rows = {(c["schedule"], c["V"], c["M"]) for c in p.candidates}
+    assert {"gpipe", "1f1b", "interleaved"} <= {r[0] for r in rows}
+    assert {2, 4} <= {r[1] for r in rows if r[0] == "interleaved"}
+    assert {4, 8, 16} <= {r[2] for r in rows if r[0] == "1f1b"}
+    assert "| interleaved |" in p.table()
+    best = min((c for c in p.candidates if c["fits"]), key=lambda c: c["step_s"])
+    assert (p.schedule, p.virtual, p.microbatches) == (best["schedule"], best["V"], best["M"])
+    # per-call fixed costs make tiny microbatches expensive: the search does not just max out M
+    assert all(c["step_s"] > 0 for c in p.candidates)
 
 
 def test_measured_costs_change_the_placement():
@@ -364,11 +390,11 @@ def test_measured_costs_change_the_placement():
     p0 = plan_model(m, cfg, 8, example_input=ex, costs=copy.deepcopy(base))
     fast = copy.deepcopy(base)
     for c in fast:
-        c.fwd_s, c.bwd_s, c.measured = c.fwd_s / 100, c.bwd_s / 100, True
+        c.fwd_s, c.bwd_s, c.fixed_s, c.measured = c.fwd_s / 100, c.bwd_s / 100, c.fixed_s / 100, True
     p1 = plan_model(m, cfg, 8, example_input=ex, costs=fast)
     assert p1.measured and not p0.measured
     assert (p0.strategy, p0.dp, p0.pp, p0.tp) != (p1.strategy, p1.dp, p1.pp, p1.tp)
-    cfg_pp = Config.from_env(strategy="pp", pp_stages=4, global_batch=64)
+    cfg_pp = Config.from_env(strategy="pp", pp_stages=4, schedule="1f1b", microbatches=8, global_batch=64)
     q0 = plan_model(m, cfg_pp, 4, example_input=ex, costs=copy.deepcopy(base))
     skew = copy.deepcopy(base)
     for c in skew[1:6]:  # the first blocks measure 3x slower than the model says
