@@ -13,13 +13,14 @@ Default (the driver's contract) measures BOTH halves of the metric in one run:
   profiles/r2_resnet_b1024.md; 11.38k at 1024 vs 11.59k at 1536, profiles/r2_resnet_b1536.md;
   12.65k at 1536 vs 12.85k at 2048, profiles/r2_resnet_b2048.md);
 * ``gpt2_pp``: GPT-2 medium (seq 1024, bf16, FusedAdam), pipeline parallel over
-  RCCL P2P with the interleaved 1F1B schedule (2 model chunks per rank) -- ``pp2`` at 2
-  GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1 GPU (a pipeline needs two
-  stages); 64 sequences per GPU (weak scaling), 16-sequence microbatches.  The sizes come
-  from a 1-GPU sweep (profiles/r2_gpt2m_dp1_batch_sweep.jsonl): GEMM efficiency keeps
-  rising with the rows per GEMM (4 / 8 / 16 / 32 / 64 sequences: 194k / 235k / 277k /
-  308k / 326k tok/s), and interleaving keeps the bubble small (16 microbatches per replica at
-  pp4: 8.6 % simulated, vs 15.8 % for plain 1F1B).
+  RCCL P2P -- ``pp2`` at 2 GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1 GPU
+  (a pipeline needs two stages); 64 sequences per GPU (weak scaling).  The schedule (GPipe,
+  1F1B, interleaved with 2 or 4 chunks per rank) and the microbatch count are the planner's
+  choice (``--schedule auto``): it prices every variant with layer costs measured on the
+  GPUs of the job (per-call fixed cost + per-sample slope, so small microbatches pay for
+  their lower GEMM efficiency: profiles/r2_gpt2m_dp1_batch_sweep.jsonl, 4 / 8 / 16 / 32 / 64
+  sequences: 194k / 235k / 277k / 308k / 326k tok/s) against the simulated bubble.
+  ``--schedule`` / ``--microbatches`` / ``--gpt2-mb`` pin them by hand.
 
 Synthetic data and random init (no network on the box).  ``--model resnet50`` /
 ``--model gpt2-medium`` run one half only.  Without a launcher environment the
@@ -57,10 +58,13 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
     ap.add_argument("--gpt2-batch-per-gpu", type=int, default=64, help="GPT-2 sequences per GPU (global = this x N)")
     ap.add_argument("--gpt2-config", default="gpt2-medium", help="GPT-2 size (gpt2-tiny for CPU harness tests)")
-    ap.add_argument("--gpt2-mb", type=int, default=16, help="GPT-2 sequences per pipeline microbatch")
+    ap.add_argument("--gpt2-mb", type=int, default=0,
+                    help="GPT-2 sequences per pipeline microbatch (0: the planner picks the microbatch count)")
     ap.add_argument("--gpt2-steps", type=int, default=None, help="GPT-2 timed steps (default: --steps)")
     ap.add_argument("--gpt2-warmup", type=int, default=None, help="GPT-2 warmup steps (default: --warmup)")
-    ap.add_argument("--schedule", default="interleaved", help="pipeline schedule (gpipe | 1f1b | interleaved)")
+    ap.add_argument("--schedule", default="auto",
+                    help="pipeline schedule (auto: the planner prices gpipe / 1f1b / interleaved V=2,4 at every "
+                         "microbatch count and picks the cheapest | gpipe | 1f1b | interleaved)")
     ap.add_argument("--no-pg", action="store_true", help="no world-1 process group when run without a launcher")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
@@ -166,14 +170,14 @@ def bench_gpt2(args, world, rank):
     strategy, stages, par = gpt2_layout(world)
     dp = world // stages
     per_replica = gbatch // dp
-    micro = args.microbatches or (max(per_replica // args.gpt2_mb, 1) if stages > 1 else None)
+    micro = args.microbatches or (max(per_replica // args.gpt2_mb, 1) if stages > 1 and args.gpt2_mb else None)
     torch.manual_seed(0)
     model = GPT2(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
     kw = {}
     if args.schedule and stages > 1:
         sched = args.schedule
-        if sched == "interleaved" and (micro or 1) % stages:
+        if sched == "interleaved" and micro and micro % stages:
             sched = "1f1b"  # interleaving needs microbatches % stages == 0
         kw["schedule"] = sched
     engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if stages > 1 else None,
@@ -204,7 +208,8 @@ def bench_gpt2(args, world, rank):
     if loss is not None and (stages == 1 or rank % stages == stages - 1):
         lv = float(loss.detach())
     info = {"model": args.gpt2_config, "global_batch": gbatch, "per_gpu_batch": args.gpt2_batch_per_gpu,
-            "seq_len": args.seq_len, "parallelism": par, "microbatches": micro if stages > 1 else 1,
+            "seq_len": args.seq_len, "parallelism": par, "microbatches": getattr(engine, "M", 1) if stages > 1 else 1,
+            "planned_step_ms": round(engine.plan.est_step_s * 1e3, 2) if getattr(engine, "plan", None) else None,
             "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
             "virtual_stages": getattr(engine, "V", None) if stages > 1 else None,
             "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "loss_last_stage": lv,

@@ -33,6 +33,7 @@ class LlamaConfig:
 
 _SIZES = {
     "llama3-8b": dict(),
+    "llama3-70b": dict(hidden=8192, intermediate=28672, layers=80, heads=64, kv_heads=8),
     "llama3-1b": dict(hidden=2048, intermediate=8192, layers=16, heads=32, kv_heads=8),
     "llama3-tiny": dict(vocab_size=512, hidden=64, intermediate=160, layers=4, heads=4, kv_heads=2,
                         max_position=256),

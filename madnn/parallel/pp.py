@@ -734,7 +734,17 @@ class PipelineEngine:
         ref = inputs if inputs is not None else targets
         sig = (tuple(ref.shape), ref.dtype) if ref is not None else "static"
         new_sig = sig != self._sig
-        if self._needs_tied:  # a previous step's gradients were never consumed: drop its tied sums
+        if self.dp._needs_finalize:
+            # gradient accumulation across train_step calls (no optimizer step in between)
+            if self.tied:
+                # the tied slots already hold the cross-stage SUM; summing them again at the end
+                # of this step would count the first step's gradients twice
+                raise RuntimeError("pipeline: train_step called again before optimizer.step() with parameters "
+                                   "tied across stages; accumulate with more microbatches instead")
+            if self.dp.comm_stream is not None:
+                # this step's in-place accumulation must follow the previous step's reduction
+                torch.cuda.current_stream().wait_stream(self.dp.comm_stream)
+        if self._needs_tied:
             self._wait_tied()
         pend = {} if new_sig else self._prepost()
         acts_in: Dict[tuple, torch.Tensor] = {}
@@ -848,6 +858,9 @@ class PipelineEngine:
         """(groups to sum squared gradient norms over, params to leave out of this rank's sum):
         pipeline ranks hold disjoint parameters except tied ones, counted on their first owner."""
         skip = [p for p, _g, src in self.tied if src != rt.get_rank()]
+        # the pipeline mesh has no tensor-parallel axis (build_pipeline: tp=1); a TP x PP layout
+        # would also have to sum over the tp group and skip TP-replicated parameters
+        assert self.groups.mesh.tp == 1, "clip_grad_norm_ over a tp x pp mesh is not supported"
         return ([self.groups.pp_group] if self.nstages > 1 else []), skip
 
     def after_step(self):

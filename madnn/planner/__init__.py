@@ -83,7 +83,8 @@ class Plan:
                 "est step (ms) | max mem/GPU (GB) | fits |",
                 "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
         for c in sorted(self.candidates, key=lambda c: c["step_s"]):
-            rows.append(f"| {c['strategy']} | {c['dp']} | {c['pp']} | {c.get('tp', 1)} | {c.get('schedule', '-')} | "
+            sched = c.get("schedule", "-") + (f" V={c['V']}" if c.get("V", 1) > 1 else "")
+            rows.append(f"| {c['strategy']} | {c['dp']} | {c['pp']} | {c.get('tp', 1)} | {sched} | "
                         f"{c['M']} | {c['ckpt']} | {c.get('compute_s', 0) * 1e3:.2f} | "
                         f"{c.get('comm_s', 0) * 1e3:.2f} | {c.get('bubble', 0):.3f} | {c['step_s'] * 1e3:.2f} | "
                         f"{c['mem_gb']:.1f} | {c['fits']} |")

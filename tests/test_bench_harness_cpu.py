@@ -92,12 +92,12 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     assert res["gpt2_pp"]["microbatches"] == 4 and res["gpt2_pp"]["model"] == "gpt2-medium"
 
 
-def _gpt2_8rank(extra_env=None, timeout=900):
+def _gpt2_8rank(extra_env=None, timeout=900, extra_args=()):
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
            "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "1", "--warmup", "1",
-           "--device", "cpu", "--model", "gpt2-medium", "--gpt2-batch-per-gpu", "2", "--gpt2-mb", "1",
-           "--seq-len", "16"]
+           "--device", "cpu", "--model", "gpt2-medium", "--gpt2-batch-per-gpu", "2", "--seq-len", "16",
+           *extra_args]
     env = dict(os.environ, OMP_NUM_THREADS="1", MADNN_LOG_LEVEL="WARNING", **(extra_env or {}))
     return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
 
@@ -107,7 +107,8 @@ def test_bench_py_gpt2_dp2_pp4_interleaved_eight_ranks_emulated_rccl():
     dp2 x pp4, interleaved 1F1B with 2 model chunks per rank (short sequences, CPU/gloo) -- with
     every pipeline group's point-to-point ops serialised in issue order, as eagerly initialised
     RCCL communicators execute them (``MADNN_EMULATE_RCCL_P2P``)."""
-    out = _gpt2_8rank({"MADNN_EMULATE_RCCL_P2P": "1", "MADNN_EMULATE_RCCL_P2P_TIMEOUT": "120"})
+    out = _gpt2_8rank({"MADNN_EMULATE_RCCL_P2P": "1", "MADNN_EMULATE_RCCL_P2P_TIMEOUT": "120"},
+                      extra_args=("--schedule", "interleaved", "--microbatches", "8"))
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -115,7 +116,19 @@ def test_bench_py_gpt2_dp2_pp4_interleaved_eight_ranks_emulated_rccl():
     pp = res["gpt2_pp"]
     assert res["n_gpus"] == 8 and res["value"] > 0 and "error" not in pp
     assert res["config"]["parallelism"] == "dp2xpp4"
-    assert pp["schedule"] == "interleaved" and pp["virtual_stages"] == 2 and pp["microbatches"] == 8
+    assert pp["schedule"] == "interleaved" and pp["virtual_stages"] in (2, 4) and pp["microbatches"] == 8
+
+
+def test_bench_py_gpt2_eight_ranks_planner_schedule_emulated_rccl():
+    """The default bench: the planner picks the schedule and microbatch count of the dp2 x pp4
+    GPT-2 half (here from analytic costs), run under the emulated RCCL serialisation."""
+    out = _gpt2_8rank({"MADNN_EMULATE_RCCL_P2P": "1", "MADNN_EMULATE_RCCL_P2P_TIMEOUT": "120"})
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    pp = res["gpt2_pp"]
+    assert "error" not in pp and res["config"]["parallelism"] == "dp2xpp4"
+    assert pp["schedule"] in ("gpipe", "1f1b", "interleaved") and pp["planned_step_ms"] > 0
+    assert 16 % pp["microbatches"] == 0
 
 
 def test_bench_py_gpt2_shared_groups_deadlock_under_emulated_rccl():

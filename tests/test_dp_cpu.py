@@ -378,3 +378,46 @@ def test_grad_sink_writes_in_place_cpu():
     # a second accumulation (no_sync microbatch) adds in place into the same slot
     ops.linear(x, lin.weight, lin.bias, force_fn=True).square().sum().backward()
     torch.testing.assert_close(lin.weight.grad, 2 * ref.weight.grad)
+
+
+def _w_bf16_reduce(rank, world, out_dir):
+    """reduce_dtype="auto" all-reduces bf16 parameters' gradient buckets in bf16. At
+    8 ranks that tracks the fp32 reduction within bf16 rounding (checked against an fp32-reduce
+    run of the same bf16 model and against fp32 single-process training)."""
+    import madnn
+    from madnn.models import MLP
+    from madnn.optim import FusedSGD
+
+    g = torch.Generator().manual_seed(9)
+    x, y = torch.randn(8 * world, 32, generator=g), torch.randint(0, 10, (8 * world,), generator=g)
+    finals = {}
+    for rd in ("auto", "float32"):
+        torch.manual_seed(0)
+        m = MLP(32, 64, 10)
+        opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9)
+        eng, opt = madnn.distribute(m, opt, strategy="dp", reduce_dtype=rd, cpu_dtype="bfloat16")
+        assert {bk.grad_dtype for bk in eng.space.buckets} == ({torch.bfloat16} if rd == "auto" else {torch.float32})
+        for _ in range(3):
+            xs, ys = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+            F.cross_entropy(eng(xs).float(), ys).backward()
+            opt.step()
+        finals[rd] = torch.cat([eng.space.master_view(p).flatten() for p in m.parameters()])
+        eng.remove_hooks()
+    torch.manual_seed(0)
+    ref = MLP(32, 64, 10)
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    for _ in range(3):
+        F.cross_entropy(ref(x), y).backward()
+        ropt.step()
+        ropt.zero_grad()
+    want = torch.cat([p.detach().flatten() for p in ref.parameters()])
+    d_auto = (finals["auto"] - want).abs().max().item()
+    d_f32 = (finals["float32"] - want).abs().max().item()
+    # bf16 compute dominates the error; the bf16 reduction adds at most its own rounding on top
+    assert d_auto < 3e-2 and d_f32 < 3e-2, (d_auto, d_f32)
+    assert (finals["auto"] - finals["float32"]).abs().max().item() < 2e-2
+    _check_same_across_ranks(finals["auto"])
+
+
+def test_bf16_reduce_tracks_fp32_reduce_at_8_ranks(tmp_path):
+    run_dist(_w_bf16_reduce, 8, str(tmp_path))

@@ -179,3 +179,40 @@ def _w_meta_tied(rank, world):
 
 def test_pp_meta_model_tied_weights_by_name():
     run_dist(_w_meta_tied, 2)
+
+
+def _w_accumulate(rank, world):
+    """two train_steps then one optimizer step equal one step on the concatenated
+    batch (no tied parameters); with GPT-2's tied wte/lm_head a second train_step raises."""
+    import madnn
+    from madnn.optim import FusedSGD
+
+    torch.manual_seed(0)
+    model = _Deep()
+    ref = copy.deepcopy(model)
+    opt = FusedSGD(model.parameters(), lr=0.1)
+    eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=2, microbatches=2, schedule="1f1b",
+                                example_input=torch.randn(1, 16), loss_fn=F.cross_entropy, checkpointing="none")
+    g = torch.Generator().manual_seed(4)
+    x, y = torch.randn(8, 16, generator=g), torch.randint(0, 5, (8,), generator=g)
+    eng.train_step(x[:4], y[:4])
+    eng.train_step(x[4:], y[4:])
+    opt.step()
+    ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    (F.cross_entropy(ref(x[:4]), y[:4]) + F.cross_entropy(ref(x[4:]), y[4:])).backward()
+    ropt.step()
+    ref_params = dict(ref.named_parameters())
+    for name, p in eng.state_dict().items():
+        torch.testing.assert_close(p.detach(), ref_params[name].detach(), atol=1e-5, rtol=1e-5)
+    gm = _gpt_tiny()
+    gopt = FusedSGD(gm.parameters(), lr=0.1)
+    geng, gopt = madnn.distribute(gm, gopt, strategy="pp", pp_stages=2, microbatches=2, schedule="1f1b",
+                                  example_input=torch.zeros(1, 16, dtype=torch.long), checkpointing="none")
+    ids = torch.randint(0, 512, (4, 16), generator=g)
+    geng.train_step(ids, ids)
+    with pytest.raises(RuntimeError, match="tied"):
+        geng.train_step(ids, ids)
+
+
+def test_pp_gradient_accumulation_across_train_steps():
+    run_dist(_w_accumulate, 2)

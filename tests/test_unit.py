@@ -366,11 +366,28 @@ def test_planner_searches_schedules_and_microbatches():
     assert {"gpipe", "1f1b", "interleaved"} <= {r[0] for r in rows}
     assert {2, 4} <= {r[1] for r in rows if r[0] == "interleaved"}
     assert {4, 8, 16} <= {r[2] for r in rows if r[0] == "1f1b"}
-    assert "| interleaved |" in p.table()
+    assert "| interleaved V=2 |" in p.table() and "| interleaved V=4 |" in p.table()
     best = min((c for c in p.candidates if c["fits"]), key=lambda c: c["step_s"])
     assert (p.schedule, p.virtual, p.microbatches) == (best["schedule"], best["V"], best["M"])
     # per-call fixed costs make tiny microbatches expensive: the search does not just max out M
     assert all(c["step_s"] > 0 for c in p.candidates)
+
+
+def test_planner_auto_pipeline_when_a_replica_does_not_fit():
+    """Automatic placement picks a pipeline when no data-parallel replica fits one GPU: Llama-3
+    70B (~1.1 TB of mixed-precision Adam state) at 8 GPUs becomes pp=8 with checkpointing and the
+    cheapest schedule, every stage inside 288 GB; the DP rows are all marked as not fitting."""
+    from madnn.models.llama import Llama, llama_config
+    from madnn.planner import plan_model
+
+    with torch.device("meta"):
+        m = Llama(llama_config("llama3-70b"))
+    p = plan_model(m, Config.from_env(strategy="auto"), 8, example_input=torch.zeros(1, 2048, dtype=torch.long),
+                   global_batch=32)
+    assert (p.strategy, p.dp, p.pp) == ("pp", 1, 8), p.describe()
+    assert max(p.est_mem_gb) <= 309.3 * 0.85 and any(p.checkpoint)
+    assert all(not c["fits"] for c in p.candidates if c["strategy"] == "dp")
+    assert "V=" in p.table() or p.virtual == 1
 
 
 def test_measured_costs_change_the_placement():
