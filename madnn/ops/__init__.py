@@ -1041,6 +1041,54 @@ def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
     return space.grad_slot(weight)
 
 
+WGRAD = os.environ.get("MADNN_WGRAD", "auto")  # weight-gradient GEMM: auto (timed per shape) | lt | k12
+_WGRAD_CHOICE: dict = {}
+
+
+def _wgrad_k12_ok(g2, x2, out) -> bool:
+    return (_is_dev(g2) and g2.dtype == x2.dtype == out.dtype == torch.bfloat16 and g2.shape[0] % 64 == 0
+            and g2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and g2.is_contiguous() and x2.is_contiguous()
+            and out.is_contiguous() and load_kernels())
+
+
+def _time_wgrad(fn, iters: int = 3) -> float:
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """``out[N, K] = g2[M, N]^T @ x2[M, K]``: a Linear's weight gradient, reduced over the M tokens.
+
+    Two implementations: hipBLASLt (``torch.mm``) and K12 with the tokens split over several
+    workgroups per output tile (``linear_wgrad``).  A weight gradient has few output tiles and a
+    very long reduction (GPT-2 medium: 16-64 tiles of 256^2 over 65536 tokens), which leaves most
+    of the 256 CUs idle unless the reduction is split; hipBLASLt's choice does not always split
+    (``profiles/r3_wgrad_ab.json``: 1.9x on the attention projection, 1.15x on c_fc, 0.95x on
+    c_proj).  ``MADNN_WGRAD=auto`` times both once per (M, N, K) on first use (like cuDNN's
+    benchmark mode; never under graph capture) and keeps the faster."""
+    if WGRAD == "lt" or not _wgrad_k12_ok(g2, x2, out):
+        return torch.mm(g2.t(), x2, out=out)
+    if WGRAD == "k12":
+        return torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0)
+    key = (g2.shape[0], g2.shape[1], x2.shape[1])
+    choice = _WGRAD_CHOICE.get(key)
+    if choice is None:
+        if torch.cuda.is_current_stream_capturing():
+            return torch.mm(g2.t(), x2, out=out)
+        t_lt = _time_wgrad(lambda: torch.mm(g2.t(), x2, out=out))
+        t_k12 = _time_wgrad(lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0))
+        choice = _WGRAD_CHOICE[key] = "k12" if t_k12 < t_lt else "lt"
+    if choice == "k12":
+        return torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0)
+    return torch.mm(g2.t(), x2, out=out)
+
+
 LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)
 _LT_FAILED = {}   # (gelu, residual) -> the error that disabled that epilogue kind
 _LT_KIND = {"gelu": os.environ.get("MADNN_LT_GELU", "1") != "0", "res": os.environ.get("MADNN_LT_RES", "1") != "0"}
@@ -1074,7 +1122,8 @@ class _LinearFn(torch.autograd.Function):
     Forward: one hipBLASLt GEMM whose epilogue adds the bias, applies the GELU (keeping the
     pre-activation as its AUX output for the backward) and adds the residual stream -- no
     standalone elementwise passes.  Backward: the bias gradient (and the GELU backward) come from
-    one K11 pass, the two GEMMs stay on hipBLASLt, and the weight-gradient GEMM writes straight
+    one K11 pass, the data-gradient GEMM stays on hipBLASLt, and the weight-gradient GEMM
+    (:func:`wgrad_into`: hipBLASLt or K12 split-K, whichever is faster for the shape) writes straight
     into the reducer's bucket when the weight has a :func:`grad_sink`; the residual's gradient is
     the output gradient itself (no copy)."""
 
@@ -1129,8 +1178,9 @@ class _LinearFn(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             sink = grad_sink(ctx.param)
             if sink is not None and sink.dtype == g2.dtype == x2.dtype and sink.is_contiguous():
-                torch.mm(g2.t(), x2, out=sink)
-                dw = sink
+                dw = wgrad_into(g2, x2, sink)
+            elif weight.dtype == g2.dtype == x2.dtype and _is_dev(g2):
+                dw = wgrad_into(g2, x2, torch.empty(weight.shape, dtype=weight.dtype, device=weight.device))
             else:
                 dw = (g2.t() @ x2).to(weight.dtype)
         ctx.param = None

@@ -99,6 +99,9 @@ hipError_t madnn_conv3x3_wgrad(const void*, const void*, float*, void*, int, int
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
+int madnn_wgrad_splits(int64_t, int64_t, int64_t);
+hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
+                              hipStream_t);
 }
 
 namespace {
@@ -719,6 +722,37 @@ at::Tensor linear_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::op
   return dx;
 }
 
+// dW[N, K] = dy[M, N]^T x[M, K] over the M tokens, split along M (fp32 slabs + reduce) so the few
+// output tiles of a weight gradient fill the GPU.  With `out` the result is written there (the
+// reducer's bucket slot: a grad sink), with accumulate added to its contents.  splits <= 0: auto.
+at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                        bool accumulate, int64_t splits) {
+  gemm_check(dy, "dy");
+  gemm_check(x, "x");
+  const int64_t N = dy.size(-1), K = x.size(-1), M = dy.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(x.numel() == M * K, "linear_wgrad: dy / x token mismatch");
+  TORCH_CHECK(M % 64 == 0 && madnn_gemm_supported(K, N, M, K, N), "linear_wgrad: unsupported shape M=", M, " N=", N,
+              " K=", K);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dw;
+  if (out.has_value() && out->defined()) {
+    gemm_check(*out, "out");
+    TORCH_CHECK(out->numel() == N * K, "linear_wgrad: out must hold N x K");
+    dw = *out;
+  } else {
+    TORCH_CHECK(!accumulate, "linear_wgrad: accumulate needs out");
+    dw = at::empty({N, K}, dy.options());
+  }
+  const int sp = splits > 0 ? (int)splits : madnn_wgrad_splits(M, N, K);
+  at::Tensor ws = sp > 1 ? at::empty({sp, N, K}, dy.options().dtype(at::kFloat)) : at::Tensor();
+  check(madnn_linear_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr, sp,
+                           accumulate ? 1 : 0, M, N, K, cur_stream(dy)),
+        "linear_wgrad");
+  return dw;
+}
+
+int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) { return madnn_wgrad_splits(M, N, K); }
+
 // ---- K13 NHWC 3x3 / stride 1 / pad 1 convolution on MFMA --------------------------------------
 // x: [N, Ci, H, W] channels_last bf16; w: [Co, Ci, 3, 3] channels_last ([Co][3][3][Ci] in memory).
 std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
@@ -1155,6 +1189,8 @@ TORCH_LIBRARY(madnn, m) {
   m.def("stem_fwd(Tensor x, Tensor wp, bool stats) -> (Tensor, Tensor)");
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
+  m.def("linear_wgrad(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
+  m.def("wgrad_splits(int M, int N, int K) -> int", &wgrad_splits);
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, bool out_bf16) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
@@ -1217,6 +1253,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("stem_wgrad", stem_wgrad);
   m.impl("linear_fwd", linear_fwd);
   m.impl("linear_dgrad", linear_dgrad);
+  m.impl("linear_wgrad", linear_wgrad);
   m.impl("conv3x3_fwd", conv3x3_fwd);
   m.impl("conv3x3_wgrad", conv3x3_wgrad);
 }

@@ -15,6 +15,10 @@
 //   * "col" operand memory: X[k][x], x contiguous (ds_read_b64_tr_b16 fragments).
 //   linear forward : i = out feature (A = W[n][k], row), j = token (B = X[m][k], row)
 //   linear dgrad   : i = in feature  (A = W[n][k] read as [k=n][i], col), j = token (B = dY, row)
+//   linear wgrad   : i = in feature  (A = X[m][k], col), j = out feature (B = dY[m][n], col); the
+//                    reduction runs over the TOKENS (65536 for GPT-2 at 64 x 1024), the output is
+//                    small (a few 256^2 tiles), so the reduction is split over `splits` workgroups
+//                    per tile: fp32 partial slabs + one streaming reduce (wgrad_reduce_kernel).
 // i sits on the accumulator rows, j on the MFMA lane, so a lane owns 4 consecutive i of one
 // output row (the same orientation as K9, conv.hip).
 //
@@ -72,6 +76,9 @@ struct Args {
   int64_t I, J, K;
   int i_tiles, j_tiles;
   int bias_f32, act;    // act: 0 none, 1 tanh-GELU
+  float* ws;            // split-K: fp32 partial slabs [splits][J][I] (null: bf16 epilogue)
+  int splits;           // workgroups per output tile along the reduction
+  int64_t kper;         // reduction elements per split (multiple of kBK)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -134,9 +141,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
     wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
   }
+  const int ntile = p.i_tiles * p.j_tiles;
+  const int split = wid / ntile;
+  wid -= split * ntile;
   const int it = wid % p.i_tiles, jt = wid / p.i_tiles;
   const int64_t i0 = (int64_t)it * kT, j0 = (int64_t)jt * kT;
-  const int nk = (int)(p.K / kBK);
+  const int64_t kbeg = (int64_t)split * p.kper;
+  const int64_t klen = p.K - kbeg < p.kper ? p.K - kbeg : p.kper;
+  const int nk = (int)(klen / kBK);
   const int total = 4 * nk;  // half-tiles
 
   // per-lane DMA offsets: part (0,1: A halves; 2,3: B halves) x 2 instructions per wave
@@ -154,7 +166,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
   // 2,3: A halves (the B halves are consumed first, so they are restaged first)
   auto stage = [&](int H) {
     const int u = H >> 2, part = (H + 2) & 3;
-    const int64_t k0 = (int64_t)u * kBK;
+    const int64_t k0 = kbeg + (int64_t)u * kBK;
     const uint16_t* base;
     if (part < 2) {
       const int64_t x0 = i0 + 128 * part;
@@ -264,6 +276,28 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
   }
   if (wr == 0) barrier();  // balance the stagger: every wave has now passed the same barriers
 
+  if (p.ws != nullptr) {
+    // split-K partial: fp32 straight from the accumulators, 4 consecutive i (16 B) per lane
+    float* slab = p.ws + (int64_t)split * p.J * p.I;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t ig = i0 + wr * 128 + a * 32 + 8 * g + 4 * hh;
+        if (ig >= p.I) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int64_t jg = j0 + wc * 64 + b * 32 + l32;
+          if (jg < p.J) {
+            *reinterpret_cast<f32x4*>(slab + jg * p.I + ig) =
+                f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+          }
+        }
+      }
+    }
+    return;
+  }
+
   // ---- epilogue: (acc + bias) -> bf16 -> LDS [256 j][256 i] -> rows
   char* ot = reinterpret_cast<char*>(smem);
 #pragma unroll
@@ -331,11 +365,44 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
   }
 }
 
+// out[e] = bf16(sum_s ws[s][e] (+ out[e])), 8 elements per lane, 16-B accesses
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, uint16_t* out, int splits,
+                                                           int64_t n, int accumulate) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; e < n; e += stride) {
+    f32x4 lo = *reinterpret_cast<const f32x4*>(ws + e), hi = *reinterpret_cast<const f32x4*>(ws + e + 4);
+    for (int q = 1; q < splits; ++q) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(ws + (int64_t)q * n + e);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(ws + (int64_t)q * n + e + 4);
+      lo += a;
+      hi += b;
+    }
+    if (accumulate) {
+      const u32x4 o = *reinterpret_cast<const u32x4*>(out + e);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        lo[2 * k] += bf16_to_f32((unsigned short)(o[k] & 0xffffu));
+        lo[2 * k + 1] += bf16_to_f32((unsigned short)(o[k] >> 16));
+        hi[2 * k] += bf16_to_f32((unsigned short)(o[2 + k] & 0xffffu));
+        hi[2 * k + 1] += bf16_to_f32((unsigned short)(o[2 + k] >> 16));
+      }
+    }
+    u32x4 v;
+    v[0] = (unsigned)f32_to_bf16(lo[0]) | ((unsigned)f32_to_bf16(lo[1]) << 16);
+    v[1] = (unsigned)f32_to_bf16(lo[2]) | ((unsigned)f32_to_bf16(lo[3]) << 16);
+    v[2] = (unsigned)f32_to_bf16(hi[0]) | ((unsigned)f32_to_bf16(hi[1]) << 16);
+    v[3] = (unsigned)f32_to_bf16(hi[2]) | ((unsigned)f32_to_bf16(hi[3]) << 16);
+    *reinterpret_cast<u32x4*>(out + e) = v;
+  }
+}
+
 template <bool A_COL, bool B_COL>
 hipError_t launch(Args& p, hipStream_t s) {
   p.i_tiles = (int)((p.I + kT - 1) / kT);
   p.j_tiles = (int)((p.J + kT - 1) / kT);
-  const int64_t grid = (int64_t)p.i_tiles * p.j_tiles;
+  if (p.splits < 1) p.splits = 1;
+  if (p.kper <= 0) p.kper = p.K;
+  const int64_t grid = (int64_t)p.i_tiles * p.j_tiles * p.splits;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
@@ -397,6 +464,59 @@ hipError_t madnn_linear_dgrad(const void* dy, const void* w, const void* res, vo
   p.J = M;
   p.K = N;
   return launch<true, false>(p, s);
+}
+
+// Workgroups per output tile for a weight gradient: 256 CUs, one 128-KiB-LDS workgroup per CU.
+// Model: rounds of 256 workgroups x k-steps per split (~1.8 us per 256^2 x 64 step at ~1.2 PF/s)
+// + the fp32 slab round trip (splits x I x J x 8 B at ~5 TB/s); splits keep >= 8 k-steps each.
+int madnn_wgrad_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((K + kT - 1) / kT) * ((N + kT - 1) / kT);
+  const int64_t nk = M / kBK;
+  int best = 1;
+  double best_t = 1e30;
+  for (int sp = 1; sp <= 32; ++sp) {
+    if (nk / sp < 8) break;
+    const int64_t kper_steps = (nk + sp - 1) / sp;
+    const int64_t rounds = (tiles * sp + 255) / 256;
+    const double t = rounds * kper_steps * 1.8 + (sp > 1 ? sp * (double)N * K * 8.0 / 5.0e6 : 0.0);
+    if (t < best_t * 0.98) {
+      best_t = t;
+      best = sp;
+    }
+  }
+  return best;
+}
+
+// dW[n][k] (+)= sum_m dY[m][n] X[m][k] (bf16 out; with accumulate the existing dW is added).
+// ws: splits x N x K fp32 workspace when splits > 1 (madnn_wgrad_splits), else unused.
+hipError_t madnn_linear_wgrad(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
+                              int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  if (M % kBK || !madnn_gemm_supported(K, N, M, K, N)) return hipErrorInvalidValue;
+  if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
+  Args p{};
+  p.a = static_cast<const uint16_t*>(x);   // A[i = k][kk = m] = X[m][k]: column memory
+  p.lda = K;
+  p.b = static_cast<const uint16_t*>(dy);  // B[kk = m][j = n] = dY[m][n]: column memory
+  p.ldb = N;
+  p.out = static_cast<uint16_t*>(dw);
+  p.ldo = K;
+  p.res = accumulate && splits <= 1 ? static_cast<const uint16_t*>(dw) : nullptr;
+  p.ldr = K;
+  p.I = K;
+  p.J = N;
+  p.K = M;
+  p.splits = splits > 1 ? splits : 1;
+  const int64_t nk = M / kBK;
+  p.kper = ((nk + p.splits - 1) / p.splits) * kBK;
+  p.ws = p.splits > 1 ? ws : nullptr;
+  hipError_t e = launch<true, true>(p, s);
+  if (e != hipSuccess || p.splits == 1) return e;
+  const int64_t n = N * K;
+  int64_t blocks = (n / 8 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, static_cast<uint16_t*>(dw),
+                     p.splits, n, accumulate);
+  return hipGetLastError();
 }
 
 }  // extern "C"

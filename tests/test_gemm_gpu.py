@@ -98,3 +98,35 @@ def test_linear_asymmetric_exact():
     dy = torch.randint(-3, 4, (M, N), device="cuda", generator=g).bfloat16()
     dx = m.linear_dgrad(dy, w, None, False)
     assert torch.equal(dx, (dy.float() @ w.float()).bfloat16())
+
+
+# ---- weight gradient: dW[N, K] = dy[M, N]^T x[M, K], split along the M tokens
+WGRAD_SHAPES = [(256, 256, 64, 1), (4096, 1024, 1024, 0), (2048, 3072, 1024, 5), (1024, 200, 520, 3),
+                (8192, 1032, 4096, 0), (64, 64, 64, 1)]
+
+
+@pytest.mark.parametrize("M,N,K,splits", WGRAD_SHAPES)
+def test_linear_wgrad_split_k(M, N, K, splits):
+    m = _ops()
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
+    dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    dw = m.linear_wgrad(dy, x, None, False, splits)
+    ref = dy.float().t() @ x.float()
+    assert dw.shape == (N, K) and dw.dtype == torch.bfloat16
+    assert _rel(dw, ref) < 6e-3, (M, N, K, splits)
+    # accumulate into an existing gradient (a second backward before the optimizer step)
+    base = torch.randn(N, K, device="cuda", generator=g).bfloat16()
+    out = base.clone()
+    m.linear_wgrad(dy, x, out, True, splits)
+    assert _rel(out, ref + base.float()) < 6e-3
+
+
+def test_linear_wgrad_splits_heuristic_fills_the_gpu():
+    m = _ops()
+    # GPT-2 medium at 64 x 1024 tokens: 16 (proj) .. 64 (c_fc) output tiles -> split the tokens
+    for N, K in ((1024, 1024), (3072, 1024), (4096, 1024), (1024, 4096)):
+        tiles = (N // 256) * (K // 256)
+        sp = m.wgrad_splits(65536, N, K)
+        assert sp >= 2 and 192 <= tiles * sp, (N, K, sp)  # >= 3/4 of the 256 CUs busy
+    assert m.wgrad_splits(64, 1024, 1024) == 1  # nothing to split
