@@ -562,12 +562,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if wgrad == "k9":
                 dw = torch.ops.madnn.conv1x1_wgrad(dy, x).to(w.dtype).view(w.shape)
-            elif x.dim() == 4:
-                dw = torch.ops.aten.convolution_backward(dy, x, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0),
-                                                         (1, 1), False, (0, 0), 1, (False, True, False))[1]
-                dw = dw.view(w.shape)
             else:
-                dw = torch.mm(dy.t(), x).view(w.shape)
+                dw = _conv1x1_wgrad_lib(dy, x, w)
         return dx, dw, None, None
 
 
@@ -664,11 +660,8 @@ class _BNReluConv1x1EpiFn(torch.autograd.Function):
         da, part = torch.ops.madnn.conv1x1_dgrad_bnb(dout, w, y, scale, shift)
         if ctx.wgrad == "k9":
             dw = torch.ops.madnn.conv1x1_wgrad(dout, a).to(w.dtype).view(w.shape)
-        elif a.dim() == 4:
-            dw = torch.ops.aten.convolution_backward(dout, a, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0),
-                                                     (1, 1), False, (0, 0), 1, (False, True, False))[1].view(w.shape)
         else:
-            dw = torch.mm(dout.t(), a).view(w.shape)
+            dw = _conv1x1_wgrad_lib(dout, a, w)
         dy, dbw, dbb = torch.ops.madnn.bn_bwd_ext(da, y, bn_w, mean, invstd, scale, shift, part, True)
         need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
@@ -1072,21 +1065,47 @@ def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.T
     (``profiles/r3_wgrad_ab.json``: 1.9x on the attention projection, 1.15x on c_fc, 0.95x on
     c_proj).  ``MADNN_WGRAD=auto`` times both once per (M, N, K) on first use (like cuDNN's
     benchmark mode; never under graph capture) and keeps the faster."""
+    lib = lambda: torch.mm(g2.t(), x2, out=out)  # noqa: E731
     if WGRAD == "lt" or not _wgrad_k12_ok(g2, x2, out):
-        return torch.mm(g2.t(), x2, out=out)
+        return lib()
+    return tuned_wgrad(("linear",) + tuple(g2.shape) + (x2.shape[1],), lib,
+                       lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0))
+
+
+def tuned_wgrad(key, lib, k12):
+    """Run the weight-gradient implementation that was faster for ``key`` (timed once, on first
+    use, outside graph capture): ``lib`` (the library kernel: hipBLASLt / MIOpen) or ``k12`` (K12
+    split-K).  ``MADNN_WGRAD=lt`` / ``k12`` pin one."""
+    if WGRAD == "lt":
+        return lib()
     if WGRAD == "k12":
-        return torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0)
-    key = (g2.shape[0], g2.shape[1], x2.shape[1])
+        return k12()
     choice = _WGRAD_CHOICE.get(key)
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
-            return torch.mm(g2.t(), x2, out=out)
-        t_lt = _time_wgrad(lambda: torch.mm(g2.t(), x2, out=out))
-        t_k12 = _time_wgrad(lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0))
-        choice = _WGRAD_CHOICE[key] = "k12" if t_k12 < t_lt else "lt"
-    if choice == "k12":
-        return torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0)
-    return torch.mm(g2.t(), x2, out=out)
+            return lib()
+        t_lib = _time_wgrad(lib)
+        t_k12 = _time_wgrad(k12)
+        choice = _WGRAD_CHOICE[key] = "k12" if t_k12 < t_lib else "lib"
+    return k12() if choice == "k12" else lib()
+
+
+def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The 1x1 convolution's weight gradient on the library path: MIOpen's wrw for NHWC 4-D
+    tensors, hipBLASLt for 2-D rows -- or K12 split-K over the pixels when that was faster for
+    the shape (:func:`tuned_wgrad`)."""
+    if x.dim() == 4:
+        lib = lambda: torch.ops.aten.convolution_backward(  # noqa: E731
+            dy, x, w.view(w.size(0), -1, 1, 1), None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1,
+            (False, True, False))[1].view(w.shape)
+    else:
+        lib = lambda: torch.mm(dy.t(), x).view(w.shape)  # noqa: E731
+    dr, xr = _rows(dy), _rows(x)
+    probe = torch.empty(0, dtype=w.dtype, device=w.device)
+    if not _wgrad_k12_ok(dr, xr, probe) or w.dtype != torch.bfloat16:
+        return lib()
+    return tuned_wgrad(("conv1x1", dr.shape[0], dr.shape[1], xr.shape[1]), lib,
+                       lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape))
 
 
 LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)
