@@ -48,13 +48,26 @@ def main():
         w = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
         dy = (torch.rand(MM, N, device="cuda") * 2 - 1).bfloat16()
         fl = 2.0 * MM * N * K
+        import ctypes
+
+        tune = ctypes.CDLL(str(ops.kernels_path())).madnn_gemm_tune
+
+        def shape(v, f):
+            def run():
+                tune(0, v)
+                return f()
+            return run
+
         cands = {
             "fwd_lt": lambda: torch.mm(x, w.t()),
-            "fwd_k12": lambda: m.linear_fwd(x, w, None, None, 0, False),
+            "fwd_k12": shape(1, lambda: m.linear_fwd(x, w, None, None, 0, False)),
+            "fwd_k12m32": shape(0, lambda: m.linear_fwd(x, w, None, None, 0, False)),
             "dgrad_lt": lambda: torch.mm(dy, w),
-            "dgrad_k12": lambda: m.linear_dgrad(dy, w, None, False),
+            "dgrad_k12": shape(1, lambda: m.linear_dgrad(dy, w, None, False)),
+            "dgrad_k12m32": shape(0, lambda: m.linear_dgrad(dy, w, None, False)),
         }
         ref = torch.mm(x, w.t())
+        tune(0, 1)
         err = float((m.linear_fwd(x, w, None, None, 0, False)[0].float() - ref.float()).abs().max())
         refd = torch.mm(dy, w)
         errd = float((m.linear_dgrad(dy, w, None, False).float() - refd.float()).abs().max())

@@ -47,7 +47,20 @@ def main():
         out = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
         fl = 2.0 * M * N * K
         auto = int(m.wgrad_splits(M, N, K))
-        cands = {"lt": lambda: torch.mm(dy.t(), x, out=out), "k12_auto": lambda: m.linear_wgrad(dy, x, out, False, 0)}
+        import ctypes
+
+        tune = ctypes.CDLL(str(ops.kernels_path())).madnn_gemm_tune
+
+        def m32(f):
+            def run():
+                tune(0, 0)
+                r = f()
+                tune(0, 1)
+                return r
+            return run
+
+        cands = {"lt": lambda: torch.mm(dy.t(), x, out=out), "k12_auto": lambda: m.linear_wgrad(dy, x, out, False, 0),
+                 "k12_auto_m32": m32(lambda: m.linear_wgrad(dy, x, out, False, 0))}
         for sp in sorted({1, 2, 4, 8, 16} - {auto}):
             cands[f"k12_s{sp}"] = (lambda sp=sp: m.linear_wgrad(dy, x, out, False, sp))
         ref = torch.mm(dy.t(), x)

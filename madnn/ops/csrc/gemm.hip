@@ -119,6 +119,39 @@ __device__ __forceinline__ bf16x8 frag(const uint16_t* tile, int s, int x, int l
   }
 }
 
+// v_mfma_f32_16x16x32_bf16 operands (cdna_hip_programming.md §3): lane l holds
+// A[row l&15][k 8(l>>4) + j] and B[k 8(l>>4) + j][col l&15]; the accumulator holds
+// D[row 4(l>>4) + r][col l&15] in register r.  On random data the chip holds a higher clock on
+// this shape than on 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back 7).
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// k-step s (32 deep) of the operand whose 16 rows/cols start at x: row tiles [128][64] read by
+// ds_read_b128 (row x + l&15, 16-B chunk 4s + l>>4); col tiles [64][128] by two
+// ds_read_b64_tr_b16 (a 16-lane group g reads k rows 32s + 8g .. +7 of columns x .. x+15 and
+// lane i of the group receives column x + i).  Both reads are bank-conflict-free on the
+// swz<64> / swz<128> images (16 distinct 16-B slots per 16 lanes / per half-wave).
+template <bool COL>
+__device__ __forceinline__ bf16x8 frag16(const uint16_t* tile, int s, int x, int lane) {
+  if constexpr (COL) {
+    const int g = lane >> 4, i = lane & 15;
+    const int col = x + 4 * (i & 3);
+    const int row = 32 * s + 8 * g + (i >> 2);
+    const char* base = reinterpret_cast<const char*>(tile);
+    const int sub = 8 * ((col >> 2) & 1);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + swz<128>(row, col >> 3) + sub));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + swz<128>(row + 4, col >> 3) + sub));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  } else {
+    return lds_row(tile, x + (lane & 15), 4 * s + (lane >> 4));
+  }
+}
+
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * (x + k1 * x * x * x);
@@ -128,7 +161,7 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + t);
 }
 
-template <bool A_COL, bool B_COL>
+template <bool A_COL, bool B_COL, bool M16>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[kLds];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
@@ -188,11 +221,21 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     }
   };
 
-  f32x16 acc[4][2];
+  // accumulators: 32x32x16 -> acc[4 i-blocks of 32][2 j-blocks of 32] (f32x16);
+  //               16x16x32 -> ac4[8 i-blocks of 16][4 j-blocks of 16] (f32x4); 128 VGPRs either way
+  f32x16 acc[M16 ? 1 : 4][M16 ? 1 : 2];
+  f32x4 ac4[M16 ? 8 : 1][M16 ? 4 : 1];
+  if constexpr (!M16) {
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+      for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+  } else {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ac4[a][b] = zero4();
+  }
 
   // prologue: half-tiles 0..5 (K tile 0 + the B halves of K tile 1)
 #pragma unroll
@@ -208,6 +251,92 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
 
   bf16x8 af[2][4], bf0[4], bf1[4];
   const int bcol = (wc & 1) * 64;
+  if constexpr (M16) {
+    // same 4-phase schedule, 16 MFMAs per phase: af[a][s] = i-block a (of 4) x k-step s (of 2),
+    // bf0 / bf1 [c][s] = j-blocks 0,1 / 2,3 of the wave's 64 columns
+    for (int t = 0; t < nk; ++t) {
+      const uint16_t* sa = smem + (t & 1) * kStage + wr * kHalf;
+      const uint16_t* sb = smem + (t & 1) * kStage + (2 + (wc >> 1)) * kHalf;
+      const int P = 4 * t;
+      // ---- Q0: A rows 0..63, B cols 0..31
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) bf0[2 * c + s2] = frag16<B_COL>(sb, s2, bcol + 16 * c, lane);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) af[a >> 1][2 * (a & 1) + s2] = frag16<A_COL>(sa, s2, 16 * a, lane);
+      }
+      if (P + 6 < total) stage(P + 6);
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            ac4[a][c] = mfma16(af[a >> 1][2 * (a & 1) + s2], bf0[2 * c + s2], ac4[a][c]);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- Q1: B cols 32..63
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) bf1[2 * c + s2] = frag16<B_COL>(sb, s2, bcol + 32 + 16 * c, lane);
+      if (P + 7 < total) stage(P + 7);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the B half-tiles' last reads
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            ac4[a][2 + c] = mfma16(af[a >> 1][2 * (a & 1) + s2], bf1[2 * c + s2], ac4[a][2 + c]);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- Q2: A rows 64..127 (the stage's last reads: retire them before the barrier)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) af[a >> 1][2 * (a & 1) + s2] = frag16<A_COL>(sa, s2, 64 + 16 * a, lane);
+      if (P + 8 < total) stage(P + 8);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the A half-tiles' last reads
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            ac4[4 + a][2 + c] = mfma16(af[a >> 1][2 * (a & 1) + s2], bf1[2 * c + s2], ac4[4 + a][2 + c]);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+      // ---- Q3: no reads; retire K tile t+1's DMA (the B halves of K tile t+2 stay in flight)
+      if (P + 9 < total) {
+        stage(P + 9);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else if (P + 8 < total) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            ac4[4 + a][c] = mfma16(af[a >> 1][2 * (a & 1) + s2], bf0[2 * c + s2], ac4[4 + a][c]);
+      __builtin_amdgcn_s_setprio(0);
+      barrier();
+    }
+  }
+  if constexpr (!M16) {
   for (int t = 0; t < nk; ++t) {
     const uint16_t* sa = smem + (t & 1) * kStage + wr * kHalf;
     const uint16_t* sb = smem + (t & 1) * kStage + (2 + (wc >> 1)) * kHalf;
@@ -274,64 +403,61 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     __builtin_amdgcn_s_setprio(0);
     barrier();
   }
+  }  // !M16
   if (wr == 0) barrier();  // balance the stagger: every wave has now passed the same barriers
+
+  // every lane owns groups of 4 consecutive i of one j: visit them as (il, jl, v[4])
+  auto for_each_group = [&](auto&& fn) {
+    if constexpr (!M16) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            fn(wr * 128 + a * 32 + 8 * g + 4 * hh, wc * 64 + b * 32 + l32,
+               f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]});
+    } else {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) fn(wr * 128 + a * 16 + 4 * (lane >> 4), wc * 64 + b * 16 + (lane & 15), ac4[a][b]);
+    }
+  };
 
   if (p.ws != nullptr) {
     // split-K partial: fp32 straight from the accumulators, 4 consecutive i (16 B) per lane
     float* slab = p.ws + (int64_t)split * p.J * p.I;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int64_t ig = i0 + wr * 128 + a * 32 + 8 * g + 4 * hh;
-        if (ig >= p.I) continue;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int64_t jg = j0 + wc * 64 + b * 32 + l32;
-          if (jg < p.J) {
-            *reinterpret_cast<f32x4*>(slab + jg * p.I + ig) =
-                f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-          }
-        }
-      }
-    }
+    for_each_group([&](int il, int jl, const f32x4& v) {
+      const int64_t ig = i0 + il, jg = j0 + jl;
+      if (ig < p.I && jg < p.J) *reinterpret_cast<f32x4*>(slab + jg * p.I + ig) = v;
+    });
     return;
   }
 
   // ---- epilogue: (acc + bias) -> bf16 -> LDS [256 j][256 i] -> rows
   char* ot = reinterpret_cast<char*>(smem);
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int il = wr * 128 + a * 32 + 8 * g + 4 * hh;  // first of this lane's 4 i
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias != nullptr) {
-        const int64_t ig = i0 + il;
-        if (ig < p.I) {
-          if (p.bias_f32) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(p.bias) + ig);
-            bv[0] = v[0]; bv[1] = v[1]; bv[2] = v[2]; bv[3] = v[3];
-          } else {
-            const u32x2 v = *reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(p.bias) + ig);
-            bv[0] = bf16_to_f32((unsigned short)(v[0] & 0xffffu));
-            bv[1] = bf16_to_f32((unsigned short)(v[0] >> 16));
-            bv[2] = bf16_to_f32((unsigned short)(v[1] & 0xffffu));
-            bv[3] = bf16_to_f32((unsigned short)(v[1] >> 16));
-          }
+  for_each_group([&](int il, int jl, const f32x4& v) {  // il: first of this lane's 4 i
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr) {
+      const int64_t ig = i0 + il;
+      if (ig < p.I) {
+        if (p.bias_f32) {
+          const f32x4 w = *reinterpret_cast<const f32x4*>(static_cast<const float*>(p.bias) + ig);
+          bv[0] = w[0]; bv[1] = w[1]; bv[2] = w[2]; bv[3] = w[3];
+        } else {
+          const u32x2 w = *reinterpret_cast<const u32x2*>(static_cast<const uint16_t*>(p.bias) + ig);
+          bv[0] = bf16_to_f32((unsigned short)(w[0] & 0xffffu));
+          bv[1] = bf16_to_f32((unsigned short)(w[0] >> 16));
+          bv[2] = bf16_to_f32((unsigned short)(w[1] & 0xffffu));
+          bv[3] = bf16_to_f32((unsigned short)(w[1] >> 16));
         }
       }
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int jl = wc * 64 + b * 32 + l32;
-        const unsigned lo = (unsigned)f32_to_bf16(acc[a][b][4 * g] + bv[0]) |
-                            ((unsigned)f32_to_bf16(acc[a][b][4 * g + 1] + bv[1]) << 16);
-        const unsigned hi = (unsigned)f32_to_bf16(acc[a][b][4 * g + 2] + bv[2]) |
-                            ((unsigned)f32_to_bf16(acc[a][b][4 * g + 3] + bv[3]) << 16);
-        *reinterpret_cast<u32x2*>(ot + jl * 512 + 16 * ((il >> 3) ^ (jl & 31)) + 8 * hh) = u32x2{lo, hi};
-      }
     }
-  }
+    const unsigned lo = (unsigned)f32_to_bf16(v[0] + bv[0]) | ((unsigned)f32_to_bf16(v[1] + bv[1]) << 16);
+    const unsigned hi = (unsigned)f32_to_bf16(v[2] + bv[2]) | ((unsigned)f32_to_bf16(v[3] + bv[3]) << 16);
+    *reinterpret_cast<u32x2*>(ot + jl * 512 + 16 * ((il >> 3) ^ (jl & 31)) + 8 * ((il >> 2) & 1)) = u32x2{lo, hi};
+  });
   __syncthreads();
   const int c = tid & 31;
   const int64_t ig = i0 + 8 * c;
@@ -396,6 +522,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+int g_mfma16 = 1;  // K12 MFMA shape: 1 = 16x16x32 (default), 0 = 32x32x16 (madnn_gemm_tune(0, v))
+
 template <bool A_COL, bool B_COL>
 hipError_t launch(Args& p, hipStream_t s) {
   p.i_tiles = (int)((p.I + kT - 1) / kT);
@@ -404,7 +532,11 @@ hipError_t launch(Args& p, hipStream_t s) {
   if (p.kper <= 0) p.kper = p.K;
   const int64_t grid = (int64_t)p.i_tiles * p.j_tiles * p.splits;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
+  if (g_mfma16) {
+    hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, true>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
+  }
   return hipGetLastError();
 }
 
@@ -414,6 +546,16 @@ hipError_t launch(Args& p, hipStream_t s) {
 using namespace madnn::gemm;
 
 extern "C" {
+
+// Tunables: key 0 = MFMA shape (1: 16x16x32, 0: 32x32x16).  Returns the previous value.
+int madnn_gemm_tune(int key, int value) {
+  if (key == 0) {
+    const int old = g_mfma16;
+    g_mfma16 = value ? 1 : 0;
+    return old;
+  }
+  return -1;
+}
 
 // Shapes K12 takes: reduction % 64 == 0, output features % 8 == 0, 16-B aligned rows, and
 // 32-bit-safe per-lane DMA offsets.
