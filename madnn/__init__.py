@@ -12,10 +12,12 @@ from .config import Config
 from .runtime import init, shutdown, get_rank, get_world_size, device, barrier, seed_all
 from .api import distribute, parallelize, synchronize_model, Trainer
 from . import ops, optim, data, comm, models
+from .ckpt import save, load, consolidate
 
 __version__ = "0.1.0"
 
 __all__ = [
     "Config", "init", "shutdown", "get_rank", "get_world_size", "device", "barrier", "seed_all",
     "distribute", "parallelize", "synchronize_model", "Trainer", "ops", "optim", "data", "comm", "models",
+    "save", "load", "consolidate",
 ]

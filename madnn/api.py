@@ -226,6 +226,7 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
         if fused:
             optimizer.bind(space)
             optimizer.grad_source = engine
+            optimizer.nonfinite = cfg.nonfinite
             engine.optimizer = optimizer
         else:
             if cfg.sync == "grads":

@@ -68,6 +68,7 @@ class Config:
     debug_shapes: bool = False
     check_collectives: bool = False
     sync_comm: bool = False              # run comm on the compute stream (race debugging)
+    nonfinite: str = "ignore"            # NaN/Inf gradients: ignore | skip (the optimizer step) | raise
     timeout_s: float = 600.0
     seed: int = 0
     extra: dict = field(default_factory=dict)
@@ -107,6 +108,8 @@ class Config:
             raise ValueError(f"unknown remainder policy {self.remainder!r}")
         if self.checkpointing not in ("none", "auto", "all"):
             raise ValueError(f"unknown checkpointing policy {self.checkpointing!r}")
+        if self.nonfinite not in ("ignore", "skip", "raise"):
+            raise ValueError(f"unknown nonfinite policy {self.nonfinite!r}")
         if self.bucket_mb < 0:
             raise ValueError("bucket_mb must be >= 0 (0 = auto)")
 

@@ -24,6 +24,10 @@ from .. import ops
 from ..parallel.flat import FlatBucket, FlatParamSpace, _phys_view
 
 
+class NonFiniteGradients(RuntimeError):
+    """Raised by a fused optimizer step with ``nonfinite="raise"`` when a gradient is NaN/Inf."""
+
+
 class _FlatOptimizer(torch.optim.Optimizer):
     _state_names: tuple = ()
 
@@ -36,6 +40,8 @@ class _FlatOptimizer(torch.optim.Optimizer):
         self._dscale: Optional[torch.Tensor] = None
         self._pending_load = None
         self.norm_spec = None              # (groups, skip params) for clipping when no engine provides it
+        self.nonfinite = "ignore"          # ignore | skip | raise (set from Config.nonfinite by distribute)
+        self.skipped_steps = 0
 
     # ----------------------------------------------------------------- binding
     def bind(self, space: FlatParamSpace):
@@ -155,6 +161,23 @@ class _FlatOptimizer(torch.optim.Optimizer):
             else:
                 gs.finalize_grads()
         cached = getattr(self, "_grads_cached", None)
+        if self.nonfinite != "ignore" and not self._grads_finite(late, cached):
+            self.skipped_steps += 1
+            if self.nonfinite == "raise":
+                raise NonFiniteGradients(f"non-finite gradients at optimizer step {self.skipped_steps}")
+            from ..utils.logging import get_logger
+
+            get_logger().warning("madnn: non-finite gradients; optimizer step skipped (%d so far)", self.skipped_steps)
+            if late:
+                gs.finalize_grads()
+            for bk in self.space.buckets:  # nothing of this step's gradients may leak into the next
+                if bk.grad is not None:
+                    bk.grad.zero_()
+            self._grads_cached = None
+            self._dscale = None
+            if self.grad_source is not None:
+                self.grad_source.after_step()
+            return loss
         order = [i for i, bk in enumerate(self.space.buckets) if bk.index not in late] + \
                 [i for i, bk in enumerate(self.space.buckets) if bk.index in late]
         for i in order:
@@ -171,6 +194,25 @@ class _FlatOptimizer(torch.optim.Optimizer):
         if self.grad_source is not None:
             self.grad_source.after_step()
         return loss
+
+    @torch.no_grad()
+    def _grads_finite(self, late, cached) -> bool:
+        """Whether every reduced gradient of the step is finite -- on EVERY rank (one MAX
+        all-reduce of a flag over the world group, so pipeline stages holding different
+        parameters skip or step together).  One host sync per step: only with ``nonfinite`` on."""
+        if late:
+            self.grad_source.finalize_grads()
+        flats = cached if cached is not None else [self._grads(bk) for bk in self.space.buckets]
+        if cached is None:
+            self._grads_cached = flats
+        sq = ops.grad_norm(flats, max_norm=0.0)[0:1].float()
+        bad = (~torch.isfinite(sq)).float()
+        from .. import comm
+        import torch.distributed as dist
+
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            comm.all_reduce(bad, "max")
+        return float(bad.item()) == 0.0
 
     def zero_grad(self, set_to_none: bool = True):
         for group in self.param_groups:
@@ -304,4 +346,4 @@ def FusedAdamW(params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, 
     return FusedAdam(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, adamw=True)
 
 
-__all__ = ["FusedSGD", "FusedAdam", "FusedAdamW"]
+__all__ = ["FusedSGD", "FusedAdam", "FusedAdamW", "NonFiniteGradients"]

@@ -207,14 +207,24 @@ class DataParallel(nn.Module):
                     if p.grad is not None:
                         p.grad.record_stream(self.comm_stream)
                 buf = self.space.pack_grads(bk, scale)
+                self._maybe_corrupt(buf)
                 bk.work = comm.all_reduce(buf, op, group=self.group, async_op=True)
         else:
             buf = self.space.pack_grads(bk, scale)
+            self._maybe_corrupt(buf)
             bk.work = comm.all_reduce(buf, op, group=self.group, async_op=True)
         bk.launched = True
         self.stats["buckets_launched"] += 1
         self.stats["bytes_reduced"] += buf.numel() * buf.element_size()
         self._step_bytes += buf.numel() * buf.element_size()
+
+    def _maybe_corrupt(self, buf):
+        import os
+
+        if os.environ.get("MADNN_FAULT"):
+            from ..utils.fault import maybe_corrupt
+
+            maybe_corrupt(self._steps + 1, buf)  # fault injection: NaN gradients of this step
 
     def _on_backward_end(self):
         self._in_backward = False

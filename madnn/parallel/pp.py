@@ -1063,6 +1063,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
             raise TypeError("pipeline engine needs a madnn fused optimizer (FusedSGD / FusedAdam)")
         optimizer.bind(space)
         optimizer.grad_source = engine
+        optimizer.nonfinite = cfg.nonfinite
         dp_engine.optimizer = optimizer
     get_logger().info("madnn pp: rank %d/%d chunks %s dp=%d microbatches=%d schedule=%s tied=%d", stage, S,
                       ranges, plan.dp, plan.microbatches, schedule, len(tied_local))

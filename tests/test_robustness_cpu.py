@@ -260,3 +260,43 @@ def _w_double_backward(rank, world):
 @pytest.mark.slow
 def test_second_backward_before_step_is_reduced():
     run_dist(_w_double_backward, 2)
+
+
+def _w_corrupt(rank, world, policy):
+    """MADNN_FAULT=1:2:corrupt poisons rank 1's gradients of step 2 with NaN before the reduction;
+    with nonfinite="skip" every rank skips that step together (weights stay finite and identical),
+    with "raise" every rank raises NonFiniteGradients."""
+    import os
+
+    import madnn
+    from madnn.models import MLP
+    from madnn.optim import FusedSGD, NonFiniteGradients
+
+    os.environ["MADNN_FAULT"] = "1:2:corrupt"
+    torch.manual_seed(0)
+    m = MLP(8, 16, 4)
+    opt = FusedSGD(m.parameters(), lr=0.1)
+    eng, opt = madnn.distribute(m, opt, strategy="dp", nonfinite=policy)
+    x, y = torch.randn(4, 8), torch.randint(0, 4, (4,))
+    snaps = []
+    try:
+        for _ in range(3):
+            torch.nn.functional.cross_entropy(eng(x), y).backward()
+            opt.step()
+            snaps.append(torch.cat([p.detach().flatten().clone() for p in m.parameters()]))
+    except NonFiniteGradients:
+        assert policy == "raise" and len(snaps) == 1
+        return
+    assert policy == "skip" and opt.skipped_steps == 1
+    assert all(torch.isfinite(s).all() for s in snaps)
+    assert torch.equal(snaps[0], snaps[1]) and not torch.equal(snaps[1], snaps[2])  # step 2 skipped
+    flat = snaps[-1]
+    allf = [torch.empty_like(flat) for _ in range(world)]
+    torch.distributed.all_gather(allf, flat)
+    torch.testing.assert_close(allf[0], allf[1], rtol=0, atol=0)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("policy", ["skip", "raise"])
+def test_corrupt_gradients_skipped_or_raised_on_every_rank(policy):
+    run_dist(_w_corrupt, 2, policy)

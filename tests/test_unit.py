@@ -639,3 +639,18 @@ def test_periodic_sync_counts_samples():
     for _ in range(2):  # per-sample backward: 49, 50 -> crosses 50
         m(torch.randn(1, 4)).sum().backward()
     assert ps.counter == 50 and calls[-1] == 50 and ps.backwards == 5
+
+
+def test_step_profiler_writes_a_trace(tmp_path):
+    from madnn.models import MLP
+    from madnn.utils.profiling import kernel_table, step_profiler
+
+    m = MLP(8, 16, 4)
+    x = torch.randn(4, 8)
+    with step_profiler(str(tmp_path), wait=0, warmup=1, active=2) as prof:
+        for _ in range(3):
+            m(x).sum().backward()
+            prof.step()
+    trace = (tmp_path / "trace-rank0.json").read_text()
+    assert "addmm" in trace or "linear" in trace
+    assert isinstance(kernel_table(prof), str)
