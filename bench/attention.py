@@ -44,7 +44,11 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--native", default="",
+                    help="FUNC:KEY:ON:OFF -- A/B a native tunable (e.g. madnn_attn_tune:0:1:0): K8 only, both arms")
     a = ap.parse_args()
+    if a.native:
+        return ab_native(a)
     from madnn import ops
 
     assert ops.load_kernels()
@@ -76,6 +80,50 @@ def main():
                "k8_fwd_tflops": round(fl / t_k8f / 1e12, 1), "sdpa_fwd_tflops": round(fl / t_sdf / 1e12, 1),
                "k8_bwd_tflops": round(2.5 * fl / t_k8b / 1e12, 1), "sdpa_bwd_tflops": round(2.5 * fl / t_sdb / 1e12, 1),
                "max_abs_diff_fwd": float((o1.float() - o2.transpose(1, 2).float()).abs().max())}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=2)
+
+
+def ab_native(a):
+    """K8 forward / backward times with a native tunable ON vs OFF, interleaved rounds in one process."""
+    import ctypes
+
+    from madnn import ops
+
+    assert ops.load_kernels()
+    fn, key, von, voff = a.native.split(":")
+    knob = getattr(ctypes.CDLL(str(ops.kernels_path())), fn)
+    dev = torch.device("cuda")
+    rows = []
+    for name, B, S, H, HKV, D, causal in SHAPES:
+        g = torch.Generator(device=dev).manual_seed(0)
+        q = torch.randn(B, S, H, D, device=dev, generator=g).bfloat16().requires_grad_(True)
+        k = torch.randn(B, S, HKV, D, device=dev, generator=g).bfloat16().requires_grad_(True)
+        v = torch.randn(B, S, HKV, D, device=dev, generator=g).bfloat16().requires_grad_(True)
+        fl = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
+        res = {True: {"f": [], "b": []}, False: {"f": [], "b": []}}
+        outs = {}
+        for rnd in range(6):
+            for arm in ((True, False) if rnd % 2 == 0 else (False, True)):
+                knob(int(key), int(von if arm else voff))
+                o = ops.attention(q, k, v, causal=causal)
+                do = torch.randn(o.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(1)).bfloat16()
+                res[arm]["f"].append(timeit(lambda: ops.attention(q, k, v, causal=causal)))
+                res[arm]["b"].append(timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True)))
+                if rnd == 0:
+                    outs[arm] = (o.detach().float(), [t.float() for t in torch.autograd.grad(o, (q, k, v), do)])
+        knob(int(key), int(von))
+        med = {arm: {p: statistics.median(res[arm][p]) for p in "fb"} for arm in (True, False)}
+        row = {"shape": name, "native": a.native,
+               "on_fwd_ms": round(med[True]["f"] * 1e3, 3), "off_fwd_ms": round(med[False]["f"] * 1e3, 3),
+               "on_bwd_ms": round(med[True]["b"] * 1e3, 3), "off_bwd_ms": round(med[False]["b"] * 1e3, 3),
+               "on_fwd_tflops": round(fl / med[True]["f"] / 1e12, 1),
+               "on_bwd_tflops": round(2.5 * fl / med[True]["b"] / 1e12, 1),
+               "max_abs_diff_o": float((outs[True][0] - outs[False][0]).abs().max()),
+               "max_abs_diff_grads": [float((x - y).abs().max()) for x, y in zip(outs[True][1], outs[False][1])]}
         rows.append(row)
         print(json.dumps(row), flush=True)
     if a.json:

@@ -19,7 +19,7 @@ def main():
     v = torch.randn(B, S, HKV, D, device=dev).bfloat16().requires_grad_(True)
     for _ in range(int(os.environ.get("ATTN_ITERS", "3"))):
         o = ops.attention(q, k, v, causal=causal)
-        o.backward(torch.ones_like(o))
+        o.backward(torch.randn_like(o))
     torch.cuda.synchronize()
 
 

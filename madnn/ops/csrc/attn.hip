@@ -159,7 +159,14 @@ __device__ __forceinline__ void store4_bf16(uint16_t* p, float a, float b, float
 }
 
 // ------------------------------------------------------------------ forward
-template <int D, bool CAUSAL>
+// V2 (default; madnn_attn_tune(0, 0) selects V1 for A/B): the causal / sequence-end mask is one
+// compare of a compile-time key offset against a per-lane limit, and the running max is moved
+// only when a row's max grows by more than 2^8 (lazy rescale: the O / l rescale pass -- 32
+// multiplies and an exp per lane -- is skipped on most tiles; p <= 256 is exact in fp32 and
+// relative-exact in the bf16 P operand, and O / l and the LSE do not depend on which m is used).
+constexpr float kRescaleSlack = 8.f;
+
+template <int D, bool CAUSAL, bool V2>
 __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
@@ -212,12 +219,20 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
       }
       const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
       if (edge) {
+        // V2: key k0 + kb*32 + acc_row(r, hh) is valid iff its compile-time offset
+        // kb*32 + (r&3) + 8*(r>>2) <= lim (one compare + select per element)
+        const int lim = (CAUSAL ? min(a.S - 1, qrow) : a.S - 1) - k0 - 4 * hh;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kb * 32 + acc_row(r, hh);
-            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+            bool ok;
+            if constexpr (V2) {
+              ok = kb * 32 + (r & 3) + 8 * (r >> 2) <= lim;
+            } else {
+              const int key = k0 + kb * 32 + acc_row(r, hh);
+              ok = key < a.S && (!CAUSAL || key <= qrow);
+            }
             sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
           }
         }
@@ -230,19 +245,11 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mnew = fmaxf(m, mx * a.scale_log2);
-      float rs = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -mnew));
-          sc[kb][r] = p;
-          rs += p;
-        }
-      }
-      // rescale O only when some row's max moved (exact: alpha == 1 otherwise)
-      if (__any(mnew > m)) {
+      const float mtile = mx * a.scale_log2;
+      // rescale O only when some row's max moved (V2: by more than the slack); alpha == 1 exactly
+      // on the rows whose max did not move
+      if (__any(mtile > m + (V2 ? kRescaleSlack : 0.f))) {
+        const float mnew = fmaxf(m, mtile);
         const float alpha = ex2(m - mnew);
         l *= alpha;
 #pragma unroll
@@ -250,9 +257,19 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
 #pragma unroll
           for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
         }
+        m = mnew;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -m));
+          sc[kb][r] = p;
+          rs += p;
+        }
       }
       l += rs;
-      m = mnew;
       // O^T[d][q] += sum_key V[key][d] P^T[key][q]
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -588,10 +605,18 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   }
 }
 
+int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default), 0 = V1
+// (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
+// their loops are not VALU-issue-bound)
+
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
-  hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+  if (g_attn_v2) {
+    hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, true>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, false>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -607,6 +632,7 @@ hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+
 }  // namespace attn
 }  // namespace madnn
 
@@ -615,6 +641,14 @@ using namespace madnn::attn;
 extern "C" {
 
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
+
+// A/B knob: key 0 = kernel version (1 = V2, 0 = V1); returns the previous value
+int madnn_attn_tune(int key, int value) {
+  if (key != 0) return -1;
+  const int old = g_attn_v2;
+  g_attn_v2 = value ? 1 : 0;
+  return old;
+}
 
 hipError_t madnn_attn_fwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t st) {
   if (a->S <= 0 || a->B <= 0) return hipSuccess;

@@ -113,7 +113,10 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(xhat*w*dy))     (LayerNorm)
 // dx = rstd * (w*dy - xhat * mean(xhat*w*dy))                  (RMSNorm)
 // partial[blk][0:H] = sum_rows dy*xhat, partial[blk][H:2H] = sum_rows dy
-template <int XDT, int WDT, int TPR, int NC>
+// EARLY: the weight is loaded once per lane (its columns never change across the grid-stride
+// rows) and the residual gradient is loaded together with x and dy, so its latency hides under
+// the row reduction instead of following it (A/B: madnn_norm_tune key 2).
+template <int XDT, int WDT, int TPR, int NC, bool EARLY>
 __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const void* __restrict__ dres,
@@ -128,13 +131,26 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+  float wk[EARLY ? NC : 1][8];
+  if constexpr (EARLY) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (col < H) {
+        load8<WDT>(w, col, wk[c]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wk[c][j] = 0.f;
+      }
+    }
+  }
 
   for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += (int64_t)gridDim.x * RPB) {
     const int64_t row = row0 + sub;
     const bool live = row < rows;
     const float mean = (live && !rms) ? mean_in[row] : 0.f;
     const float rstd = live ? rstd_in[row] : 0.f;
-    float xh[NC][8], wdy[NC][8];
+    float xh[NC][8], wdy[NC][8], rv[EARLY ? NC : 1][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -143,7 +159,13 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
         float xv[8], gv[8], wv[8];
         load8<XDT>(x, row * H + col, xv);
         load8<XDT>(dy, row * H + col, gv);
-        load8<WDT>(w, col, wv);
+        if constexpr (EARLY) {
+          if (dres) load8<XDT>(dres, row * H + col, rv[c]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wv[j] = wk[c][j];
+        } else {
+          load8<WDT>(w, col, wv);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[c][j] = (xv[j] - mean) * rstd;
@@ -169,10 +191,15 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (wdy[c][j] - c2 - xh[c][j] * c1);
         if (dres) {
-          float r[8];
-          load8<XDT>(dres, row * H + col, r);
+          if constexpr (EARLY) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+            for (int j = 0; j < 8; ++j) o[j] += rv[c][j];
+          } else {
+            float r[8];
+            load8<XDT>(dres, row * H + col, r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += r[j];
+          }
         }
         store8<XDT>(dx, row * H + col, o);
       }
@@ -284,15 +311,15 @@ static NormCfg pick_cfg(int H) {
 // backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
 // (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
 // +0.5 % over 16 (4: -0.1 %)
-static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4;
+static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1;
 
 extern "C" {
 
 int madnn_norm_tune(int key, int value) {
-  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : nullptr;
+  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value > 0) *f = value;
+  if (value > 0 || key == 2) *f = value;
   return old;
 }
 
@@ -339,8 +366,13 @@ hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const fl
     MADNN_NORM_CFG(H, TPR, NC, {
       constexpr int RPB = kNormThreads / TPR;
       const size_t lds = RPB > 1 ? (size_t)RPB * 2 * NC * TPR * 8 * sizeof(float) : 0;
-      hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC>), dim3(G), dim3(kNormThreads), lds, stream, dy, x, w,
-                         mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      if (g_norm_bwd_early) {
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true>), dim3(G), dim3(kNormThreads), lds, stream, dy, x,
+                           w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      } else {
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, false>), dim3(G), dim3(kNormThreads), lds, stream, dy,
+                           x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      }
       MADNN_HIP_CHECK(hipGetLastError());
       const int fgrid = ((has_bias ? 2 * H : H) + 31) / 32;
       hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(32 * kWgSlices), 0, stream, workspace, G, H,
