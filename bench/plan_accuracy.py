@@ -6,6 +6,7 @@ same model, batch and optimizer run through ``madnn.distribute``.
 """
 import argparse
 import json
+import statistics
 import os
 import sys
 import time
@@ -58,17 +59,20 @@ def run_case(model_name: str, batch: int, steps: int = 6, warmup: int = 3) -> di
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    per = []
     for _ in range(steps):
+        t0 = time.perf_counter()
         step()
-    torch.cuda.synchronize()
-    meas = (time.perf_counter() - t0) / steps
+        torch.cuda.synchronize()
+        per.append(time.perf_counter() - t0)
+    meas = statistics.median(per)  # one-off host stalls (allocator, first-use tuning) do not count
     eng.remove_hooks()
     del eng, opt, model
     torch.cuda.empty_cache()
     out = {"model": model_name, "batch": batch, "est_ms": plan.est_step_s * 1e3, "measured_ms": meas * 1e3,
            "ratio": plan.est_step_s / meas, "plan_s": round(plan_s, 1), "calibration": plan.calibration,
-           "measured_costs": plan.measured}
+           "measured_costs": plan.measured,
+           "step_ms": [round(t * 1e3, 2) for t in per]}
     print(json.dumps(out), flush=True)
     return out
 

@@ -1135,6 +1135,56 @@ def _lt_linear(x2, weight, bias, residual, gelu):
         return None
 
 
+GELU_FWD = os.environ.get("MADNN_GELU_FWD", "auto")  # GELU Linear forward: auto (timed per shape) | lt | k12
+_GELU_FWD_CHOICE: dict = {}
+
+
+def _k12_fwd_ok(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> bool:
+    return (_is_dev(x2) and x2.dtype == weight.dtype == torch.bfloat16 and x2.is_contiguous()
+            and weight.is_contiguous() and x2.shape[1] % 64 == 0 and weight.shape[0] % 8 == 0
+            and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
+            and (bias is None or (bias.is_contiguous() and bias.dtype in (torch.float32, torch.bfloat16)))
+            and load_kernels())
+
+
+def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
+    """``(gelu_tanh(pre), pre)`` with ``pre = x W^T + b``, from whichever of two implementations was
+    faster for the shape (timed once on first use, like :func:`tuned_wgrad`):
+
+    * ``lt``: hipBLASLt GEMM (bias epilogue), then the K11 streaming GELU pass (hipBLASLt has no
+      GELU+AUX algorithm at GPT-2's 65536-row shapes on gfx950);
+    * ``k12``: one K12 GEMM whose epilogue adds the bias, stores the pre-activation (the backward's
+      AUX) and the GELU output from the same LDS-staged rows -- no separate HBM pass.
+
+    ``MADNN_GELU_FWD=lt`` / ``k12`` pin one."""
+    x2 = x.reshape(-1, x.shape[-1])
+    out_shape = (*x.shape[:-1], weight.shape[0])
+
+    def lt():
+        pre = F.linear(x2, weight, bias if bias is None or bias.dtype == x2.dtype else bias.to(x2.dtype))
+        return gelu_tanh(pre), pre
+
+    def k12():
+        return torch.ops.madnn.linear_fwd(x2, weight, bias, None, 1, True)
+
+    choice = GELU_FWD
+    if choice not in ("lt", "k12"):
+        choice = "lt"
+        if _k12_fwd_ok(x2, weight, bias):
+            key = (tuple(x2.shape), tuple(weight.shape), bias is not None)
+            choice = _GELU_FWD_CHOICE.get(key)
+            if choice is None:
+                if torch.cuda.is_current_stream_capturing():
+                    choice = "lt"
+                else:
+                    t_lt, t_k12 = _time_wgrad(lt), _time_wgrad(k12)
+                    choice = _GELU_FWD_CHOICE[key] = "k12" if t_k12 < t_lt else "lt"
+    elif choice == "k12" and not _k12_fwd_ok(x2, weight, bias):
+        choice = "lt"
+    y, pre = k12() if choice == "k12" else lt()
+    return y.view(out_shape), pre.view(out_shape)
+
+
 class _LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) (+ residual) with act in {identity, tanh-GELU}.
 
@@ -1167,6 +1217,10 @@ class _LinearFn(torch.autograd.Function):
             else:
                 ctx.save_for_backward(x, weight)
             return y
+        if gelu:
+            y, pre = _gelu_linear_fwd(x, weight, bias)
+            ctx.save_for_backward(x, weight, pre)
+            return y + residual if residual is not None else y
         pre = F.linear(x, weight, bias)
         if gelu:
             ctx.save_for_backward(x, weight, pre)

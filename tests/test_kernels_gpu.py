@@ -397,6 +397,34 @@ def _rel(a, b):
     return float((a.detach().float() - b.detach().float()).norm() / b.detach().float().norm().clamp_min(1e-12))
 
 
+@pytest.mark.parametrize("choice", ["k12", "lt", "auto"])
+@pytest.mark.parametrize("bias_dt", [torch.bfloat16, torch.float32, None])
+def test_gelu_linear_forward_choices_match_fp32(cuda, monkeypatch, choice, bias_dt):
+    """The GELU Linear forward through K12's fused bias + AUX + GELU epilogue, through hipBLASLt +
+    the K11 GELU pass, and through the per-shape timed choice: output, saved pre-activation and
+    all three gradients vs autograd of the fp32 composition."""
+    monkeypatch.setattr(madnn.ops, "GELU_FWD", choice)
+    monkeypatch.setitem(madnn.ops._LT_KIND, "gelu", False)  # hipBLASLt's GELU epilogue out of the way
+    torch.manual_seed(11)
+    M, K, N = 768, 320, 1032  # partial i / j tiles, K a multiple of 64
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * K ** -0.5).requires_grad_()
+    b = (torch.randn(N, device=cuda, dtype=bias_dt) * 0.1).requires_grad_() if bias_dt else None
+    y = madnn.ops.linear(x, w, b, gelu=True)
+    xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
+    bf = b.detach().float().requires_grad_() if b is not None else None
+    yf = torch.nn.functional.gelu(torch.nn.functional.linear(xf, wf, bf), approximate="tanh")
+    assert y.dtype == torch.bfloat16 and _rel(y, yf) < 1e-2
+    g = torch.randn_like(yf)
+    y.backward(g.bfloat16())
+    yf.backward(g)
+    assert _rel(x.grad, xf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2
+    if b is not None:
+        assert b.grad.dtype == bias_dt and _rel(b.grad, bf.grad) < 2e-2
+    if choice == "auto":
+        assert set(madnn.ops._GELU_FWD_CHOICE.values()) <= {"k12", "lt"}
+
+
 @pytest.mark.parametrize("rms", [False, True])
 def test_norm_fork_gradient_joins_backward(cuda, rms):
     """fork=True: (N(x), x) where the alias's gradient is added inside the K3 backward pass."""
