@@ -765,9 +765,7 @@ _POOL_BN = os.environ.get("MADNN_POOL_BN", "1") != "0"
 # ---------------------------------------------------------------------- K13
 _K13 = os.environ.get("MADNN_CONV3X3", "1") != "0"
 _K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A/B runs)
-# weight grad: "auto" = K13 on the wide layers (W >= 48: 686 vs 910 us at ResNet-50's 56x56 layer,
-# batch 1536), MIOpen on the narrower ones where it is as fast or faster
-# (profiles/r2_k13_conv3x3_vs_miopen.json); "k13" | "miopen" force one (A/B runs)
+# weight grad: "auto" = K13 or MIOpen per shape, timed once (_conv3x3_wgrad); "k13" | "miopen" force one
 _K13_WGRAD = os.environ.get("MADNN_CONV3X3_WGRAD", "auto")
 
 
@@ -799,6 +797,27 @@ def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
 
+def _conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The 3x3 / stride-1 weight gradient on K13 (split over the pixels, fp32 slabs + one reduce) or
+    MIOpen, whichever was faster for the shape (timed once, :func:`tuned_wgrad`).  At batch 2048 K13
+    wins on the 56 / 28 / 14 maps and MIOpen on the 7x7 one (profiles/r3_resnet_wgrad_shapes_b2048.json);
+    ``MADNN_CONV3X3_WGRAD=k13`` / ``miopen`` pin one."""
+    k13 = lambda: torch.ops.madnn.conv3x3_wgrad(dy, x, w.dtype == torch.bfloat16)  # noqa: E731
+    lib = lambda: torch.ops.aten.convolution_backward(  # noqa: E731
+        dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1, (False, True, False))[1]
+    if _K13_WGRAD == "k13":
+        dw = k13()
+    elif _K13_WGRAD == "miopen" or (_K13_WGRAD == "wide" and x.size(3) < 48):  # "wide": the round-2 rule
+        dw = lib()
+    elif _K13_WGRAD == "wide":
+        dw = k13()
+    else:
+        dw = tuned_wgrad(("conv3x3",) + tuple(x.shape) + (w.size(0),), lib, k13)
+    if dw.stride() != w.stride() or dw.dtype != w.dtype:
+        dw = torch.empty_like(w).copy_(dw)
+    return dw
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     """3x3 / stride 1 / pad 1 convolution (K13): MFMA implicit GEMM forward over an LDS-staged input
     halo with the BatchNorm statistics in its epilogue; the data gradient is the same kernel on the
@@ -825,13 +844,7 @@ class _Conv3x3Fn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
                                                          (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            if _K13_WGRAD == "k13" or (_K13_WGRAD == "auto" and x.size(3) >= 48):
-                dw = torch.ops.madnn.conv3x3_wgrad(dy, x, w.dtype == torch.bfloat16)
-            else:
-                dw = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
-                                                         (False, True, False))[1]
-            if dw.stride() != w.stride() or dw.dtype != w.dtype:
-                dw = torch.empty_like(w).copy_(dw)
+            dw = _conv3x3_wgrad(dy, x, w)
         return dx, dw, None
 
 
@@ -857,13 +870,7 @@ class _BNReluConv3x3Fn(torch.autograd.Function):
         dout = _nhwc(dout.to(y.dtype))
         wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
         da, part = torch.ops.madnn.conv3x3_fwd_bnb(dout, wt, y, scale, shift)
-        if _K13_WGRAD == "k13" or (_K13_WGRAD == "auto" and a.size(3) >= 48):
-            dw = torch.ops.madnn.conv3x3_wgrad(dout, a, w.dtype == torch.bfloat16)
-        else:
-            dw = torch.ops.aten.convolution_backward(dout, a, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
-                                                     (False, True, False))[1]
-        if dw.stride() != w.stride() or dw.dtype != w.dtype:
-            dw = torch.empty_like(w).copy_(dw)
+        dw = _conv3x3_wgrad(dout, a, w)
         dy, dbw, dbb = torch.ops.madnn.bn_bwd_ext(da, y, bn_w, mean, invstd, scale, shift, part, True)
         need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None

@@ -624,7 +624,7 @@ int madnn_wgrad_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t nk = M / kBK;
   int best = 1;
   double best_t = 1e30;
-  for (int sp = 1; sp <= 32; ++sp) {
+  for (int sp = 1; sp <= 256; ++sp) {  // ResNet's 1x1 convs: 4-16 tiles over 10^5-10^6 pixels
     if (nk / sp < 8) break;
     const int64_t kper_steps = (nk + sp - 1) / sp;
     const int64_t rounds = (tiles * sp + 255) / 256;
