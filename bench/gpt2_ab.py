@@ -6,6 +6,7 @@ Variants toggle at run time (the model is built once):
   lt_res  : residual add in c_proj's hipBLASLt epilogue (on) vs a separate ATen add (off)
   gelu    : K11-family GELU forward kernel (on) vs ATen's F.gelu (off)
   wgrad   : weight gradients on the per-shape faster of hipBLASLt / K12 split-K (on) vs hipBLASLt (off)
+  colsum  : attn-proj / c_proj bias grads from the next norm's backward column sums (on) vs their own pass (off)
   gelu_fwd: c_fc forward on K12 with the fused bias + AUX + GELU epilogue (on) vs hipBLASLt + K11 GELU (off)
 Prints a JSON line with the per-window ms/step and the median of each arm.
 """
@@ -28,7 +29,7 @@ def main():
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--switch", default="lt_res",
-                    choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp", "native", "wgrad", "gelu_fwd"])
+                    choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp", "native", "wgrad", "gelu_fwd", "colsum"])
     ap.add_argument("--native", default="", help="FUNC:KEY:ON:OFF -- a native tunable, e.g. madnn_norm_tune:1:4:2")
     a = ap.parse_args()
     import madnn
@@ -44,7 +45,9 @@ def main():
     ids = torch.randint(0, 50257, (a.batch, a.seq), device="cuda")
 
     def set_arm(on):
-        if a.switch == "gelu_fwd":
+        if a.switch == "colsum":
+            ops.NORM_COLSUM = on
+        elif a.switch == "gelu_fwd":
             ops.GELU_FWD = "k12" if on else "lt"
         elif a.switch == "wgrad":  # per-shape timed hipBLASLt / K12 split-K (on) vs hipBLASLt only (off)
             ops.WGRAD = "auto" if on else "lt"

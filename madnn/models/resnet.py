@@ -34,6 +34,9 @@ from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_epi_
 _FORK_DS = os.environ.get("MADNN_FORK_DOWNSAMPLE", "1") != "0"
 # A/B knob: the downsample path's BatchNorm runs inside bn3's kernels (1) or as its own passes (0)
 _DUAL_BN = os.environ.get("MADNN_DUAL_BN", "1") != "0"
+# A/B knob: the stride-2 1x1 downsample convolution as a stride-1 1x1 on conv1's compact subsample
+# of the block input (1) or as a stride-2 library convolution on the full input (0)
+_DS_SUB = os.environ.get("MADNN_DS_SUB", "1") != "0"
 
 
 def conv3x3(cin, cout, stride=1, groups=1, dilation=1):
@@ -84,11 +87,17 @@ class Bottleneck(nn.Module):
             y, st, idt = self.conv1(x, stats=True, fork=True)
         elif _FORK_DS:
             # the downsample path's input gradient is likewise summed inside conv1's data grad
-            y, st, xf = self.conv1(x, stats=True, fork=True)
-            if self._dual_bn():
+            dual = self._dual_bn()
+            sub = dual and _DS_SUB and isinstance(x, torch.Tensor) and self.downsample[0].subsampled_ok()
+            y, st, xf = self.conv1(x, stats=True, fork=2 if sub else True)
+            if dual:
                 # relu(bn3(conv3) + bn_ds(conv_ds)): the downsample BN is applied inside bn3's
-                # passes (forward and backward), its normalised output never written to HBM
-                yd, std = self.downsample[0](xf, stats=True)
+                # passes (forward and backward), its normalised output never written to HBM.
+                # sub: conv1 hands over the compact x[:, :, ::2, ::2] and the stride-2 downsample
+                # runs as a stride-1 1x1 on it (K9, BN statistics from its epilogue); its compact
+                # input gradient is added into conv1's data grad at the even pixels
+                yd, std = (self.downsample[0].forward_subsampled(xf, stats=True) if sub
+                           else self.downsample[0](xf, stats=True))
                 y, st = self._bn1_conv2(y, st)
                 y, st = self._bn2_conv3(y, st)
                 return batch_norm_add_bn_relu(y, yd, self.bn3, self.downsample[1], st, std)

@@ -56,8 +56,21 @@ class FusedConv2d(nn.Conv2d):
         if stats:
             out.append(None)
         if fork:
-            out.append(x)
+            out.append(x[:, :, ::2, ::2] if fork == 2 else x)
         return out[0] if len(out) == 1 else tuple(out)
+
+    def subsampled_ok(self) -> bool:
+        """A 1x1 / stride-2 / unpadded convolution: equal to a stride-1 1x1 on ``x[:, :, ::2, ::2]``."""
+        return (self.kernel_size == (1, 1) and self.stride == (2, 2) and self.padding in ((0, 0), "valid")
+                and self.dilation == (1, 1) and self.groups == 1 and self.bias is None)
+
+    def forward_subsampled(self, xs: torch.Tensor, stats: bool = False):
+        """This stride-2 1x1 convolution given the subsampled input ``xs = x[:, :, ::2, ::2]`` (e.g. from
+        ``conv1x1(..., fork=2)``): a stride-1 1x1 on K9 / the library (with the statistics when on K9)."""
+        if _K9 and ops.conv1x1_supported(xs, self.weight):
+            return ops.conv1x1(xs, self.weight, stats=stats)
+        y = torch.nn.functional.conv2d(xs, self.weight)
+        return (y, None) if stats else y
 
     def extra_repr(self):
         k = {(1, 1): ", kernel=madnn.K9", (7, 7): ", kernel=madnn.K10",

@@ -174,6 +174,10 @@ class _NormFn(torch.autograd.Function):
         y, s, mean, rstd = _need_native("norm_fwd").norm_fwd(xc, rc, w, b, float(eps), bool(rms))
         saved_x = s if res is not None else xc
         ctx.save_for_backward(saved_x, w, mean, rstd)
+        # the input came straight from a biased madnn Linear (the transformer residual stream): the
+        # backward also returns dx's column sums for that Linear's bias gradient (_LinearFn reads
+        # them off the gradient tensor instead of running its own column-sum pass)
+        ctx.colsum = NORM_COLSUM and _from_biased_linear(x)
         ctx.rms = rms
         ctx.has_bias = b is not None
         ctx.has_res = res is not None
@@ -189,9 +193,20 @@ class _NormFn(torch.autograd.Function):
     def backward(ctx, dy, ds):
         x, w, mean, rstd = ctx.saved_tensors
         dres = ds.contiguous() if ((ctx.has_res or ctx.fork) and ds is not None) else None
-        dx, dw, db = torch.ops.madnn.norm_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.rms, ctx.has_bias)
+        dx, dw, db, cs = torch.ops.madnn.norm_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.rms, ctx.has_bias,
+                                                  ctx.colsum)
         dx = dx.view(ctx.shape)
+        if ctx.colsum:
+            dx._madnn_colsum = cs
         return dx, (dx if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None, None
+
+
+NORM_COLSUM = os.environ.get("MADNN_NORM_COLSUM", "1") != "0"  # A/B switch (see _NormFn.forward)
+
+
+def _from_biased_linear(x: torch.Tensor) -> bool:
+    gf = x.grad_fn
+    return gf is not None and type(gf).__name__ == "_LinearFnBackward" and getattr(gf, "bias_dtype", None) is not None
 
 
 def _norm(x, weight, bias, eps, rms, residual, fork=False):
@@ -520,7 +535,11 @@ _K9_DGRAD = os.environ.get("MADNN_K9_DGRAD", "narrow")  # "wide" | "narrow" (A/B
 class _Conv1x1Fn(torch.autograd.Function):
     """Stride-1 1x1 convolution on NHWC bf16 (see :func:`conv1x1_route`).  With ``fork`` the
     input is also returned (as the block's identity path); its gradient is then accumulated
-    inside the data-grad kernel instead of by a separate autograd add."""
+    inside the data-grad kernel instead of by a separate autograd add.  ``fork == 2`` returns the
+    stride-2 subsample ``x[:, :, ::2, ::2]`` instead (compact NHWC: the input of a ResNet
+    downsample convolution, which then runs as a stride-1 1x1 on a quarter of the pixels); its
+    compact gradient is added into the even pixels of this convolution's data grad -- no
+    zero-filled full-resolution gradient and no stride-2 data-grad kernel."""
 
     @staticmethod
     def forward(ctx, x, w, stats, fork):
@@ -532,7 +551,10 @@ class _Conv1x1Fn(torch.autograd.Function):
             part = x.new_empty((0, 2, w.size(0)), dtype=torch.float32)
         ctx.save_for_backward(x, w)
         ctx.route = (dgrad, wgrad)
+        ctx.fork = fork
         ctx.mark_non_differentiable(part)
+        if fork == 2:
+            return y, part, x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
         if fork:
             return y, part, x.view_as(x)
         return y, part
@@ -542,6 +564,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dgrad, wgrad = ctx.route
         dy = _nhwc(dy.to(x.dtype))
+        sub = None
+        if ctx.fork == 2:
+            sub, dfork = dfork, None
         res = _nhwc(dfork.to(x.dtype)) if dfork is not None else None
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -559,6 +584,10 @@ class _Conv1x1Fn(torch.autograd.Function):
                     torch.mm(_rows(dy), w2, out=_rows(dx))
         elif res is not None:
             dx = res
+        if sub is not None:
+            if dx is None:
+                dx = torch.zeros_like(x)
+            dx[:, :, ::2, ::2].add_(sub.to(dx.dtype))
         if ctx.needs_input_grad[1]:
             if wgrad == "k9":
                 dw = torch.ops.madnn.conv1x1_wgrad(dy, x).to(w.dtype).view(w.shape)
@@ -587,7 +616,8 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
     :func:`conv1x1_route`).  ``stats``: also return the per-workgroup channel sums / sums of
     squares of y for :func:`batch_norm_act` (None when the forward did not run on K9).
     ``fork``: also return an alias of ``x`` to use as the residual path, whose gradient is then
-    added inside this convolution's data-grad kernel."""
+    added inside this convolution's data-grad kernel; ``fork=2``: return the compact stride-2
+    subsample of ``x`` instead (see :class:`_Conv1x1Fn`)."""
     _need_native("conv1x1")
     outs = _Conv1x1Fn.apply(x, w, stats, fork)
     y, part = outs[0], outs[1]
@@ -1249,7 +1279,11 @@ class _LinearFn(torch.autograd.Function):
             if ctx.bias_dtype is None:
                 db = None
         elif ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
-            db, _ = bias_grad(g, None, ctx.bias_dtype)
+            cs = getattr(g, "_madnn_colsum", None)  # from the consuming norm's backward (_NormFn)
+            if cs is not None and cs.numel() == g.shape[-1]:
+                db = cs.to(ctx.bias_dtype)
+            else:
+                db, _ = bias_grad(g, None, ctx.bias_dtype)
         g2 = g.reshape(-1, g.shape[-1])
         dx = dw = None
         if ctx.needs_input_grad[0]:

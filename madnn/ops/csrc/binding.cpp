@@ -30,7 +30,7 @@ hipError_t madnn_norm_fwd(const void*, const void*, const void*, const void*, vo
                           int, float, int, int, int, hipStream_t);
 int64_t madnn_norm_bwd_workspace(int64_t, int);
 hipError_t madnn_norm_bwd(const void*, const void*, const void*, const float*, const float*, const void*, void*, void*,
-                          void*, float*, int64_t, int, int, int, int, hipStream_t);
+                          void*, float*, float*, int64_t, int, int, int, int, hipStream_t);
 int madnn_bn_supported(int);
 int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
@@ -288,10 +288,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Te
   return {y, sum, mean, rstd};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x,
-                                                        const at::Tensor& w, const at::Tensor& mean,
-                                                        const at::Tensor& rstd, const c10::optional<at::Tensor>& dres,
-                                                        bool rms, bool has_bias) {
+// colsum: also the fp32 column sums of dx over the rows (the producing Linear's bias gradient)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x,
+                                                                    const at::Tensor& w, const at::Tensor& mean,
+                                                                    const at::Tensor& rstd,
+                                                                    const c10::optional<at::Tensor>& dres, bool rms,
+                                                                    bool has_bias, bool colsum) {
   check_dev(x, "x");
   const int64_t H = w.numel();
   const int64_t rows = x.numel() / H;
@@ -306,12 +308,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, co
   if (dres.has_value() && dres->defined()) {
     dr = dres->scalar_type() == x.scalar_type() ? dres->contiguous() : dres->to(x.scalar_type()).contiguous();
   }
+  at::Tensor cs = colsum ? at::empty({H}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
   check(madnn_norm_bwd(dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                        rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr(),
-                       has_bias ? db.data_ptr() : nullptr, ws.data_ptr<float>(), rows, (int)H, rms ? 1 : 0,
-                       dt_code(x), dt_code(w), cur_stream(x)),
+                       has_bias ? db.data_ptr() : nullptr, colsum ? cs.data_ptr<float>() : nullptr,
+                       ws.data_ptr<float>(), rows, (int)H, rms ? 1 : 0, dt_code(x), dt_code(w), cur_stream(x)),
         "norm_bwd");
-  return {dx, dw, db};
+  return {dx, dw, db, cs};
 }
 
 // ---- K5 fused BatchNorm(+add)(+ReLU), NHWC -------------------------------
@@ -1216,8 +1219,8 @@ TORCH_LIBRARY(madnn, m) {
   m.def("grad_norm(Tensor[] flats, float max_norm, float scale) -> Tensor");
   m.def("norm_fwd(Tensor x, Tensor? res, Tensor w, Tensor? b, float eps, bool rms) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
-      "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dres, bool rms, bool has_bias) -> "
-      "(Tensor, Tensor, Tensor)");
+      "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dres, bool rms, bool has_bias, "
+      "bool colsum=False) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(madnn, CUDA, m) {

@@ -113,24 +113,34 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(xhat*w*dy))     (LayerNorm)
 // dx = rstd * (w*dy - xhat * mean(xhat*w*dy))                  (RMSNorm)
 // partial[blk][0:H] = sum_rows dy*xhat, partial[blk][H:2H] = sum_rows dy
+// CS: also partial[blk][2H:3H] = sum_rows dx (the written input gradient, residual included): the
+// bias gradient of the Linear that produced this norm's input (the transformer residual stream),
+// so that Linear's backward needs no column-sum pass of its own (ops._LinearFn, `_madnn_colsum`).
 // EARLY: the weight is loaded once per lane (its columns never change across the grid-stride
 // rows) and the residual gradient is loaded together with x and dy, so its latency hides under
 // the row reduction instead of following it (A/B: madnn_norm_tune key 2).
-template <int XDT, int WDT, int TPR, int NC, bool EARLY>
+template <int XDT, int WDT, int TPR, int NC, bool EARLY, bool CS>
 __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const void* __restrict__ dres,
     void* __restrict__ dx, float* __restrict__ partial, int64_t rows, int H, int rms, int has_bias) {
+  constexpr int NS = CS ? 3 : 2;  // column sums per workgroup partial row
   __shared__ __attribute__((aligned(16))) float red[kNormThreads / kWave];
-  extern __shared__ __attribute__((aligned(16))) float slab[];  // [RPB][2][NC*TPR*8] when RPB > 1
+  extern __shared__ __attribute__((aligned(16))) float slab[];  // [RPB][NS][NC*TPR*8] when RPB > 1
   constexpr int RPB = kNormThreads / TPR;
   const int sub = threadIdx.x / TPR;
   const int t = threadIdx.x % TPR;
-  float dg[NC][8], db[NC][8];
+  float dg[NC][8], db[NC][8], ds[CS ? NC : 1][8];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+  if constexpr (CS) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ds[c][j] = 0.f;
+  }
   float wk[EARLY ? NC : 1][8];
   if constexpr (EARLY) {
 #pragma unroll
@@ -202,6 +212,11 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
           }
         }
         store8<XDT>(dx, row * H + col, o);
+        if constexpr (CS) {
+          // the sum of what is written (rounded to XDT, as the Linear's own column-sum pass would read it)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ds[c][j] += XDT == kBF16 ? bf16_to_f32(f32_to_bf16(o[j])) : o[j];
+        }
       }
     }
   }
@@ -214,29 +229,33 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int lc = c * TPR * 8 + t * 8 + j;
-        slab[(sub * 2 + 0) * W + lc] = dg[c][j];
-        slab[(sub * 2 + 1) * W + lc] = db[c][j];
+        slab[(sub * NS + 0) * W + lc] = dg[c][j];
+        slab[(sub * NS + 1) * W + lc] = db[c][j];
+        if constexpr (CS) slab[(sub * NS + 2) * W + lc] = ds[c][j];
       }
     __syncthreads();
     // each thread finalises a strided set of columns
     for (int lc = threadIdx.x; lc < W; lc += kNormThreads) {
       if (lc >= H) continue;
-      float a = 0.f, bb = 0.f;
+      float a = 0.f, bb = 0.f, cc = 0.f;
 #pragma unroll
       for (int r = 0; r < RPB; ++r) {
-        a += slab[(r * 2 + 0) * W + lc];
-        bb += slab[(r * 2 + 1) * W + lc];
+        a += slab[(r * NS + 0) * W + lc];
+        bb += slab[(r * NS + 1) * W + lc];
+        if constexpr (CS) cc += slab[(r * NS + 2) * W + lc];
       }
-      partial[(int64_t)blockIdx.x * 2 * H + lc] = a;
-      if (has_bias) partial[(int64_t)blockIdx.x * 2 * H + H + lc] = bb;
+      partial[(int64_t)blockIdx.x * NS * H + lc] = a;
+      if (has_bias) partial[(int64_t)blockIdx.x * NS * H + H + lc] = bb;
+      if constexpr (CS) partial[(int64_t)blockIdx.x * NS * H + 2 * H + lc] = cc;
     }
   } else {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (col < H) {
-        store8<kF32>(partial, (int64_t)blockIdx.x * 2 * H + col, dg[c]);
-        if (has_bias) store8<kF32>(partial, (int64_t)blockIdx.x * 2 * H + H + col, db[c]);
+        store8<kF32>(partial, (int64_t)blockIdx.x * NS * H + col, dg[c]);
+        if (has_bias) store8<kF32>(partial, (int64_t)blockIdx.x * NS * H + H + col, db[c]);
+        if constexpr (CS) store8<kF32>(partial, (int64_t)blockIdx.x * NS * H + 2 * H + col, ds[c]);
       }
     }
   }
@@ -250,30 +269,36 @@ constexpr int kWgSlices = 32;
 template <int WDT>
 __global__ __launch_bounds__(1024) void norm_wgrad_finalize_kernel(const float* __restrict__ partial, int G, int H,
                                                                    int has_bias, void* __restrict__ dw,
-                                                                   void* __restrict__ dbias) {
+                                                                   void* __restrict__ dbias, int ns,
+                                                                   float* __restrict__ dsum) {
   __shared__ float red[kWgSlices][33];
   const int lc = threadIdx.x & 31;
   const int ls = threadIdx.x >> 5;
-  const int col2 = blockIdx.x * 32 + lc;  // column in [0, 2H)
+  const int col2 = blockIdx.x * 32 + lc;  // column in [0, ns*H)
+  const int64_t pitch = (int64_t)ns * H;
   float acc = 0.f;
-  if (col2 < 2 * H) {
+  if (col2 < ns * H) {
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     int g = ls;
     for (; g + 3 * kWgSlices < G; g += 4 * kWgSlices) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += partial[(int64_t)(g + u * kWgSlices) * 2 * H + col2];
+      for (int u = 0; u < 4; ++u) a[u] += partial[(int64_t)(g + u * kWgSlices) * pitch + col2];
     }
-    for (; g < G; g += kWgSlices) a[0] += partial[(int64_t)g * 2 * H + col2];
+    for (; g < G; g += kWgSlices) a[0] += partial[(int64_t)g * pitch + col2];
     acc = (a[0] + a[1]) + (a[2] + a[3]);
   }
   red[ls][lc] = acc;
   __syncthreads();
-  if (ls == 0 && col2 < 2 * H) {
+  if (ls == 0 && col2 < ns * H) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < kWgSlices; ++k) s += red[k][lc];
     if (col2 < H) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dw), col2, s);
-    else if (has_bias) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dbias), col2 - H, s);
+    else if (col2 < 2 * H) {
+      if (has_bias) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dbias), col2 - H, s);
+    } else {
+      dsum[col2 - 2 * H] = s;
+    }
   }
 }
 
@@ -343,40 +368,46 @@ hipError_t madnn_norm_fwd(const void* x, const void* res, const void* w, const v
   return hipGetLastError();
 }
 
-// Workspace size (floats) the backward needs for its dgamma/dbeta partials.
-int64_t madnn_norm_bwd_workspace(int64_t rows, int H) {
+// Workspace size (floats) the backward needs for its dgamma/dbeta (/ dx column-sum) partials.
+static int64_t norm_bwd_groups(int64_t rows, int H) {
   using namespace madnn;
   NormCfg c = pick_cfg(H);
   const int RPB = kNormThreads / c.tpr;
   int64_t blocks = (rows + RPB - 1) / RPB;
   int64_t G = blocks < (int64_t)g_norm_bwd_wg * kNumCU ? blocks : (int64_t)g_norm_bwd_wg * kNumCU;
-  if (G < 1) G = 1;
-  return G * 2 * (int64_t)H;
+  return G < 1 ? 1 : G;
 }
 
+int64_t madnn_norm_bwd_workspace(int64_t rows, int H) { return norm_bwd_groups(rows, H) * 3 * (int64_t)H; }
+
+// dsum (optional, fp32 [H]): column sums of dx over the rows (see norm_bwd_kernel CS)
 hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const float* mean_in, const float* rstd_in,
-                          const void* dres, void* dx, void* dw, void* dbias, float* workspace, int64_t rows, int H,
-                          int rms, int xdt, int wdt, hipStream_t stream) {
+                          const void* dres, void* dx, void* dw, void* dbias, float* dsum, float* workspace,
+                          int64_t rows, int H, int rms, int xdt, int wdt, hipStream_t stream) {
   using namespace madnn;
   if (rows <= 0) return hipSuccess;
   if (H % 8 != 0 || H > 16384) return hipErrorInvalidValue;
   const int has_bias = dbias != nullptr;
-  const int G = (int)(madnn_norm_bwd_workspace(rows, H) / (2 * (int64_t)H));
+  const int G = (int)norm_bwd_groups(rows, H);
+  const int ns = dsum != nullptr ? 3 : 2;
   MADNN_DISPATCH_XW(xdt, wdt, XDT, WDT, {
     MADNN_NORM_CFG(H, TPR, NC, {
       constexpr int RPB = kNormThreads / TPR;
-      const size_t lds = RPB > 1 ? (size_t)RPB * 2 * NC * TPR * 8 * sizeof(float) : 0;
-      if (g_norm_bwd_early) {
-        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true>), dim3(G), dim3(kNormThreads), lds, stream, dy, x,
-                           w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      const size_t lds = RPB > 1 ? (size_t)RPB * ns * NC * TPR * 8 * sizeof(float) : 0;
+      if (dsum != nullptr) {
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true, true>), dim3(G), dim3(kNormThreads), lds, stream,
+                           dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+      } else if (g_norm_bwd_early) {
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true, false>), dim3(G), dim3(kNormThreads), lds, stream,
+                           dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
       } else {
-        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, false>), dim3(G), dim3(kNormThreads), lds, stream, dy,
-                           x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, false, false>), dim3(G), dim3(kNormThreads), lds,
+                           stream, dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
       }
       MADNN_HIP_CHECK(hipGetLastError());
-      const int fgrid = ((has_bias ? 2 * H : H) + 31) / 32;
+      const int fgrid = ((dsum != nullptr ? 3 * H : (has_bias ? 2 * H : H)) + 31) / 32;
       hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(32 * kWgSlices), 0, stream, workspace, G, H,
-                         has_bias, dw, dbias);
+                         has_bias, dw, dbias, ns, dsum);
     });
   });
   return hipGetLastError();

@@ -140,6 +140,53 @@ def test_bf16_bottleneck_k9_matches_miopen_and_fp32(cuda, monkeypatch):
         assert ((a - b).norm() / b.norm()).item() < 0.1  # bf16 activations vs fp32: ~7 % on dx
 
 
+@pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8)])
+def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw):
+    """A stride-2 downsample Bottleneck: the downsample 1x1 run as a stride-1 K9 conv on conv1's
+    compact x[:, :, ::2, ::2] (gradient added into conv1's data grad at the even pixels) vs the
+    stride-2 library convolution on the full input (same bf16 block: tight), and vs fp32 eager."""
+    import madnn.models.resnet as R
+    from torch import nn
+
+    from madnn.nn.conv import FusedConv2d
+    from madnn.nn.norm import FusedBatchNorm2d
+
+    torch.manual_seed(5)
+    ds = nn.Sequential(FusedConv2d(inplanes, planes * 4, 1, stride=2, bias=False), FusedBatchNorm2d(planes * 4))
+    blk = R.Bottleneck(inplanes, planes, stride=2, downsample=ds)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    ref = R.Bottleneck(inplanes, planes, stride=2,
+                       downsample=nn.Sequential(nn.Conv2d(inplanes, planes * 4, 1, stride=2, bias=False),
+                                                nn.BatchNorm2d(planes * 4)))
+    ref.load_state_dict(blk.state_dict())
+    blk = blk.to(cuda).to(memory_format=torch.channels_last)
+    for p in blk.parameters():
+        if p.dim() == 4:
+            p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
+    x0 = _rand((4, inplanes, hw, hw), cuda)
+    g = torch.randn(4, planes * 4, hw // 2, hw // 2, device=cuda)
+    res = []
+    for sub in (True, False):
+        monkeypatch.setattr(R, "_DS_SUB", sub)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        y.float().backward(g)
+        res.append((y.float(), x.grad.float(), blk.conv1.weight.grad.float(), ds[0].weight.grad.float(),
+                    ds[1].weight.grad.float()))
+    for a, b in zip(*res):
+        assert ((a - b).norm() / b.norm()).item() < 2e-2
+    xr = x0.float().cpu().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g.cpu())
+    for a, b in zip(res[0], (yr, xr.grad, ref.conv1.weight.grad, ref.downsample[0].weight.grad,
+                             ref.downsample[1].weight.grad)):
+        a = a.cpu().reshape(b.shape)
+        assert ((a - b).norm() / b.norm()).item() < 0.1
+
+
 @pytest.mark.parametrize("cin,cout", [(256, 64), (1024, 256), (128, 512), (2048, 512)])
 def test_conv1x1_fork_accumulates_residual_grad(cuda, cin, cout):
     """fork=True: the identity path's gradient is summed inside the data-grad pass (K9 epilogue or

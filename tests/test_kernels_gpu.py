@@ -654,3 +654,53 @@ def test_batchnorm_many_producer_partial_rows(cuda):
     torch.testing.assert_close(rm1, rm2, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(rv1, rv2, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(y1.float(), y2.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("mode", ["plain", "fork", "residual"])
+def test_norm_colsum_feeds_linear_bias_grad(cuda, monkeypatch, mode):
+    """A biased Linear feeding a K3 norm: the norm backward's dx column sums become the Linear's bias
+    gradient (no separate column-sum pass) -- equal to the fp32 reference in every norm mode."""
+    calls = []
+    real = madnn.ops.bias_grad
+    monkeypatch.setattr(madnn.ops, "bias_grad", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(12)
+    x = torch.randn(4, 96, 256, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(512, 256, device=cuda, dtype=torch.bfloat16) * 0.06).requires_grad_()
+    b = (torch.randn(512, device=cuda, dtype=torch.bfloat16) * 0.1).requires_grad_()
+    lw = (torch.rand(512, device=cuda) + 0.5).requires_grad_()
+    lb = (torch.randn(512, device=cuda) * 0.1).requires_grad_()
+    r = torch.randn(4, 96, 512, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    g1, g2 = torch.randn(4, 96, 512, device=cuda), torch.randn(4, 96, 512, device=cuda)
+
+    def run(xx, ww, bb, rr, lin, norm):
+        h = lin(xx, ww, bb)
+        if mode == "plain":
+            return (norm(h, None).float() * g1).sum()
+        if mode == "fork":
+            y, ha = norm(h, "fork")
+            return (y.float() * g1).sum() + (ha.float() * g2).sum()
+        y, s = norm(h, rr)
+        return (y.float() * g1).sum() + (s.float() * g2).sum()
+
+    def mnorm(h, arg):
+        if arg == "fork":
+            return madnn.ops.layer_norm(h, lw, lb, fork=True)
+        if arg is None:
+            return madnn.ops.layer_norm(h, lw, lb)
+        return madnn.ops.layer_norm(h, lw, lb, residual=arg)
+
+    run(x, w, b, r, lambda a, ww, bb: madnn.ops.linear(a, ww, bb), mnorm).backward()
+    assert not calls, "the Linear ran its own bias column-sum pass"
+    xf, wf, bf, rf = (t.detach().float().requires_grad_() for t in (x, w, b, r))
+    lwf, lbf = lw.detach().clone().requires_grad_(), lb.detach().clone().requires_grad_()
+
+    def fnorm(h, arg):
+        if arg == "fork":
+            return torch.nn.functional.layer_norm(h, (512,), lwf, lbf), h
+        if arg is None:
+            return torch.nn.functional.layer_norm(h, (512,), lwf, lbf)
+        s = h + arg
+        return torch.nn.functional.layer_norm(s, (512,), lwf, lbf), s
+
+    run(xf, wf, bf, rf, torch.nn.functional.linear, fnorm).backward()
+    assert _rel(b.grad, bf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2 and _rel(x.grad, xf.grad) < 2e-2
