@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_conv_gpu.py tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py tests/test_kernels_gpu.py tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/gpu_tests_q.log 2>&1 || { tail -n 40 gpurun_out/gpu_tests_q.log; exit 3; }
 tail -n 1 gpurun_out/gpu_tests_q.log
 timeout -k 10 400 python -u bench/gpt2_ab.py --batch 64 --switch colsum --windows 6 --steps 6 \

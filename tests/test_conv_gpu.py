@@ -177,7 +177,8 @@ def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes,
         res.append((y.float(), x.grad.float(), blk.conv1.weight.grad.float(), ds[0].weight.grad.float(),
                     ds[1].weight.grad.float()))
     for a, b in zip(*res):
-        assert ((a - b).norm() / b.norm()).item() < 2e-2
+        # the compact path rounds the even pixels' input gradient once more (bf16 add after the data grad)
+        assert ((a - b).norm() / b.norm()).item() < 3e-2
     xr = x0.float().cpu().requires_grad_(True)
     yr = ref(xr)
     yr.backward(g.cpu())
