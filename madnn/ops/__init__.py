@@ -455,6 +455,10 @@ class _AttnPackedFn(torch.autograd.Function):
         o, lse = torch.ops.madnn.attn_fwd(q, k, v, bool(causal), float(scale))
         ctx.save_for_backward(qkv, o, lse)
         ctx.meta = (heads, kv_heads, bool(causal), float(scale))
+        # qkv is (a view of) a biased madnn Linear's output: the backward kernels also sum dQKV's
+        # columns, which that Linear takes as its bias gradient (no column-sum pass of its own)
+        ctx.colsum = ATTN_COLSUM and (_from_biased_linear(qkv) or
+                                      (qkv._base is not None and _from_biased_linear(qkv._base)))
         return o
 
     @staticmethod
@@ -464,8 +468,16 @@ class _AttnPackedFn(torch.autograd.Function):
         q, k, v = qkv.split([heads, kv_heads, kv_heads], dim=2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.split([heads, kv_heads, kv_heads], dim=2)
-        torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale)
+        cs = None
+        if ctx.colsum:
+            cs = torch.empty((heads + 2 * kv_heads) * qkv.size(-1), dtype=torch.float32, device=qkv.device)
+        torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, cs)
+        if cs is not None:
+            dqkv._madnn_colsum = cs
         return dqkv, None, None, None, None
+
+
+ATTN_COLSUM = os.environ.get("MADNN_ATTN_COLSUM", "1") != "0"  # A/B switch (see _AttnPackedFn.forward)
 
 
 def attention_supported(t: torch.Tensor, head_dim: int, dropout: float = 0.0) -> bool:
@@ -1279,7 +1291,10 @@ class _LinearFn(torch.autograd.Function):
             if ctx.bias_dtype is None:
                 db = None
         elif ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
-            cs = getattr(g, "_madnn_colsum", None)  # from the consuming norm's backward (_NormFn)
+            # from the consumer's backward (_NormFn, _AttnPackedFn); a reshaped view keeps it on its base
+            cs = getattr(g, "_madnn_colsum", None)
+            if cs is None and g._base is not None and g.numel() == g._base.numel():
+                cs = getattr(g._base, "_madnn_colsum", None)
             if cs is not None and cs.numel() == g.shape[-1]:
                 db = cs.to(ctx.bias_dtype)
             else:

@@ -29,6 +29,10 @@ struct MadnnAttnArgs {
   int B, S, H, Hkv;
   float scale;       // softmax scale (1/sqrt(D) by default)
   float scale_log2;  // scale * log2(e)
+  // backward, optional: per-workgroup column sums of the written dq / dk / dv (the packed QKV
+  // projection's bias gradient before the final reduce): [B * ceil(S / 128)][(H + 2 Hkv) * D] fp32,
+  // dq in columns [0, H D), dk in [H D, (H + Hkv) D), dv in [(H + Hkv) D, (H + 2 Hkv) D)
+  float* cpart;
 };
 
 }

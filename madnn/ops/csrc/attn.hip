@@ -439,6 +439,28 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       }
     }
   }
+  if (a.cpart != nullptr) {
+    // column sums of the stored (bf16-rounded) dq over this workgroup's 128 query rows: lane
+    // (l32, hh) holds column 32 d + 8 g + 4 hh + i of row qrow; sum the 32 rows of a half-wave by
+    // shuffles, then the 4 waves through LDS
+    __shared__ float red[4][D];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = qrow < a.S ? bf16_to_f32(f32_to_bf16(dq[d][r] * a.scale)) : 0.f;
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (l32 == 0) red[wave][d * 32 + 8 * (r >> 2) + 4 * hh + (r & 3)] = v;
+      }
+    }
+    __syncthreads();
+    if (tid < D) {
+      const float s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      const int64_t C = (int64_t)(a.H + 2 * a.Hkv) * D;
+      a.cpart[((int64_t)b * nqb + qblk) * C + (int64_t)h * D + tid] = s;
+    }
+  }
 }
 
 // --------------------------------------------------------------- backward: dK, dV
@@ -592,16 +614,60 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   // lane holds dK/dV[key = k0w + acc_row(r, hh)][d = 32*db + l32]
   uint16_t* kp = a.dk + b * a.dk_sb + hk * a.dk_sh;
   uint16_t* vp = a.dv + b * a.dv_sb + hk * a.dv_sh;
+  float ck[DB], cv[DB];  // this lane's column sums over its 16 keys (cpart)
+#pragma unroll
+  for (int d = 0; d < DB; ++d) ck[d] = cv[d] = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int key = k0w + acc_row(r, hh);
     if (key < a.S) {
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        kp[(int64_t)key * a.dk_ss + d * 32 + l32] = f32_to_bf16(dk[d][r] * a.scale);
-        vp[(int64_t)key * a.dv_ss + d * 32 + l32] = f32_to_bf16(dv[d][r]);
+        const unsigned short kb16 = f32_to_bf16(dk[d][r] * a.scale), vb16 = f32_to_bf16(dv[d][r]);
+        kp[(int64_t)key * a.dk_ss + d * 32 + l32] = kb16;
+        vp[(int64_t)key * a.dv_ss + d * 32 + l32] = vb16;
+        ck[d] += bf16_to_f32(kb16);
+        cv[d] += bf16_to_f32(vb16);
       }
     }
+  }
+  if (a.cpart != nullptr) {
+    // + the partner half-wave (same columns, the other keys), then the 4 waves through LDS
+    __shared__ float red[4][2 * D];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      ck[d] += __shfl_xor(ck[d], 32);
+      cv[d] += __shfl_xor(cv[d], 32);
+      if (hh == 0) {
+        red[wave][d * 32 + l32] = ck[d];
+        red[wave][D + d * 32 + l32] = cv[d];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * D) {
+      const float s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      const int64_t C = (int64_t)(a.H + 2 * a.Hkv) * D;
+      const int64_t col = (int64_t)a.H * D + (tid < D ? (int64_t)hk * D + tid : (int64_t)(a.Hkv + hk) * D + tid - D);
+      a.cpart[((int64_t)b * nkb + kblk) * C + col] = s;
+    }
+  }
+}
+
+// colsum[c] = sum_r cpart[r][c]: the dQKV column sums over all B * S rows
+__global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float* __restrict__ cpart, int R, int C,
+                                                                    float* __restrict__ out) {
+  __shared__ float red[32][33];
+  const int c = threadIdx.x % 32, sl = threadIdx.x / 32;
+  const int n = blockIdx.x * 32 + c;
+  float acc = 0.f;
+  if (n < C)
+    for (int r = sl; r < R; r += 32) acc += cpart[(int64_t)r * C + n];
+  red[sl][c] = acc;
+  __syncthreads();
+  if (sl == 0 && n < C) {
+    float tot = 0.f;
+    for (int q = 0; q < 32; ++q) tot += red[q][c];
+    out[n] = tot;
   }
 }
 
@@ -655,6 +721,16 @@ hipError_t madnn_attn_fwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t
   if (D == 64) return causal ? launch_fwd<64, true>(*a, st) : launch_fwd<64, false>(*a, st);
   if (D == 128) return causal ? launch_fwd<128, true>(*a, st) : launch_fwd<128, false>(*a, st);
   return hipErrorInvalidValue;
+}
+
+// rows of MadnnAttnArgs::cpart: one per (batch, 128-row sequence block)
+int64_t madnn_attn_colsum_rows(int B, int S) { return (int64_t)B * ((S + kRowsWG - 1) / kRowsWG); }
+
+hipError_t madnn_attn_colsum_finalize(const float* cpart, int64_t R, int64_t C, float* out, hipStream_t st) {
+  if (R <= 0 || C <= 0) return hipSuccess;
+  hipLaunchKernelGGL(attn_colsum_finalize_kernel, dim3((unsigned)((C + 31) / 32)), dim3(1024), 0, st, cpart, (int)R,
+                     (int)C, out);
+  return hipGetLastError();
 }
 
 hipError_t madnn_attn_bwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t st) {

@@ -43,6 +43,8 @@ hipError_t madnn_gelu_fwd(const void*, void*, int64_t, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
+int64_t madnn_attn_colsum_rows(int, int);
+hipError_t madnn_attn_colsum_finalize(const float*, int64_t, int64_t, float*, hipStream_t);
 int madnn_maxpool_supported(int64_t, int, int);
 hipError_t madnn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int madnn_pool_bn_supported(int64_t, int);
@@ -1125,7 +1127,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
 // Writes dq/dk/dv into the given (possibly strided, e.g. one packed dQKV buffer) outputs.
 void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
               const at::Tensor& o, const at::Tensor& lse, const at::Tensor& dq, const at::Tensor& dk,
-              const at::Tensor& dv, bool causal, double scale) {
+              const at::Tensor& dv, bool causal, double scale, const c10::optional<at::Tensor>& colsum) {
   MadnnAttnArgs a = attn_args(q, k, v, scale);
   const int64_t D = q.size(3);
   TORCH_CHECK(o.is_contiguous() && o.sizes() == q.sizes(), "attn_bwd: o must be contiguous [B, S, H, D]");
@@ -1149,7 +1151,20 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   a.dq_sb = dq.stride(0); a.dq_ss = dq.stride(1); a.dq_sh = dq.stride(2);
   a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dk_sh = dk.stride(2);
   a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1); a.dv_sh = dv.stride(2);
+  // colsum (optional, fp32 [(H + 2 Hkv) D]): the column sums of dq | dk | dv over all B * S rows
+  const bool cs = colsum.has_value() && colsum->defined();
+  at::Tensor cpart;
+  int64_t R = 0, C = 0;
+  if (cs) {
+    C = (q.size(2) + 2 * k.size(2)) * D;
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->is_contiguous() && colsum->numel() == C,
+                "attn_bwd: colsum must be a contiguous fp32 [(H + 2 Hkv) * D]");
+    R = madnn_attn_colsum_rows(a.B, a.S);
+    cpart = at::empty({R, C}, q.options().dtype(at::kFloat));
+    a.cpart = cpart.data_ptr<float>();
+  }
   check(madnn_attn_bwd(&a, (int)D, causal ? 1 : 0, cur_stream(q)), "attn_bwd");
+  if (cs) check(madnn_attn_colsum_finalize(a.cpart, R, C, colsum->data_ptr<float>(), cur_stream(q)), "attn_colsum");
 }
 
 }  // namespace
@@ -1177,7 +1192,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> (Tensor, Tensor)");
   m.def(
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
-      "Tensor(c!) dv, bool causal, float scale) -> ()");
+      "Tensor(c!) dv, bool causal, float scale, Tensor(d!)? colsum=None) -> ()");
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
   m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");

@@ -101,3 +101,29 @@ def test_selfattention_module_uses_k8_and_matches_sdpa(cuda):
             ops.attention_supported = orig
         assert _rel(y, y2) < 1e-2
         assert _rel(gx, x.grad) < 3e-2
+
+
+@pytest.mark.parametrize("H,HKV,D,S", [(4, 4, 64, 256), (8, 2, 128, 200)])
+def test_qkv_bias_grad_from_attention_colsum(cuda, monkeypatch, H, HKV, D, S):
+    """A biased QKV projection feeding K8 packed attention: the backward kernels' dQKV column sums
+    become the projection's bias gradient (no column-sum pass) -- equal to the fp32 reference."""
+    import madnn
+
+    calls = []
+    real = madnn.ops.bias_grad
+    monkeypatch.setattr(madnn.ops, "bias_grad", lambda *a, **k: calls.append(1) or real(*a, **k))
+    torch.manual_seed(9)
+    B, E = 2, 256
+    x = torch.randn(B, S, E, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn((H + 2 * HKV) * D, E, device=cuda) * E ** -0.5).bfloat16().requires_grad_()
+    b = (torch.randn((H + 2 * HKV) * D, device=cuda) * 0.1).bfloat16().requires_grad_()
+    g = torch.randn(B, S, H, D, device=cuda)
+    qkv = madnn.ops.linear(x, w, b).view(B, S, H + 2 * HKV, D)
+    o = madnn.ops.attention_qkvpacked(qkv, H, HKV, causal=True)
+    (o.float() * g).sum().backward()
+    assert not calls, "the QKV projection ran its own bias column-sum pass"
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    qf = torch.nn.functional.linear(xf, wf, bf).view(B, S, H + 2 * HKV, D)
+    q, k, v = qf.split([H, HKV, HKV], dim=2)
+    (_ref(q, k, v, True, D ** -0.5) * g).sum().backward()
+    assert _rel(b.grad, bf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2 and _rel(x.grad, xf.grad) < 2e-2
