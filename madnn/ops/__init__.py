@@ -204,8 +204,15 @@ class _NormFn(torch.autograd.Function):
 NORM_COLSUM = os.environ.get("MADNN_NORM_COLSUM", "1") != "0"  # A/B switch (see _NormFn.forward)
 
 
+_VIEW_NODES = ("ViewBackward0", "ReshapeAliasBackward0", "UnsafeViewBackward0")
+
+
 def _from_biased_linear(x: torch.Tensor) -> bool:
+    """``x`` is a biased madnn Linear's output, or one reshape of it (autograd passes the gradient
+    back through the view, whose base then carries the consumer's column sums)."""
     gf = x.grad_fn
+    if gf is not None and type(gf).__name__ in _VIEW_NODES and len(gf.next_functions) == 1:
+        gf = gf.next_functions[0][0]
     return gf is not None and type(gf).__name__ == "_LinearFnBackward" and getattr(gf, "bias_dtype", None) is not None
 
 
@@ -457,8 +464,7 @@ class _AttnPackedFn(torch.autograd.Function):
         ctx.meta = (heads, kv_heads, bool(causal), float(scale))
         # qkv is (a view of) a biased madnn Linear's output: the backward kernels also sum dQKV's
         # columns, which that Linear takes as its bias gradient (no column-sum pass of its own)
-        ctx.colsum = ATTN_COLSUM and (_from_biased_linear(qkv) or
-                                      (qkv._base is not None and _from_biased_linear(qkv._base)))
+        ctx.colsum = ATTN_COLSUM and _from_biased_linear(qkv)
         return o
 
     @staticmethod
