@@ -27,7 +27,7 @@ from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
 from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_epi_supported, bn_relu_conv1x1_supported,
-                   bn_relu_conv3x3,
+                   bn_relu_conv3x3, conv1x1_route,
                    bn_relu_conv3x3_supported, bn_relu_maxpool, bn_relu_maxpool_supported)
 
 # A/B knob: sum the downsample path's input gradient inside conv1's data grad (1) or by autograd (0)
@@ -85,6 +85,11 @@ class Bottleneck(nn.Module):
             # K9: BN statistics from the GEMM epilogue; the identity path's gradient is added
             # inside conv1's data-grad kernel (no separate residual-gradient add)
             y, st, idt = self.conv1(x, stats=True, fork=True)
+            if isinstance(idt, torch.Tensor) and isinstance(self.bn3, BN) and self.conv1._k9(x) \
+                    and conv1x1_route(x.size(1), self.conv1.weight.size(0))[1] == "k9":
+                # idt's only consumer is bn3 and its gradient is summed inside K9's data grad: that
+                # kernel applies bn3's ReLU mask itself (ops._BNFn deferred mask)
+                idt._madnn_defer_mask = True
         elif _FORK_DS:
             # the downsample path's input gradient is likewise summed inside conv1's data grad
             dual = self._dual_bn()

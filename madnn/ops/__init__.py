@@ -252,16 +252,41 @@ class _BNFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_w = weight is not None
+        # the residual is a ResNet block's identity whose only consumer is this BN and whose gradient
+        # is summed inside a K9 data grad (Bottleneck marks it): hand that kernel dy and the ReLU bit
+        # mask instead of writing the masked copy of dy (one activation-sized write less)
+        ctx.defer = (DEFER_RES_MASK and relu and residual is not None and mask.numel() > 0
+                     and getattr(residual, "_madnn_defer_mask", False))
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        defer = ctx.defer and dy.dtype == x.dtype and dy.stride() == x.stride()
         dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
-                                                  mean, invstd, scale, shift, ctx.relu, need_w)
+                                                  mean, invstd, scale, shift, ctx.relu, need_w, not defer)
+        if defer:
+            dres = dy.view_as(dy)
+            dres._madnn_resmask = mask
         return (dx, dw if need_w else None, db if need_w else None, dres if ctx.has_res else None,
                 None, None, None, None, None, None, None, None)
+
+
+DEFER_RES_MASK = os.environ.get("MADNN_DEFER_RES_MASK", "1") != "0"  # A/B switch (see _BNFn.forward)
+
+
+def _apply_bit_mask(t: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """``t`` (NHWC / row-major) with the elements whose bit in ``mask`` (8 per byte, memory order) is
+    clear set to zero -- the unfused fallback of a deferred ReLU-masked residual gradient."""
+    flat = _nhwc(t).permute(0, 2, 3, 1).reshape(-1) if t.dim() == 4 else t.reshape(-1)
+    shifts = torch.arange(8, device=mask.device, dtype=torch.uint8)
+    keep = mask.reshape(-1, 1).bitwise_right_shift(shifts).bitwise_and(1).reshape(-1)
+    out = (flat * keep.to(flat.dtype)).view(flat.shape)
+    if t.dim() == 4:
+        n, c, h, w = t.shape
+        return out.view(n, h, w, c).permute(0, 3, 1, 2)
+    return out.view(t.shape)
 
 
 def bn_supported(x: torch.Tensor, weight: Optional[torch.Tensor]) -> bool:
@@ -585,11 +610,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         sub = None
         if ctx.fork == 2:
             sub, dfork = dfork, None
+        # a deferred ReLU mask (_BNFn): the identity gradient is dfork where its bit is set
+        resmask = getattr(dfork, "_madnn_resmask", None) if dfork is not None else None
         res = _nhwc(dfork.to(x.dtype)) if dfork is not None else None
+        if resmask is not None and not (ctx.needs_input_grad[0] and dgrad == "k9"):
+            res, resmask = _apply_bit_mask(res, resmask), None
         dx = dw = None
         if ctx.needs_input_grad[0]:
             if dgrad == "k9":
-                dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res)
+                dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res, resmask)
             else:
                 w2 = w.reshape(w.size(0), -1)
                 if res is not None:

@@ -75,7 +75,7 @@ int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, const float*,
                              const float*, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, const void*,
-                               const float*, const float*, float*, hipStream_t);
+                               const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
@@ -388,7 +388,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tenso
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
     const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& mask, bool has_res,
     const c10::optional<at::Tensor>& w, const at::Tensor& save_mean, const at::Tensor& save_invstd,
-    const at::Tensor& scale, const at::Tensor& shift, bool relu, bool need_wgrad) {
+    const at::Tensor& scale, const at::Tensor& shift, bool relu, bool need_wgrad, bool write_dres) {
   check_dev(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = bn_rows(x, C);
@@ -399,7 +399,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(
     dyc.copy_(dy);
   }
   at::Tensor dx = at::empty_like(x);
-  at::Tensor dres = has_res ? at::empty_like(x) : at::Tensor();
+  // !write_dres (ReLU + residual only): the residual's gradient (dy masked by the ReLU) is left to
+  // the consumer, which reads dy and the bit mask itself (conv1x1_dgrad resmask)
+  TORCH_CHECK(write_dres || (relu && has_res), "bn_bwd: write_dres=False needs ReLU + residual");
+  at::Tensor dres = has_res && write_dres ? at::empty_like(x) : at::Tensor();
   const uint8_t* mk = nullptr;
   if (relu && has_res) {
     TORCH_CHECK(mask.has_value() && mask->numel() == x.numel() / 8, "bn_bwd: ReLU bit mask required");
@@ -604,8 +607,10 @@ std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Te
   return {y, part};
 }
 
-// dx = dy (*) w^T, plus `res` (a gradient of x's layout accumulated from another path) if given
-at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res) {
+// dx = dy (*) w^T, plus `res` (a gradient of x's layout accumulated from another path) if given;
+// resmask: a ReLU bit mask over res's elements (8 per byte) -- res counts only where it is set
+at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res,
+                         const c10::optional<at::Tensor>& resmask) {
   const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
   const int64_t M = conv_rows(dy, cout, "dy");
   conv_check_w(w, cout, cin);
@@ -615,8 +620,14 @@ at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::o
   if (has_res) {
     TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad: residual layout");
   }
+  const bool has_mask = resmask.has_value() && resmask->defined();
+  if (has_mask) {
+    TORCH_CHECK(has_res && resmask->scalar_type() == at::kByte && resmask->is_contiguous() &&
+                    resmask->numel() == M * cin / 8, "conv1x1_dgrad: resmask must be a uint8 bit mask over res");
+  }
   check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
-                            cout, nullptr, nullptr, nullptr, nullptr, cur_stream(dy)),
+                            cout, nullptr, nullptr, nullptr, nullptr, cur_stream(dy),
+                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr),
         "conv1x1_dgrad");
   return dx;
 }
@@ -1180,7 +1191,7 @@ TORCH_LIBRARY(madnn, m) {
       "Tensor");
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? mask, bool has_res, Tensor? w, Tensor save_mean, Tensor save_invstd, "
-      "Tensor scale, Tensor shift, bool relu, bool need_wgrad) -> (Tensor, Tensor, Tensor, Tensor)");
+      "Tensor scale, Tensor shift, bool relu, bool need_wgrad, bool write_dres=True) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "bn_fwd_dual(Tensor x, Tensor r, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
       "Tensor(c!)? nbt, float momentum, float eps, Tensor? partial, Tensor? w_r, Tensor? b_r, "
@@ -1194,7 +1205,7 @@ TORCH_LIBRARY(madnn, m) {
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
       "Tensor(c!) dv, bool causal, float scale, Tensor(d!)? colsum=None) -> ()");
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
-  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None) -> Tensor");
+  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None) -> Tensor");
   m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
       "conv3x3_fwd_bnb(Tensor x, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");

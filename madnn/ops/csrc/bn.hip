@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       for (int j = 0; j < 8; ++j) o[j] = ra[j] * dv[j] + rb[j] * rv[j] + rc[j];
       store8<XDT>(dres, i, o);
     } else if constexpr (RES) {
-      store8<XDT>(dres, i, dv);
+      if (dres != nullptr) store8<XDT>(dres, i, dv);  // null: the consumer masks dy itself (resmask)
     }
   };
   if (fixed && (reverse & 4)) {  // two chunks per trip (see bn_apply_kernel)

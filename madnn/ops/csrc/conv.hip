@@ -70,6 +70,8 @@ struct GemmArgs {
   const uint16_t* b;
   void* out;
   const uint16_t* res;  // store epilogue: out = D + res (same layout as out), or null
+  const unsigned char* resmask;  // with res: res element e counts only where bit e of resmask is set
+                                 // (a ReLU bit mask over the same [J][I] elements, 8 per byte), or null
   float* stats;
   const float* bsc;  // B-operand BatchNorm prologue: relu(b * bsc[c] + bsh[c]) (PRO kernels)
   const float* bsh;
@@ -305,7 +307,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
           if (j < p.J) {
             u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, c));
             if (p.res != nullptr) {  // fused residual-gradient accumulation (fp32 add, one rounding)
-              const u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + j * p.ldo + i0 + 8 * c);
+              u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + j * p.ldo + i0 + 8 * c);
+              if (p.resmask != nullptr) {
+                const unsigned bits = p.resmask[(j * p.ldo + i0 + 8 * c) >> 3];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  rv[e] &= ((bits >> (2 * e)) & 1u ? 0xffffu : 0u) | ((bits >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+              }
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const float lo = bf16_to_f32((unsigned short)(v[e] & 0xffffu)) +
@@ -486,7 +494,7 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
 // backward sums as partial [madnn_conv1x1_dgrad_rows][2][cin] (see BNB)
 hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const void* res, int64_t M, int64_t cin,
                                int64_t cout, const void* bny, const float* bnsc, const float* bnsh, float* partial,
-                               hipStream_t s) {
+                               hipStream_t s, const unsigned char* resmask) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -496,6 +504,7 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   p.ldb = cout;
   p.out = dx;
   p.res = static_cast<const uint16_t*>(res);
+  p.resmask = res != nullptr ? resmask : nullptr;
   p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cin;

@@ -140,6 +140,36 @@ def test_bf16_bottleneck_k9_matches_miopen_and_fp32(cuda, monkeypatch):
         assert ((a - b).norm() / b.norm()).item() < 0.1  # bf16 activations vs fp32: ~7 % on dx
 
 
+def test_identity_block_deferred_relu_mask_matches(cuda, monkeypatch):
+    """A stride-1 Bottleneck on the K9 path: bn3's backward leaves the ReLU-masked identity gradient
+    to conv1's K9 data grad (dy + bit mask read in its epilogue) -- bitwise equal to writing the
+    masked copy first (same fp32 adds, same roundings)."""
+    import madnn.ops as O
+    from madnn.models.resnet import Bottleneck
+
+    torch.manual_seed(8)
+    blk = Bottleneck(256, 64)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+    blk = blk.to(cuda).to(memory_format=torch.channels_last)
+    for p in blk.parameters():
+        if p.dim() == 4:
+            p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
+    x0 = _rand((4, 256, 14, 14), cuda)
+    g = torch.randn(4, 256, 14, 14, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = []
+    for defer in (True, False):
+        monkeypatch.setattr(O, "DEFER_RES_MASK", defer)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        y.backward(g)
+        res.append((y.float(), x.grad.float(), blk.conv1.weight.grad.float(), blk.bn3.weight.grad.float()))
+    for a, b in zip(*res):
+        torch.testing.assert_close(a, b, atol=0, rtol=0)
+
+
 @pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8)])
 def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw):
     """A stride-2 downsample Bottleneck: the downsample 1x1 run as a stride-1 K9 conv on conv1's
