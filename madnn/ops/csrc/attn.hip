@@ -333,8 +333,11 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const MadnnAttnArgs
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
-  __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[2][kTile * D];
+  // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
+  // [128 rows][D] fp32 image (4 * 64 * D bf16 = 128 * D fp32)
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[4][kTile * D];
+  uint16_t(*sK)[kTile * D] = sKV;
+  uint16_t(*sV)[kTile * D] = sKV + 2;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
   const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
   int qblk, b, h;
@@ -440,23 +443,28 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
     }
   }
   if (a.cpart != nullptr) {
-    // column sums of the stored (bf16-rounded) dq over this workgroup's 128 query rows: lane
-    // (l32, hh) holds column 32 d + 8 g + 4 hh + i of row qrow; sum the 32 rows of a half-wave by
-    // shuffles, then the 4 waves through LDS
-    __shared__ float red[4][D];
+    // column sums of the stored (bf16-rounded) dq over this workgroup's 128 query rows: every lane
+    // writes its row (4 consecutive columns per 16-B chunk; chunk index XOR row & 15 so the 32 rows
+    // of a half-wave spread over the banks) into the K/V block as [128][D] fp32, then D threads
+    // each sum one column (shuffle trees cost ~75 us per launch at GPT-2 medium's shape)
+    float* red = reinterpret_cast<float*>(&sKV[0][0]);
+    const int row = wave * 32 + l32;
 #pragma unroll
     for (int d = 0; d < DB; ++d) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = qrow < a.S ? bf16_to_f32(f32_to_bf16(dq[d][r] * a.scale)) : 0.f;
+      for (int g = 0; g < 4; ++g) {
+        f32x4 v;
 #pragma unroll
-        for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        if (l32 == 0) red[wave][d * 32 + 8 * (r >> 2) + 4 * hh + (r & 3)] = v;
+        for (int i = 0; i < 4; ++i) v[i] = qrow < a.S ? bf16_to_f32(f32_to_bf16(dq[d][4 * g + i] * a.scale)) : 0.f;
+        const int chunk = (d * 8 + 2 * g + hh) ^ (row & 15);
+        *reinterpret_cast<f32x4*>(red + row * D + 4 * chunk) = v;
       }
     }
     __syncthreads();
     if (tid < D) {
-      const float s = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < kRowsWG; ++r) s += red[r * D + 4 * ((tid >> 2) ^ (r & 15)) + (tid & 3)];
       const int64_t C = (int64_t)(a.H + 2 * a.Hkv) * D;
       a.cpart[((int64_t)b * nqb + qblk) * C + (int64_t)h * D + tid] = s;
     }
