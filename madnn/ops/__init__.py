@@ -178,6 +178,7 @@ class _NormFn(torch.autograd.Function):
         # backward also returns dx's column sums for that Linear's bias gradient (_LinearFn reads
         # them off the gradient tensor instead of running its own column-sum pass)
         ctx.colsum = NORM_COLSUM and _from_biased_linear(x)
+        ctx.colsum_bf16 = ctx.colsum and _linear_bias_dtype(x) == torch.bfloat16
         ctx.rms = rms
         ctx.has_bias = b is not None
         ctx.has_res = res is not None
@@ -194,7 +195,7 @@ class _NormFn(torch.autograd.Function):
         x, w, mean, rstd = ctx.saved_tensors
         dres = ds.contiguous() if ((ctx.has_res or ctx.fork) and ds is not None) else None
         dx, dw, db, cs = torch.ops.madnn.norm_bwd(dy.contiguous(), x, w, mean, rstd, dres, ctx.rms, ctx.has_bias,
-                                                  ctx.colsum)
+                                                  ctx.colsum, ctx.colsum_bf16)
         dx = dx.view(ctx.shape)
         if ctx.colsum:
             dx._madnn_colsum = cs
@@ -207,13 +208,21 @@ NORM_COLSUM = os.environ.get("MADNN_NORM_COLSUM", "1") != "0"  # A/B switch (see
 _VIEW_NODES = ("ViewBackward0", "ReshapeAliasBackward0", "UnsafeViewBackward0")
 
 
-def _from_biased_linear(x: torch.Tensor) -> bool:
-    """``x`` is a biased madnn Linear's output, or one reshape of it (autograd passes the gradient
-    back through the view, whose base then carries the consumer's column sums)."""
+def _linear_bias_dtype(x: torch.Tensor):
+    """The bias dtype of the madnn Linear that produced ``x`` (directly or through one reshape), else
+    None (no such Linear, or one without a bias)."""
     gf = x.grad_fn
     if gf is not None and type(gf).__name__ in _VIEW_NODES and len(gf.next_functions) == 1:
         gf = gf.next_functions[0][0]
-    return gf is not None and type(gf).__name__ == "_LinearFnBackward" and getattr(gf, "bias_dtype", None) is not None
+    if gf is None or type(gf).__name__ != "_LinearFnBackward":
+        return None
+    return getattr(gf, "bias_dtype", None)
+
+
+def _from_biased_linear(x: torch.Tensor) -> bool:
+    """``x`` is a biased madnn Linear's output, or one reshape of it (autograd passes the gradient
+    back through the view, whose base then carries the consumer's column sums)."""
+    return _linear_bias_dtype(x) is not None
 
 
 def _norm(x, weight, bias, eps, rms, residual, fork=False):
@@ -490,6 +499,7 @@ class _AttnPackedFn(torch.autograd.Function):
         # qkv is (a view of) a biased madnn Linear's output: the backward kernels also sum dQKV's
         # columns, which that Linear takes as its bias gradient (no column-sum pass of its own)
         ctx.colsum = ATTN_COLSUM and _from_biased_linear(qkv)
+        ctx.colsum_dtype = torch.bfloat16 if ctx.colsum and _linear_bias_dtype(qkv) == torch.bfloat16 else torch.float32
         return o
 
     @staticmethod
@@ -501,7 +511,7 @@ class _AttnPackedFn(torch.autograd.Function):
         dq, dk, dv = dqkv.split([heads, kv_heads, kv_heads], dim=2)
         cs = None
         if ctx.colsum:
-            cs = torch.empty((heads + 2 * kv_heads) * qkv.size(-1), dtype=torch.float32, device=qkv.device)
+            cs = torch.empty((heads + 2 * kv_heads) * qkv.size(-1), dtype=ctx.colsum_dtype, device=qkv.device)
         torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, cs)
         if cs is not None:
             dqkv._madnn_colsum = cs

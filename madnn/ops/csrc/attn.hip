@@ -663,7 +663,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
 
 // colsum[c] = sum_r cpart[r][c]: the dQKV column sums over all B * S rows
 __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float* __restrict__ cpart, int R, int C,
-                                                                    float* __restrict__ out) {
+                                                                    void* __restrict__ out, int out_bf16) {
   __shared__ float red[32][33];
   const int c = threadIdx.x % 32, sl = threadIdx.x / 32;
   const int n = blockIdx.x * 32 + c;
@@ -675,7 +675,11 @@ __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float*
   if (sl == 0 && n < C) {
     float tot = 0.f;
     for (int q = 0; q < 32; ++q) tot += red[q][c];
-    out[n] = tot;
+    if (out_bf16) {
+      static_cast<uint16_t*>(out)[n] = f32_to_bf16(tot);
+    } else {
+      static_cast<float*>(out)[n] = tot;
+    }
   }
 }
 
@@ -734,10 +738,11 @@ hipError_t madnn_attn_fwd(const MadnnAttnArgs* a, int D, int causal, hipStream_t
 // rows of MadnnAttnArgs::cpart: one per (batch, 128-row sequence block)
 int64_t madnn_attn_colsum_rows(int B, int S) { return (int64_t)B * ((S + kRowsWG - 1) / kRowsWG); }
 
-hipError_t madnn_attn_colsum_finalize(const float* cpart, int64_t R, int64_t C, float* out, hipStream_t st) {
+hipError_t madnn_attn_colsum_finalize(const float* cpart, int64_t R, int64_t C, void* out, int out_bf16,
+                                      hipStream_t st) {
   if (R <= 0 || C <= 0) return hipSuccess;
   hipLaunchKernelGGL(attn_colsum_finalize_kernel, dim3((unsigned)((C + 31) / 32)), dim3(1024), 0, st, cpart, (int)R,
-                     (int)C, out);
+                     (int)C, out, out_bf16);
   return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ hipError_t madnn_norm_fwd(const void*, const void*, const void*, const void*, vo
                           int, float, int, int, int, hipStream_t);
 int64_t madnn_norm_bwd_workspace(int64_t, int);
 hipError_t madnn_norm_bwd(const void*, const void*, const void*, const float*, const float*, const void*, void*, void*,
-                          void*, float*, float*, int64_t, int, int, int, int, hipStream_t);
+                          void*, void*, int, float*, int64_t, int, int, int, int, hipStream_t);
 int madnn_bn_supported(int);
 int madnn_bn_partial_rows(int64_t, int);
 hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t, int, int, int, int, float, float,
@@ -44,7 +44,7 @@ int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
 int64_t madnn_attn_colsum_rows(int, int);
-hipError_t madnn_attn_colsum_finalize(const float*, int64_t, int64_t, float*, hipStream_t);
+hipError_t madnn_attn_colsum_finalize(const float*, int64_t, int64_t, void*, int, hipStream_t);
 int madnn_maxpool_supported(int64_t, int, int);
 hipError_t madnn_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 int madnn_pool_bn_supported(int64_t, int);
@@ -290,12 +290,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(const at::Te
   return {y, sum, mean, rstd};
 }
 
-// colsum: also the fp32 column sums of dx over the rows (the producing Linear's bias gradient)
+// colsum: also the column sums of dx over the rows (the producing Linear's bias gradient), in bf16
+// when colsum_bf16 (the Linear's bias dtype) else fp32
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, const at::Tensor& x,
                                                                     const at::Tensor& w, const at::Tensor& mean,
                                                                     const at::Tensor& rstd,
                                                                     const c10::optional<at::Tensor>& dres, bool rms,
-                                                                    bool has_bias, bool colsum) {
+                                                                    bool has_bias, bool colsum, bool colsum_bf16) {
   check_dev(x, "x");
   const int64_t H = w.numel();
   const int64_t rows = x.numel() / H;
@@ -310,10 +311,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Te
   if (dres.has_value() && dres->defined()) {
     dr = dres->scalar_type() == x.scalar_type() ? dres->contiguous() : dres->to(x.scalar_type()).contiguous();
   }
-  at::Tensor cs = colsum ? at::empty({H}, x.options().dtype(at::kFloat)) : at::empty({0}, x.options().dtype(at::kFloat));
+  const auto cdt = colsum_bf16 ? at::kBFloat16 : at::kFloat;
+  at::Tensor cs = colsum ? at::empty({H}, x.options().dtype(cdt)) : at::empty({0}, x.options().dtype(cdt));
   check(madnn_norm_bwd(dyc.data_ptr(), x.data_ptr(), w.data_ptr(), rms ? nullptr : mean.data_ptr<float>(),
                        rstd.data_ptr<float>(), dr.defined() ? dr.data_ptr() : nullptr, dx.data_ptr(), dw.data_ptr(),
-                       has_bias ? db.data_ptr() : nullptr, colsum ? cs.data_ptr<float>() : nullptr,
+                       has_bias ? db.data_ptr() : nullptr, colsum ? cs.data_ptr() : nullptr, colsum_bf16 ? 1 : 0,
                        ws.data_ptr<float>(), rows, (int)H, rms ? 1 : 0, dt_code(x), dt_code(w), cur_stream(x)),
         "norm_bwd");
   return {dx, dw, db, cs};
@@ -1162,20 +1164,24 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
   a.dq_sb = dq.stride(0); a.dq_ss = dq.stride(1); a.dq_sh = dq.stride(2);
   a.dk_sb = dk.stride(0); a.dk_ss = dk.stride(1); a.dk_sh = dk.stride(2);
   a.dv_sb = dv.stride(0); a.dv_ss = dv.stride(1); a.dv_sh = dv.stride(2);
-  // colsum (optional, fp32 [(H + 2 Hkv) D]): the column sums of dq | dk | dv over all B * S rows
+  // colsum (optional, fp32 or bf16 [(H + 2 Hkv) D]): the column sums of dq | dk | dv over all B * S rows
   const bool cs = colsum.has_value() && colsum->defined();
   at::Tensor cpart;
   int64_t R = 0, C = 0;
   if (cs) {
     C = (q.size(2) + 2 * k.size(2)) * D;
-    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->is_contiguous() && colsum->numel() == C,
-                "attn_bwd: colsum must be a contiguous fp32 [(H + 2 Hkv) * D]");
+    TORCH_CHECK((colsum->scalar_type() == at::kFloat || colsum->scalar_type() == at::kBFloat16) &&
+                    colsum->is_contiguous() && colsum->numel() == C,
+                "attn_bwd: colsum must be a contiguous fp32 / bf16 [(H + 2 Hkv) * D]");
     R = madnn_attn_colsum_rows(a.B, a.S);
     cpart = at::empty({R, C}, q.options().dtype(at::kFloat));
     a.cpart = cpart.data_ptr<float>();
   }
   check(madnn_attn_bwd(&a, (int)D, causal ? 1 : 0, cur_stream(q)), "attn_bwd");
-  if (cs) check(madnn_attn_colsum_finalize(a.cpart, R, C, colsum->data_ptr<float>(), cur_stream(q)), "attn_colsum");
+  if (cs)
+    check(madnn_attn_colsum_finalize(a.cpart, R, C, colsum->data_ptr(), colsum->scalar_type() == at::kBFloat16 ? 1 : 0,
+                                     cur_stream(q)),
+          "attn_colsum");
 }
 
 }  // namespace
@@ -1246,7 +1252,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("norm_fwd(Tensor x, Tensor? res, Tensor w, Tensor? b, float eps, bool rms) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "norm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dres, bool rms, bool has_bias, "
-      "bool colsum=False) -> (Tensor, Tensor, Tensor, Tensor)");
+      "bool colsum=False, bool colsum_bf16=False) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(madnn, CUDA, m) {

@@ -270,7 +270,7 @@ template <int WDT>
 __global__ __launch_bounds__(1024) void norm_wgrad_finalize_kernel(const float* __restrict__ partial, int G, int H,
                                                                    int has_bias, void* __restrict__ dw,
                                                                    void* __restrict__ dbias, int ns,
-                                                                   float* __restrict__ dsum) {
+                                                                   void* __restrict__ dsum, int dsum_bf16) {
   __shared__ float red[kWgSlices][33];
   const int lc = threadIdx.x & 31;
   const int ls = threadIdx.x >> 5;
@@ -297,7 +297,11 @@ __global__ __launch_bounds__(1024) void norm_wgrad_finalize_kernel(const float* 
     else if (col2 < 2 * H) {
       if (has_bias) Elem<WDT>::store(static_cast<typename Elem<WDT>::T*>(dbias), col2 - H, s);
     } else {
-      dsum[col2 - 2 * H] = s;
+      if (dsum_bf16) {
+        static_cast<uint16_t*>(dsum)[col2 - 2 * H] = f32_to_bf16(s);
+      } else {
+        static_cast<float*>(dsum)[col2 - 2 * H] = s;
+      }
     }
   }
 }
@@ -380,9 +384,9 @@ static int64_t norm_bwd_groups(int64_t rows, int H) {
 
 int64_t madnn_norm_bwd_workspace(int64_t rows, int H) { return norm_bwd_groups(rows, H) * 3 * (int64_t)H; }
 
-// dsum (optional, fp32 [H]): column sums of dx over the rows (see norm_bwd_kernel CS)
+// dsum (optional, [H], bf16 if dsum_bf16 else fp32): column sums of dx over the rows (norm_bwd_kernel CS)
 hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const float* mean_in, const float* rstd_in,
-                          const void* dres, void* dx, void* dw, void* dbias, float* dsum, float* workspace,
+                          const void* dres, void* dx, void* dw, void* dbias, void* dsum, int dsum_bf16, float* workspace,
                           int64_t rows, int H, int rms, int xdt, int wdt, hipStream_t stream) {
   using namespace madnn;
   if (rows <= 0) return hipSuccess;
@@ -407,7 +411,7 @@ hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const fl
       MADNN_HIP_CHECK(hipGetLastError());
       const int fgrid = ((dsum != nullptr ? 3 * H : (has_bias ? 2 * H : H)) + 31) / 32;
       hipLaunchKernelGGL((norm_wgrad_finalize_kernel<WDT>), dim3(fgrid), dim3(32 * kWgSlices), 0, stream, workspace, G, H,
-                         has_bias, dw, dbias, ns, dsum);
+                         has_bias, dw, dbias, ns, dsum, dsum_bf16);
     });
   });
   return hipGetLastError();
