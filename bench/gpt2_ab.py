@@ -8,6 +8,7 @@ Variants toggle at run time (the model is built once):
   wgrad   : weight gradients on the per-shape faster of hipBLASLt / K12 split-K (on) vs hipBLASLt (off)
   colsum  : attn-proj / c_proj bias grads from the next norm's backward column sums (on) vs their own pass (off)
   attn_colsum: qkv bias grad from the attention backward's dQKV column sums (on) vs its own pass (off)
+  xent    : one-pass K6f cross entropy (loss + finished logit gradient in the forward) (on) vs two-pass K6 (off)
   gelu_fwd: c_fc forward on K12 with the fused bias + AUX + GELU epilogue (on) vs hipBLASLt + K11 GELU (off)
 Prints a JSON line with the per-window ms/step and the median of each arm.
 """
@@ -30,7 +31,8 @@ def main():
     ap.add_argument("--windows", type=int, default=6)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--switch", default="lt_res",
-                    choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp", "native", "wgrad", "gelu_fwd", "colsum", "attn_colsum"])
+                    choices=["lt_res", "gelu", "gelu_bwd_fast", "gelu_rcp", "native", "wgrad", "gelu_fwd", "colsum", "attn_colsum",
+                             "xent"])
     ap.add_argument("--native", default="", help="FUNC:KEY:ON:OFF -- a native tunable, e.g. madnn_norm_tune:1:4:2")
     a = ap.parse_args()
     import madnn
@@ -48,6 +50,8 @@ def main():
     def set_arm(on):
         if a.switch == "attn_colsum":
             ops.ATTN_COLSUM = on
+        elif a.switch == "xent":
+            ops.XENT_FUSED = on
         elif a.switch == "colsum":
             ops.NORM_COLSUM = on
         elif a.switch == "gelu_fwd":

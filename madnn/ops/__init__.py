@@ -266,6 +266,10 @@ class _BNFn(torch.autograd.Function):
         # mask instead of writing the masked copy of dy (one activation-sized write less)
         ctx.defer = (DEFER_RES_MASK and relu and residual is not None and mask.numel() > 0
                      and getattr(residual, "_madnn_defer_mask", False))
+        if BN_SUM_IN_DGRAD and training and relu and residual is not None and mask.numel() > 0 and x.dtype == torch.bfloat16:
+            # a consumer whose data grad runs on K9 (the next identity block's conv1) may take this BN's
+            # backward sums in that kernel's epilogue: it needs the BN input and the ReLU bit mask
+            y._madnn_bnsrc = (x, mask)
         return y
 
     @staticmethod
@@ -273,8 +277,14 @@ class _BNFn(torch.autograd.Function):
         x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         defer = ctx.defer and dy.dtype == x.dtype and dy.stride() == x.stride()
-        dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
-                                                  mean, invstd, scale, shift, ctx.relu, need_w, not defer)
+        part = getattr(dy, "_madnn_bnpart", None)
+        if part is not None and ctx.has_res and dy.dtype == x.dtype and dy.stride() == x.stride():
+            # the reduction came from the K9 data grad that produced dy (_Conv1x1Fn, conv1x1_dgrad_bnres)
+            dx, dw, db, dres = torch.ops.madnn.bn_bwd_ext_res(dy, x, weight, mean, invstd, scale, shift, part,
+                                                              mask, not defer)
+        else:
+            dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
+                                                      mean, invstd, scale, shift, ctx.relu, need_w, not defer)
         if defer:
             dres = dy.view_as(dy)
             dres._madnn_resmask = mask
@@ -283,6 +293,7 @@ class _BNFn(torch.autograd.Function):
 
 
 DEFER_RES_MASK = os.environ.get("MADNN_DEFER_RES_MASK", "1") != "0"  # A/B switch (see _BNFn.forward)
+BN_SUM_IN_DGRAD = os.environ.get("MADNN_BN_SUM_IN_DGRAD", "0") == "1"  # off: A/B -0.23 % (docs/PERF.md)
 
 
 def _apply_bit_mask(t: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
@@ -438,19 +449,45 @@ class _XentFn(torch.autograd.Function):
     def forward(ctx, logits, targets, shift, vocab, ignore_index):
         lg = logits.contiguous()
         tg = targets.contiguous()
-        loss_rows, lse = torch.ops.madnn.xent_fwd(lg, tg, bool(shift), int(vocab), int(ignore_index))
         used = tg[:, 1:] if shift else tg
         cnt = ((used != ignore_index) & (used >= 0) & (used < vocab)).sum().clamp(min=1).to(torch.float32)
+        ctx.grad = None
+        ctx.fused = bool(ctx.needs_input_grad[0] and XENT_FUSED and _xent_fused_ok(lg))
+        if ctx.fused:
+            # K6f: the gradient is finished here, in the same pass over the logits as the loss
+            # (backward only applies the upstream scale, a no-op launch for loss.backward())
+            loss_rows, ctx.grad = torch.ops.madnn.xent_fused(lg, tg, bool(shift), int(vocab), int(ignore_index),
+                                                            (1.0 / cnt).reshape(1))
+            return loss_rows.sum() / cnt
+        loss_rows, lse = torch.ops.madnn.xent_fwd(lg, tg, bool(shift), int(vocab), int(ignore_index))
         ctx.save_for_backward(lg, tg, lse, cnt)
         ctx.shift, ctx.vocab, ctx.ignore_index = shift, vocab, ignore_index
         return loss_rows.sum() / cnt
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.fused:
+            grad, ctx.grad = ctx.grad, None
+            if grad is None:
+                raise RuntimeError("madnn cross_entropy: the fused (K6f) gradient was already consumed by an "
+                                   "earlier backward; set MADNN_XENT_FUSED=0 to backward through it twice")
+            torch.ops.madnn.xent_rescale(grad, g.to(torch.float32).reshape(1))
+            return grad, None, None, None, None
         lg, tg, lse, cnt = ctx.saved_tensors
         gscale = (g.to(torch.float32) / cnt).reshape(1)
         grad = torch.ops.madnn.xent_bwd(lg, tg, lse, ctx.shift, ctx.vocab, ctx.ignore_index, gscale)
         return grad, None, None, None, None
+
+
+XENT_FUSED = os.environ.get("MADNN_XENT_FUSED", "1") != "0"  # A/B switch (bench/gpt2_ab.py)
+
+
+def _xent_fused_ok(lg: torch.Tensor) -> bool:
+    """K6f preconditions (mirrored by xent_fused_ok in binding.cpp): 16-bit contiguous logits whose rows
+    are 16-byte aligned and fit 32 chunks of 8 per lane of a 512-lane workgroup."""
+    ld = lg.size(-1)
+    return (lg.dtype in (torch.bfloat16, torch.float16) and lg.is_contiguous() and ld % 8 == 0
+            and ld // 8 <= 32 * 512 and lg.data_ptr() % 16 == 0)
 
 
 def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, *, shift: bool = False, vocab: Optional[int] = None,
@@ -602,7 +639,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         else:
             y = torch.nn.functional.conv2d(x, w) if x.dim() == 4 else torch.mm(x, w.reshape(w.size(0), -1).t())
             part = x.new_empty((0, 2, w.size(0)), dtype=torch.float32)
-        ctx.save_for_backward(x, w)
+        src = getattr(x, "_madnn_bnsrc", None) if (BN_SUM_IN_DGRAD and fork == 1 and dgrad == "k9") else None
+        ctx.bnsum = src is not None and src[0].shape == x.shape and src[0].stride() == x.stride()
+        ctx.save_for_backward(x, w, *(src if ctx.bnsum else ()))
         ctx.route = (dgrad, wgrad)
         ctx.fork = fork
         ctx.mark_non_differentiable(part)
@@ -614,7 +653,7 @@ class _Conv1x1Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dpart, dfork=None):
-        x, w = ctx.saved_tensors
+        x, w = ctx.saved_tensors[:2]
         dgrad, wgrad = ctx.route
         dy = _nhwc(dy.to(x.dtype))
         sub = None
@@ -627,7 +666,13 @@ class _Conv1x1Fn(torch.autograd.Function):
             res, resmask = _apply_bit_mask(res, resmask), None
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if dgrad == "k9":
+            if dgrad == "k9" and ctx.bnsum:
+                # x = relu(bn(y) + r) of the previous block (_BNFn): that BN's backward sums come out of
+                # this epilogue, over the gradient it writes (no reduction pass over dx and y)
+                bny, bnmask = ctx.saved_tensors[2:]
+                dx, part = torch.ops.madnn.conv1x1_dgrad_bnres(dy, w, res, resmask, bny, bnmask)
+                dx._madnn_bnpart = part
+            elif dgrad == "k9":
                 dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res, resmask)
             else:
                 w2 = w.reshape(w.size(0), -1)

@@ -20,8 +20,8 @@
 //    row reads (ds_read_b128, MFMA operand with the head dim as k) and the
 //    transposed reads (ds_read_b64_tr_b16, operand with the sequence as k) are
 //    bank-conflict-free (the swizzle proofs are in the comments of swz());
-//  * the backward is three kernels: delta = rowsum(dO*O); dQ (query blocks);
-//    dK/dV (key blocks, looping over the query heads of a grouped KV head) --
+//  * the backward is two kernels: dQ (query blocks; its prologue also forms delta = rowsum(dO*O)
+//    for its rows and writes it out); dK/dV (key blocks, looping over the query heads of a grouped KV head) --
 //    no atomics, deterministic;
 //  * block -> (sequence block, batch*head) mapping is XCD-aware: the workgroups
 //    dispatched to one XCD work on the same heads, so K/V tiles hit in its L2.
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const MadnnAttnArgs
 }
 
 // ------------------------------------------------------------------ backward: dQ
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool DELTA>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
@@ -347,18 +347,33 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
   const int qrow = q0w + l32;
   const int qc = min(qrow, a.S - 1);
   bf16x8 qf[DS], df[DS];
+  // delta = rowsum(dO * O) of this lane's query row, from the dO fragments it holds anyway plus the
+  // matching O halves (the two lane halves hh = 0/1 own alternate 8-column chunks); written out for
+  // the dK/dV kernel that follows (no separate delta pass)
+  float dl = 0.f;
   {
     const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)qc * a.q_ss;
     const uint16_t* dp = a.dout + b * a.o_sb + h * a.o_sh + (int64_t)qc * a.o_ss;
+    const uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qc * a.o_ss;
 #pragma unroll
     for (int s = 0; s < DS; ++s) {
       qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
       df[s] = *reinterpret_cast<const bf16x8*>(dp + 16 * s + 8 * hh);
+      if constexpr (DELTA) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(op + 16 * s + 8 * hh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl = fmaf(static_cast<float>(df[s][j]), static_cast<float>(ov[j]), dl);
+      }
     }
+    if constexpr (DELTA) dl += __shfl_xor(dl, 32, kWave);
   }
   const int64_t srow = ((int64_t)b * a.H + h) * a.S + qc;
   const float lse = a.lse[srow];
-  const float dl = a.delta[srow];
+  if constexpr (DELTA) {
+    if (hh == 0 && qrow < a.S) a.delta[srow] = dl;
+  } else {
+    dl = a.delta[srow];
+  }
   const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
   f32x16 dq[DB];
@@ -686,6 +701,7 @@ __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float*
 int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default), 0 = V1
 // (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
 // their loops are not VALU-issue-bound)
+int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
 
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
@@ -700,11 +716,15 @@ hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
 
 template <int D, bool CAUSAL>
 hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
-  const int64_t lanes = (int64_t)a.B * a.S * a.H * (D / 8);
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((lanes + 255) / 256), dim3(256), 0, st, a);
-  MADNN_HIP_CHECK(hipGetLastError());
   const int nb = (a.S + kRowsWG - 1) / kRowsWG;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+  if (g_attn_dq_delta) {
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+  } else {
+    const int64_t lanes = (int64_t)a.B * a.S * a.H * (D / 8);
+    hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((lanes + 255) / 256), dim3(256), 0, st, a);
+    MADNN_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+  }
   MADNN_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
   return hipGetLastError();
@@ -720,11 +740,13 @@ extern "C" {
 
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 
-// A/B knob: key 0 = kernel version (1 = V2, 0 = V1); returns the previous value
+// A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0);
+// returns the previous value
 int madnn_attn_tune(int key, int value) {
-  if (key != 0) return -1;
-  const int old = g_attn_v2;
-  g_attn_v2 = value ? 1 : 0;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : nullptr;
+  if (slot == nullptr) return -1;
+  const int old = *slot;
+  *slot = value ? 1 : 0;
   return old;
 }
 

@@ -60,6 +60,10 @@ hipError_t madnn_xent_fwd(const void*, int, const int64_t*, int64_t, int64_t, in
                           hipStream_t);
 hipError_t madnn_xent_bwd(const void*, int, const int64_t*, const float*, int64_t, int64_t, int64_t, int, int, int64_t,
                           const float*, void*, hipStream_t);
+int madnn_xent_fused_chunks(int64_t);
+hipError_t madnn_xent_fused(const void*, int, const int64_t*, int64_t, int64_t, int64_t, int, int, int64_t,
+                            const float*, float*, void*, hipStream_t);
+hipError_t madnn_xent_rescale(void*, int, int64_t, const float*, hipStream_t);
 hipError_t madnn_bn_bwd(const void*, const void*, const unsigned char*, int, void*, void*, int64_t, int, int, int,
                         const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
                         float*, hipStream_t);
@@ -75,7 +79,8 @@ int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, const float*,
                              const float*, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, const void*,
-                               const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr);
+                               const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr,
+                               const unsigned char* = nullptr);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
@@ -95,7 +100,7 @@ hipError_t madnn_conv3x3_fwd_bnb(const void*, const void*, void*, float*, const 
                                  int, int, int, int, hipStream_t);
 hipError_t madnn_bn_bwd_ext(const void*, const void*, void*, int64_t, int, int, const float*, const float*,
                             const float*, const float*, const float*, float*, float*, float*, const float*, int, float*,
-                            hipStream_t);
+                            hipStream_t, const unsigned char* = nullptr, void* = nullptr);
 int madnn_bn_prereduce_floats(int);
 hipError_t madnn_conv3x3_wgrad(const void*, const void*, float*, void*, int, int, int, int, int, int, hipStream_t);
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
@@ -654,6 +659,38 @@ std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnb(const at::Tensor& dy, const
   return {dx, part};
 }
 
+// conv1x1_dgrad whose dx is the incoming gradient of relu(bn(bny) + r) with that ReLU's bit mask
+// bnmask: also returns bn's backward sums (sum g, sum g*bny), g = dx * mask, from the epilogue
+// -> (dx, partial [rows, 2, Cin]); res / resmask as in conv1x1_dgrad
+std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnres(const at::Tensor& dy, const at::Tensor& w,
+                                                       const c10::optional<at::Tensor>& res,
+                                                       const c10::optional<at::Tensor>& resmask, const at::Tensor& bny,
+                                                       const at::Tensor& bnmask) {
+  const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
+  const int64_t M = conv_rows(dy, cout, "dy");
+  conv_check_w(w, cout, cin);
+  TORCH_CHECK(conv_rows(bny, cin, "bny") == M && bny.dim() == dy.dim(), "conv1x1_dgrad_bnres: bny layout");
+  TORCH_CHECK(bnmask.scalar_type() == at::kByte && bnmask.is_contiguous() && bnmask.numel() == M * cin / 8,
+              "conv1x1_dgrad_bnres: bnmask must be a uint8 bit mask over bny");
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) {
+    TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad_bnres: residual layout");
+  }
+  const bool has_mask = resmask.has_value() && resmask->defined();
+  if (has_mask) {
+    TORCH_CHECK(has_res && resmask->scalar_type() == at::kByte && resmask->is_contiguous() &&
+                    resmask->numel() == M * cin / 8, "conv1x1_dgrad_bnres: resmask must be a uint8 bit mask over res");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dx = conv_out_like(dy, cin);
+  at::Tensor part = at::empty({madnn_conv1x1_dgrad_rows(M, cin, cout), 2, cin}, dy.options().dtype(at::kFloat));
+  check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
+                            cout, bny.data_ptr(), nullptr, nullptr, part.data_ptr<float>(), cur_stream(dy),
+                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr, bnmask.data_ptr<uint8_t>()),
+        "conv1x1_dgrad_bnres");
+  return {dx, part};
+}
+
 // fp32 [Cout, Cin] weight gradient
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
                          const c10::optional<at::Tensor>& shift) {
@@ -851,6 +888,36 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_bwd_ext(const at::Tensor& dy, 
   return {dx, dw, db};
 }
 
+// bn_bwd_ext for relu(bn(x) + r) with the ReLU bit mask (ResNet identity blocks' bn3, reduction from
+// conv1x1_dgrad_bnres): -> (dx, dw, db, dres); dres = dy * mask is written only with write_dres
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd_ext_res(
+    const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& w, const at::Tensor& save_mean,
+    const at::Tensor& save_invstd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& partial,
+    const at::Tensor& mask, bool write_dres) {
+  check_dev(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = bn_rows(x, C);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && dy.strides() == x.strides(),
+              "bn_bwd_ext_res: bf16 dy / x of one layout");
+  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.is_contiguous() && partial.dim() == 3 &&
+                  partial.size(1) == 2 && partial.size(2) == C,
+              "bn_bwd_ext_res: partial must be fp32 [rows, 2, C]");
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.is_contiguous() && mask.numel() * 8 == M * C,
+              "bn_bwd_ext_res: uint8 bit mask over x");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  at::Tensor dx = at::empty_like(x), dw = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
+  at::Tensor dres = write_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  at::Tensor ws = at::empty({(int64_t)madnn_bn_prereduce_floats((int)C)}, fo);
+  check(madnn_bn_bwd_ext(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, 1, optf(w), save_mean.data_ptr<float>(),
+                         save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                         dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), partial.data_ptr<float>(),
+                         (int)partial.size(0), ws.data_ptr<float>(), cur_stream(x), mask.data_ptr<uint8_t>(),
+                         write_dres ? dres.data_ptr() : nullptr),
+        "bn_bwd_ext_res");
+  return {dx, dw, db, dres};
+}
+
 // dW [Co, Ci, 3, 3] (channels_last) of y = conv3x3(x, w): dy [N, Co, H, W], x [N, Ci, H, W], both NHWC bf16
 at::Tensor conv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, bool out_bf16) {
   check_dev(x, "x");
@@ -969,6 +1036,38 @@ at::Tensor xent_bwd(const at::Tensor& logits, const at::Tensor& targets, const a
                        grad.data_ptr(), cur_stream(logits)),
         "xent_bwd");
   return grad;
+}
+
+// K6f: loss rows and the finished logit gradient (scaled by gscale[0]) from one pass; 16-bit logits
+// with 16-byte aligned rows only (xent_fused_ok).
+bool xent_fused_ok(const at::Tensor& logits) {
+  return (logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kHalf) && logits.is_contiguous() &&
+         madnn_xent_fused_chunks(logits.size(-1)) > 0 && (reinterpret_cast<uintptr_t>(logits.data_ptr()) & 15) == 0;
+}
+
+std::tuple<at::Tensor, at::Tensor> xent_fused(const at::Tensor& logits, const at::Tensor& targets, bool shift,
+                                              int64_t V, int64_t ignore_index, const at::Tensor& gscale) {
+  check_dev(logits, "logits");
+  const XentGeom g = xent_geom(logits, targets, shift);
+  TORCH_CHECK(V > 0 && V <= g.ld, "xent: bad vocabulary size");
+  TORCH_CHECK(xent_fused_ok(logits), "xent_fused: 16-bit contiguous logits with 16-byte aligned rows");
+  TORCH_CHECK(gscale.scalar_type() == at::kFloat && gscale.is_cuda(), "xent: fp32 device grad scale");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  at::Tensor loss = at::empty({g.n_loss_rows}, logits.options().dtype(at::kFloat));
+  at::Tensor grad = at::empty_like(logits);
+  check(madnn_xent_fused(logits.data_ptr(), dt_code(logits), targets.data_ptr<int64_t>(), g.n_loss_rows, g.seq, g.ld,
+                         (int)V, (int)ignore_index, g.n_rows_all, gscale.data_ptr<float>(), loss.data_ptr<float>(),
+                         grad.data_ptr(), cur_stream(logits)),
+        "xent_fused");
+  return {loss, grad};
+}
+
+void xent_rescale(at::Tensor grad, const at::Tensor& g) {
+  check_dev(grad, "grad");
+  TORCH_CHECK(grad.is_contiguous() && g.scalar_type() == at::kFloat && g.is_cuda(), "xent_rescale: bad operands");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
+  check(madnn_xent_rescale(grad.data_ptr(), dt_code(grad), grad.numel(), g.data_ptr<float>(), cur_stream(grad)),
+        "xent_rescale");
 }
 
 // K7 NHWC max-pool.  x: [N, C, H, W] in channels_last.  Returns (y, argmax bytes);
@@ -1196,6 +1295,10 @@ TORCH_LIBRARY(madnn, m) {
       "xent_bwd(Tensor logits, Tensor targets, Tensor lse, bool shift, int V, int ignore_index, Tensor gscale) -> "
       "Tensor");
   m.def(
+      "xent_fused(Tensor logits, Tensor targets, bool shift, int V, int ignore_index, Tensor gscale) -> "
+      "(Tensor, Tensor)");
+  m.def("xent_rescale(Tensor(a!) grad, Tensor g) -> ()");
+  m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? mask, bool has_res, Tensor? w, Tensor save_mean, Tensor save_invstd, "
       "Tensor scale, Tensor shift, bool relu, bool need_wgrad, bool write_dres=True) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
@@ -1213,6 +1316,12 @@ TORCH_LIBRARY(madnn, m) {
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
   m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None) -> Tensor");
   m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
+  m.def(
+      "conv1x1_dgrad_bnres(Tensor dy, Tensor w, Tensor? res, Tensor? resmask, Tensor bny, Tensor bnmask) -> "
+      "(Tensor, Tensor)");
+  m.def(
+      "bn_bwd_ext_res(Tensor dy, Tensor x, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, "
+      "Tensor shift, Tensor partial, Tensor mask, bool write_dres) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "conv3x3_fwd_bnb(Tensor x, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
@@ -1270,10 +1379,14 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("bn_coef", bn_coef);
   m.impl("conv3x3_fwd_bnb", conv3x3_fwd_bnb);
   m.impl("conv1x1_dgrad_bnb", conv1x1_dgrad_bnb);
+  m.impl("conv1x1_dgrad_bnres", conv1x1_dgrad_bnres);
+  m.impl("bn_bwd_ext_res", bn_bwd_ext_res);
   m.impl("bn_bwd_ext", bn_bwd_ext);
   m.impl("bn_bwd_dual", bn_bwd_dual);
   m.impl("xent_fwd", xent_fwd);
   m.impl("xent_bwd", xent_bwd);
+  m.impl("xent_fused", xent_fused);
+  m.impl("xent_rescale", xent_rescale);
   m.impl("maxpool_fwd", maxpool_fwd);
   m.impl("pool_bn_fwd", pool_bn_fwd);
   m.impl("pool_bn_bwd", pool_bn_bwd);

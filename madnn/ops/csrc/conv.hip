@@ -78,6 +78,8 @@ struct GemmArgs {
   const uint16_t* bny;  // BNB epilogue (data grad): BN input y [J][I] whose backward sums are taken,
   const float* bnsc;    //   with its forward scale / shift (ReLU mask = y * sc + sh > 0)
   const float* bnsh;
+  const unsigned char* bnmask;  // BNB with a stored ReLU bit mask over [J][I] (8 per byte) instead of
+                                // y * sc + sh > 0: the BN's ReLU follows a residual add (bnsc unused)
   int64_t lda, ldb, ldo;
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
@@ -231,6 +233,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   }
   if constexpr (BNB) {  // this thread's 8 output channels (chunk tid % CPR of the i tile) are fixed
     const int cc = tid % (BI / 8);
+    if (p.bnmask == nullptr)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bs[e] = p.bnsc[i0 + 8 * cc + e];
@@ -325,6 +328,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
             *reinterpret_cast<u32x4*>(out + j * p.ldo + i0 + 8 * c) = v;
             if constexpr (BNB) {
               const u32x4 yv = *reinterpret_cast<const u32x4*>(p.bny + j * p.ldo + i0 + 8 * c);
+              const unsigned mb = p.bnmask != nullptr ? p.bnmask[(j * p.ldo + i0 + 8 * c) >> 3] : 0u;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
 #pragma unroll
@@ -332,7 +336,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
                   const int k = 2 * e + hf;
                   const float g = bf16_to_f32((unsigned short)(hf ? v[e] >> 16 : v[e] & 0xffffu));
                   const float yy = bf16_to_f32((unsigned short)(hf ? yv[e] >> 16 : yv[e] & 0xffffu));
-                  const float gm = yy * bs[k] + bh[k] > 0.f ? g : 0.f;
+                  const bool on = p.bnmask != nullptr ? ((mb >> k) & 1u) != 0u : yy * bs[k] + bh[k] > 0.f;
+                  const float gm = on ? g : 0.f;
                   ssum[k] += gm;
                   ssq[k] += gm * yy;
                 }
@@ -492,9 +497,11 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
 // dx = dY W (+ res: an accumulated gradient of the same layout, added in the epilogue)
 // bny/bnsc/bnsh/partial (optional, all or none): dx is d relu(bn(bny)); the epilogue also writes bn's
 // backward sums as partial [madnn_conv1x1_dgrad_rows][2][cin] (see BNB)
+// bny/bnmask/partial (with or without res): the same sums for relu(bn(bny) + r), whose ReLU is the
+// stored bit mask (a ResNet identity block's bn3, whose output x is: dx feeds that bn's backward)
 hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const void* res, int64_t M, int64_t cin,
                                int64_t cout, const void* bny, const float* bnsc, const float* bnsh, float* partial,
-                               hipStream_t s, const unsigned char* resmask) {
+                               hipStream_t s, const unsigned char* resmask, const unsigned char* bnmask) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -514,7 +521,9 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   plan_persistent(p, M, wide ? 128 : 64, cin, cout);
   const int grid = p.i_tiles * p.j_groups;
   if (bny != nullptr) {
-    if (bnsc == nullptr || bnsh == nullptr || partial == nullptr || res != nullptr) return hipErrorInvalidValue;
+    if (partial == nullptr) return hipErrorInvalidValue;
+    if (bnmask == nullptr && (bnsc == nullptr || bnsh == nullptr || res != nullptr)) return hipErrorInvalidValue;
+    p.bnmask = bnmask;
     p.bny = static_cast<const uint16_t*>(bny);
     p.bnsc = bnsc;
     p.bnsh = bnsh;

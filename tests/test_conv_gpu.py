@@ -172,6 +172,46 @@ def test_identity_block_deferred_relu_mask_matches(cuda, monkeypatch):
     assert ((res[0][3] - res[1][3]).norm() / res[1][3].norm()).item() < 1e-2
 
 
+def test_identity_bn3_sums_from_next_conv1_dgrad(cuda, monkeypatch):
+    """Two chained stride-1 Bottlenecks: the first block's bn3 (relu(bn3(y) + x), bit-mask ReLU) takes
+    its backward sums from the second block's conv1 K9 data-grad epilogue (conv1x1_dgrad_bnres +
+    bn_bwd_ext_res) instead of its own reduction pass -- same forward bitwise, gradients to fp32
+    summation-order tolerance against the unfused path."""
+    import madnn.ops as O
+    from madnn.models.resnet import Bottleneck
+
+    torch.manual_seed(12)
+    blks = torch.nn.Sequential(Bottleneck(256, 64), Bottleneck(256, 64))
+    for m in blks.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
+            torch.nn.init.uniform_(m.bias, -0.2, 0.2)
+    blks = blks.to(cuda).to(memory_format=torch.channels_last)
+    for p in blks.parameters():
+        if p.dim() == 4:
+            p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
+    x0 = _rand((4, 256, 14, 14), cuda)
+    g = torch.randn(4, 256, 14, 14, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    calls = []
+    real = torch.ops.madnn.bn_bwd_ext_res
+    monkeypatch.setattr(torch.ops.madnn, "bn_bwd_ext_res", lambda *a: calls.append(1) or real(*a))
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(O, "BN_SUM_IN_DGRAD", fused)
+        blks.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = blks(x)
+        y.backward(g)
+        b0 = blks[0]
+        res.append((y.float(), x.grad.float(), b0.bn3.weight.grad.float(), b0.bn3.bias.grad.float(),
+                    b0.conv3.weight.grad.float()))
+        assert len(calls) == (1 if fused else 0)
+        calls.clear()
+    torch.testing.assert_close(res[0][0], res[1][0], atol=0, rtol=0)
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert ((a - b).norm() / b.norm()).item() < 1e-2
+
+
 @pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8)])
 def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw):
     """A stride-2 downsample Bottleneck: the downsample 1x1 run as a stride-1 K9 conv on conv1's

@@ -283,6 +283,43 @@ def test_fused_cross_entropy(cuda, V, ld, shift, dt):
         assert logits.grad[..., V:].abs().max() == 0
 
 
+@pytest.mark.parametrize("V,ld", [(50257, 50304), (128256, 128256), (130, 136)])
+def test_one_pass_cross_entropy_matches_two_pass(cuda, V, ld, monkeypatch):
+    """K6f (loss + finished gradient in one pass over the logits, backward only rescales) against the
+    two-pass K6 and fp32 F.cross_entropy, with an upstream gradient != 1 and ignored targets."""
+    torch.manual_seed(5)
+    B, S = 2, 9
+    base = (torch.randn(B, S, ld, device=cuda) * 3).bfloat16()
+    tg = torch.randint(0, V, (B, S), device=cuda)
+    tg[1, 4] = -100
+    assert ops._xent_fused_ok(base)
+    grads, losses = [], []
+    for fused in (True, False):
+        monkeypatch.setattr(ops, "XENT_FUSED", fused)
+        lg = base.clone().requires_grad_(True)
+        loss = ops.cross_entropy(lg, tg, shift=True, vocab=V)
+        (loss * 2.5).backward()
+        grads.append(lg.grad.float())
+        losses.append(loss.detach().float())
+    lr = base.float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr[:, :-1, :V].reshape(-1, V), tg[:, 1:].reshape(-1), ignore_index=-100)
+    (ref * 2.5).backward()
+    torch.testing.assert_close(losses[0], ref.detach(), atol=2e-3, rtol=2e-3)
+    torch.testing.assert_close(losses[0], losses[1], atol=1e-5, rtol=1e-5)
+    scale = lr.grad.abs().max().item()
+    torch.testing.assert_close(grads[0], lr.grad, atol=2e-2 * scale, rtol=2e-2)
+    torch.testing.assert_close(grads[0], grads[1], atol=1e-2 * scale, rtol=1e-2)
+    assert grads[0][:, :, V:].abs().sum() == 0 and grads[0][:, -1].abs().max() == 0
+    assert grads[0][1, 3].abs().max() == 0  # the ignored target's row
+    # the one-pass gradient is handed out once; a second backward says how to get two
+    monkeypatch.setattr(ops, "XENT_FUSED", True)
+    lg = base.clone().requires_grad_(True)
+    loss = ops.cross_entropy(lg, tg, shift=True, vocab=V)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="MADNN_XENT_FUSED"):
+        loss.backward()
+
+
 @pytest.mark.parametrize("geom", [(3, 2, 1, 16, 16), (3, 2, 1, 15, 13), (2, 2, 0, 8, 10), (3, 1, 1, 9, 7),
                                   (5, 3, 2, 17, 11)])
 @pytest.mark.parametrize("C", [8, 64, 200])
