@@ -293,6 +293,7 @@ class _BNFn(torch.autograd.Function):
 
 
 DEFER_RES_MASK = os.environ.get("MADNN_DEFER_RES_MASK", "1") != "0"  # A/B switch (see _BNFn.forward)
+SUB_IN_DGRAD = os.environ.get("MADNN_SUB_IN_DGRAD", "1") != "0"  # A/B switch (see _Conv1x1Fn.backward)
 BN_SUM_IN_DGRAD = os.environ.get("MADNN_BN_SUM_IN_DGRAD", "0") == "1"  # off: A/B -0.23 % (docs/PERF.md)
 
 
@@ -672,6 +673,10 @@ class _Conv1x1Fn(torch.autograd.Function):
                 bny, bnmask = ctx.saved_tensors[2:]
                 dx, part = torch.ops.madnn.conv1x1_dgrad_bnres(dy, w, res, resmask, bny, bnmask)
                 dx._madnn_bnpart = part
+            elif dgrad == "k9" and sub is not None and res is None and SUB_IN_DGRAD and x.dim() == 4:
+                # the downsample path's compact gradient is added at the even pixels in the epilogue
+                dx = torch.ops.madnn.conv1x1_dgrad(dy, w, _nhwc(sub.to(x.dtype)), None, True)
+                sub = None
             elif dgrad == "k9":
                 dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res, resmask)
             else:

@@ -80,7 +80,7 @@ hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, i
                              const float*, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, const void*,
                                const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr,
-                               const unsigned char* = nullptr);
+                               const unsigned char* = nullptr, int = 0, int = 0);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
@@ -616,15 +616,25 @@ std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Te
 
 // dx = dy (*) w^T, plus `res` (a gradient of x's layout accumulated from another path) if given;
 // resmask: a ReLU bit mask over res's elements (8 per byte) -- res counts only where it is set
+// sub (with res, no resmask): res is the gradient of x[:, :, ::2, ::2] (compact NHWC), added at dx's even
+// pixels
 at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res,
-                         const c10::optional<at::Tensor>& resmask) {
+                         const c10::optional<at::Tensor>& resmask, bool sub) {
   const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
   const int64_t M = conv_rows(dy, cout, "dy");
   conv_check_w(w, cout, cin);
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   at::Tensor dx = conv_out_like(dy, cin);
   const bool has_res = res.has_value() && res->defined();
-  if (has_res) {
+  int sub_h = 0, sub_w = 0;
+  if (sub) {
+    TORCH_CHECK(has_res && dy.dim() == 4 && res->dim() == 4 && res->size(0) == dy.size(0) && res->size(1) == cin &&
+                    res->size(2) == (dy.size(2) + 1) / 2 && res->size(3) == (dy.size(3) + 1) / 2 &&
+                    conv_rows(*res, cin, "res") == res->numel() / cin,
+                "conv1x1_dgrad: sub residual must be the NHWC gradient of x[:, :, ::2, ::2]");
+    sub_h = (int)dy.size(2);
+    sub_w = (int)dy.size(3);
+  } else if (has_res) {
     TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad: residual layout");
   }
   const bool has_mask = resmask.has_value() && resmask->defined();
@@ -632,9 +642,10 @@ at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::o
     TORCH_CHECK(has_res && resmask->scalar_type() == at::kByte && resmask->is_contiguous() &&
                     resmask->numel() == M * cin / 8, "conv1x1_dgrad: resmask must be a uint8 bit mask over res");
   }
+  TORCH_CHECK(!(sub && has_mask), "conv1x1_dgrad: a sub residual takes no mask");
   check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
                             cout, nullptr, nullptr, nullptr, nullptr, cur_stream(dy),
-                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr),
+                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr, nullptr, sub_h, sub_w),
         "conv1x1_dgrad");
   return dx;
 }
@@ -1314,7 +1325,7 @@ TORCH_LIBRARY(madnn, m) {
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
       "Tensor(c!) dv, bool causal, float scale, Tensor(d!)? colsum=None) -> ()");
   m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
-  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None) -> Tensor");
+  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None, bool sub=False) -> Tensor");
   m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
       "conv1x1_dgrad_bnres(Tensor dy, Tensor w, Tensor? res, Tensor? resmask, Tensor bny, Tensor bnmask) -> "

@@ -84,6 +84,8 @@ struct GemmArgs {
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
   int xcd;  // 1: remap workgroup ids so consecutive logical ids share an XCD (and its L2)
+  int sub_h, sub_w;  // > 0: res is the compact stride-2 subsample [N][ceil(H/2)][ceil(W/2)][I] of the
+                     // output's [N][H][W] pixel grid, added at the even (h, w) rows only
 };
 
 // One operand's 64-deep slice, register-staged: R rows of "row" memory ([x][ld], k
@@ -309,8 +311,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
           const int64_t j = (int64_t)jt * BJ + r;
           if (j < p.J) {
             u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, c));
-            if (p.res != nullptr) {  // fused residual-gradient accumulation (fp32 add, one rounding)
-              u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + j * p.ldo + i0 + 8 * c);
+            int64_t rj = j;  // residual row of output row j (-1: none)
+            if (p.sub_h > 0) {
+              const int64_t wq = j % p.sub_w, t = j / p.sub_w, hq = t % p.sub_h, nq = t / p.sub_h;
+              rj = ((hq | wq) & 1) ? -1 : (nq * ((p.sub_h + 1) / 2) + hq / 2) * ((p.sub_w + 1) / 2) + wq / 2;
+            }
+            if (p.res != nullptr && rj >= 0) {  // fused residual-gradient accumulation (fp32 add, one rounding)
+              u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + rj * p.ldo + i0 + 8 * c);
               if (p.resmask != nullptr) {
                 const unsigned bits = p.resmask[(j * p.ldo + i0 + 8 * c) >> 3];
 #pragma unroll
@@ -499,9 +506,12 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
 // backward sums as partial [madnn_conv1x1_dgrad_rows][2][cin] (see BNB)
 // bny/bnmask/partial (with or without res): the same sums for relu(bn(bny) + r), whose ReLU is the
 // stored bit mask (a ResNet identity block's bn3, whose output x is: dx feeds that bn's backward)
+// sub_h / sub_w (> 0, no resmask): res is the compact x[:, :, ::2, ::2] gradient of a [M / (H W)][H][W]
+// pixel grid, added at the even pixels (a ResNet downsample path's input gradient)
 hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const void* res, int64_t M, int64_t cin,
                                int64_t cout, const void* bny, const float* bnsc, const float* bnsh, float* partial,
-                               hipStream_t s, const unsigned char* resmask, const unsigned char* bnmask) {
+                               hipStream_t s, const unsigned char* resmask, const unsigned char* bnmask, int sub_h,
+                               int sub_w) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -512,6 +522,12 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   p.out = dx;
   p.res = static_cast<const uint16_t*>(res);
   p.resmask = res != nullptr ? resmask : nullptr;
+  if (sub_h > 0 || sub_w > 0) {
+    if (res == nullptr || resmask != nullptr || sub_h <= 0 || sub_w <= 0 || M % ((int64_t)sub_h * sub_w))
+      return hipErrorInvalidValue;
+    p.sub_h = sub_h;
+    p.sub_w = sub_w;
+  }
   p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cin;

@@ -212,8 +212,9 @@ def test_identity_bn3_sums_from_next_conv1_dgrad(cuda, monkeypatch):
         assert ((a - b).norm() / b.norm()).item() < 1e-2
 
 
-@pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8)])
-def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw):
+@pytest.mark.parametrize("in_dgrad", [True, False])
+@pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8), (256, 64, 7)])
+def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw, in_dgrad):
     """A stride-2 downsample Bottleneck: the downsample 1x1 run as a stride-1 K9 conv on conv1's
     compact x[:, :, ::2, ::2] (gradient added into conv1's data grad at the even pixels) vs the
     stride-2 library convolution on the full input (same bf16 block: tight), and vs fp32 eager."""
@@ -238,7 +239,11 @@ def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes,
         if p.dim() == 4:
             p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
     x0 = _rand((4, inplanes, hw, hw), cuda)
-    g = torch.randn(4, planes * 4, hw // 2, hw // 2, device=cuda)
+    g = torch.randn(4, planes * 4, (hw + 1) // 2, (hw + 1) // 2, device=cuda)
+    # in_dgrad: the compact gradient is added at the even pixels inside conv1's K9 data-grad epilogue
+    # (odd hw: the last row / column is even, x[:, :, ::2, ::2] keeps it)
+    import madnn.ops as O
+    monkeypatch.setattr(O, "SUB_IN_DGRAD", in_dgrad)
     res = []
     for sub in (True, False):
         monkeypatch.setattr(R, "_DS_SUB", sub)
