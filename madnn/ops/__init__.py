@@ -293,7 +293,7 @@ class _BNFn(torch.autograd.Function):
 
 
 DEFER_RES_MASK = os.environ.get("MADNN_DEFER_RES_MASK", "1") != "0"  # A/B switch (see _BNFn.forward)
-SUB_IN_DGRAD = os.environ.get("MADNN_SUB_IN_DGRAD", "1") != "0"  # A/B switch (see _Conv1x1Fn.backward)
+SUB_IN_DGRAD = os.environ.get("MADNN_SUB_IN_DGRAD", "0") == "1"  # off: A/B -0.28 % (docs/PERF.md)
 BN_SUM_IN_DGRAD = os.environ.get("MADNN_BN_SUM_IN_DGRAD", "0") == "1"  # off: A/B -0.23 % (docs/PERF.md)
 
 
