@@ -49,7 +49,9 @@ def _record(op: str, group, t: Optional[torch.Tensor]):
 
         _checker["hash"] = OrderHash()
     gid = 0
-    if group is not None and dist.is_initialized():
+    if _is_local_group(group):
+        gid = hash(("local", group.rank)) & 0x7FFFFFFF
+    elif group is not None and dist.is_initialized():
         gid = hash(tuple(dist.get_process_group_ranks(group))) & 0x7FFFFFFF
     numel = t.numel() if t is not None else 0
     dt = _DT.get(t.dtype, 9) if t is not None else 0
@@ -63,7 +65,7 @@ def order_fingerprint() -> tuple:
 
 def verify_order(group=None) -> bool:
     """All ranks compare their collective fingerprints; raises on divergence."""
-    if not dist.is_initialized():
+    if not dist.is_initialized() or _is_local_group(group):
         return True
     mine = order_fingerprint()
     objs = [None] * dist.get_world_size(group)
@@ -71,6 +73,12 @@ def verify_order(group=None) -> bool:
     if any(o != objs[0] for o in objs):
         raise RuntimeError(f"madnn: collective order diverged across ranks: {objs}")
     return True
+
+
+def _is_local_group(group) -> bool:
+    from ..runtime import LocalGroup
+
+    return isinstance(group, LocalGroup)
 
 
 def device_kind(t: torch.Tensor) -> str:
@@ -118,7 +126,7 @@ def select(t: torch.Tensor, op: str, group=None, mode: str = "sync") -> Selected
     fn = {"all_reduce": all_reduce, "broadcast": broadcast, "all_gather": all_gather_into,
           "reduce_scatter": reduce_scatter, "send": send, "recv": recv, "barrier": None}[op]
     kind = device_kind(t)
-    if not dist.is_initialized():
+    if not dist.is_initialized() or _is_local_group(group):
         return Selected(fn or (lambda *a, **k: None), kind, "local", op, mode)
     be = dist.get_backend(group)
     if kind == "cpu" and be == "nccl":
@@ -164,7 +172,7 @@ def _local(group) -> bool:
     launched world-1 job (``torch.distributed.run --nproc-per-node 1``) issues its
     RCCL collectives exactly like the 8-GPU job does, so the communicator setup and
     the reducer's stream/event protocol run on the 1-GPU box too."""
-    if not dist.is_initialized():
+    if not dist.is_initialized() or _is_local_group(group):
         return True
     return group is not None and group is not dist.group.WORLD and dist.get_world_size(group) == 1
 

@@ -110,6 +110,8 @@ int madnn_wgrad_splits(int64_t, int64_t, int64_t);
 int madnn_gemm_tune(int, int);
 hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
                               hipStream_t);
+hipError_t madnn_hwq_wait(const int*, int, int64_t, int*, hipStream_t);
+hipError_t madnn_hwq_set(int*, int, hipStream_t);
 }
 
 namespace {
@@ -1294,9 +1296,30 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, 
           "attn_colsum");
 }
 
+// Hardware-queue aliasing probe (probe.hip): bounded flag wait / flag set on the current stream.
+void hwq_wait(const at::Tensor& flag, int64_t expect, int64_t timeout_us, at::Tensor out) {
+  check_dev(flag, "flag");
+  check_dev(out, "out");
+  TORCH_CHECK(flag.scalar_type() == at::kInt && out.scalar_type() == at::kInt && out.numel() >= 2 &&
+                  out.is_contiguous() && timeout_us > 0 && timeout_us <= 2000000,
+              "hwq_wait: int32 flag, int32 out[>=2], 0 < timeout_us <= 2 s");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(flag.device());
+  check(madnn_hwq_wait(flag.data_ptr<int>(), (int)expect, timeout_us, out.data_ptr<int>(), cur_stream(flag)),
+        "hwq_wait");
+}
+
+void hwq_set(at::Tensor flag, int64_t val) {
+  check_dev(flag, "flag");
+  TORCH_CHECK(flag.scalar_type() == at::kInt, "hwq_set: int32 flag");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(flag.device());
+  check(madnn_hwq_set(flag.data_ptr<int>(), (int)val, cur_stream(flag)), "hwq_set");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
+  m.def("hwq_wait(Tensor flag, int expect, int timeout_us, Tensor(a!) out) -> ()");
+  m.def("hwq_set(Tensor(a!) flag, int val) -> ()");
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, "
       "Tensor(c!)? nbt, bool training, float momentum, float eps, bool relu, Tensor? partial=None) -> (Tensor, Tensor, "
@@ -1416,4 +1439,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_wgrad", linear_wgrad);
   m.impl("conv3x3_fwd", conv3x3_fwd);
   m.impl("conv3x3_wgrad", conv3x3_wgrad);
+  m.impl("hwq_wait", hwq_wait);
+  m.impl("hwq_set", hwq_set);
 }

@@ -11,13 +11,16 @@ configs 3 and 4 require it.  Design for one MI355X node:
   (``madnn_pipeline_order``): GPipe, 1F1B, or interleaved 1F1B where every rank
   holds V chunks (virtual stages c*S + rank), shrinking the bubble from
   (S-1)/(M+S-1) toward (S-1)/(V*M+S-1);
-* communication is derived from that order over one-directional FIFO
-  channels, each its own process group (own RCCL communicator and stream):
-  activations r -> r+1 (ring edge S-1 -> 0 between chunks), gradients back.
-  Every receive of a step is posted up front and consumed with a stream wait,
-  sends are never waited on before the step ends, so the xGMI transfers run
-  underneath compute (``simulate_schedule`` proves each channel's receive
-  order equals its send order, which is what makes that legal);
+* communication is derived from that order (``issue_plan``): between two
+  computes ONE batched exchange with the neighbours -- the previous compute's
+  output out, the next compute's input in -- issued as a single
+  ``batch_isend_irecv`` on the replica's pipeline communicator (one RCCL kernel
+  per batch, one RCCL stream per rank for all P2P traffic).  Each rank's
+  program completes even when every GPU operation of the rank runs one at a
+  time in issue order, which is what makes it safe on MI355X, where HIP
+  multiplexes the process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues
+  that may serialise dispatches of different streams (``simulate_transport``
+  models the queues; ``scripts/hwqueue_probe.py`` measures the sharing);
 * gradients of each rank are reduced over its DP group by the bucketed
   ``DataParallel`` reducer during each chunk's LAST microbatch backward
   (``no_sync`` before) on links disjoint from the PP hops;
@@ -171,6 +174,7 @@ def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_
     SV = S * V
     orders = [native_runtime.pipeline_order(kind, s, S, M, V) for s in range(S)]
     done: Dict[tuple, float] = {}          # (op, vs, m) -> finish time
+    began: Dict[tuple, float] = {}         # (op, vs, m) -> start time
     sent: Dict[tuple, list] = {}           # channel -> list of messages in send order
     recv_seq: Dict[tuple, list] = {}       # channel -> list of messages in consume order
     pos = [0] * S
@@ -202,6 +206,7 @@ def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_
                 free[s] = start + dur
                 busy[s] += dur
                 done[(op, vs, m)] = free[s]
+                began[(op, vs, m)] = start
                 if op == "F":
                     live[s] += 1
                     peak[s] = max(peak[s], live[s])
@@ -225,58 +230,116 @@ def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_
         if recv_seq.get(ch, []) != msgs:
             raise RuntimeError(f"channel {ch}: receive order differs from send order")
     makespan = max(free)
-    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan, "peak_inflight": peak}
+    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan, "peak_inflight": peak,
+            "times": {k: (began[k], done[k]) for k in done}}
 
 
 # ----------------------------------------------------------------------------
-# channel layout (shared by build_pipeline and the transport simulation)
+# issue plan: the per-rank program of compute and batched P2P exchanges
 # ----------------------------------------------------------------------------
-def p2p_channel_specs(nstages: int, nchunks: int = 1) -> List[tuple]:
-    """The one-directional channels of one pipeline replica, in creation order, as
-    ``(name at the sender, name at the receiver, sender stage, receiver stage)``: activations
-    on every edge s -> s+1, gradients on every edge s+1 -> s, and with V > 1 the ring edge
-    (activations S-1 -> 0 between chunks, their gradients 0 -> S-1)."""
+_TIMELINE_CACHE: Dict[tuple, dict] = {}
+
+
+def _timeline(kind: str, nstages: int, nmicro: int, nchunks: int) -> dict:
+    key = (kind, nstages, nmicro, nchunks)
+    if key not in _TIMELINE_CACHE:
+        _TIMELINE_CACHE[key] = simulate_schedule(kind, nstages, nmicro, nchunks)["times"]
+    return _TIMELINE_CACHE[key]
+
+
+def issue_plan(kind: str, stage: int, nstages: int, nmicro: int, nchunks: int = 1) -> List[tuple]:
+    """The program one pipeline rank issues per step: ``("C", op, c, m)`` compute items and
+    ``("X", ops)`` point-to-point batches, ``ops`` = ``(("send"|"recv", "act"|"grad", c, m, peer
+    stage), ...)``.  The engine issues each batch as ONE ``batch_isend_irecv`` on the replica's
+    pipeline communicator (one ncclGroup: one kernel per batch) and orders the compute that
+    consumes a received tensor after it.
+
+    Construction (any compute order: GPipe, 1F1B, interleaved): the compute-only schedule
+    (:func:`simulate_schedule`, forward 1 / backward 2) gives every compute a start and a finish
+    time on one global clock.  Each message is assigned to the BOUNDARY at its producer's
+    finish time T, on both ranks: the sender issues it right after the producer, the receiver
+    in a batch placed before its first compute that starts at or after T (a compute that
+    started earlier goes first).  Messages of one rank with the same boundary share a batch; in
+    balanced 1F1B that is exactly Megatron-LM's ``send_forward_recv_backward`` /
+    ``send_backward_recv_forward`` pairing.  A batch that only receives is issued from an idle
+    side stream, so its transfer does not wait for the compute issued before it (RCCL orders a
+    kernel after all work of the stream current at issue time).
+
+    Why: every rank's program then completes even when ALL of its GPU work -- computes, these
+    batch kernels, the DP all-reduce, the tied-gradient sum -- runs one operation at a time in
+    issue order, and a send completes only together with its receive (rendezvous).  By
+    induction over the boundaries in time order, every rank reaches its batch of boundary T
+    (everything before it needs only messages of earlier boundaries), and the batches of one
+    boundary name exactly each other's messages.  HIP multiplexes a process's streams onto
+    GPU_MAX_HW_QUEUES (4) hardware queues, whose dispatches can serialise across streams
+    (``scripts/hwqueue_probe.py``); such sharing only ADDS ordering to a program that already
+    completes fully serialised, and an operation that could run stays runnable until it does,
+    so no stream-to-queue mapping can deadlock it (:func:`simulate_transport` checks
+    ``queues="serial"``, round-robin queue pools and independent queues).  The round-3 engine
+    pre-posted every receive of the step, which deadlocks as soon as one of those spinning
+    receive kernels shares a queue with the compute stream (``design="prepost"``)."""
+    S, V = nstages, nchunks
+    SV = S * V
+    order = native_runtime.pipeline_order(kind, stage, S, nmicro, V)
+    times = _timeline(kind, S, nmicro, V)
+    items: List[tuple] = []
+    batches: Dict[float, list] = {}
+    for op, c, m in order:
+        vs = c * S + stage
+        start, finish = times[(op, vs, m)]
+        items.append(((start, 1), ("C", op, c, m)))
+        if op == "F":
+            if vs > 0:
+                batches.setdefault(times[("F", vs - 1, m)][1], []).append(("recv", "act", c, m, (stage - 1) % S))
+            if vs < SV - 1:
+                batches.setdefault(finish, []).append(("send", "act", c, m, (stage + 1) % S))
+        else:
+            if vs < SV - 1:
+                batches.setdefault(times[("B", vs + 1, m)][1], []).append(("recv", "grad", c, m, (stage + 1) % S))
+            if vs > 0:
+                batches.setdefault(finish, []).append(("send", "grad", c, m, (stage - 1) % S))
+    for t, ops in batches.items():
+        items.append(((t, 0), ("X", tuple(sorted(ops, key=lambda o: (o[0] != "send", o[4], o[1]))))))
+    items.sort(key=lambda kv: kv[0])
+    return [it for _, it in items]
+
+
+def _message(d: str, kind: str, c: int, m: int, stage: int, nstages: int) -> tuple:
+    """Global identity of a P2P message: (kind, receiving virtual stage, microbatch)."""
+    vs = c * nstages + stage
+    if d == "recv":
+        return (kind, vs, m)
+    return (kind, vs + 1 if kind == "act" else vs - 1, m)
+
+
+def check_plan_fifo(kind: str, nstages: int, nmicro: int, nchunks: int = 1) -> int:
+    """Every ordered rank pair's messages are received in the order they are sent (the
+    communicator matches P2P operations of one pair FIFO).  Returns the message count; raises
+    RuntimeError on a mismatch (which would deliver one microbatch's data to another)."""
     S = nstages
-    specs = [("act_out", "act_in", e, e + 1) for e in range(S - 1)]
-    specs += [("grad_out", "grad_in", e + 1, e) for e in range(S - 1)]
-    if nchunks > 1:
-        specs += [("act_out_wrap", "act_in_wrap", S - 1, 0), ("grad_out_wrap", "grad_in_wrap", 0, S - 1)]
-    return specs
-
-
-def p2p_group_layout(nstages: int, nchunks: int, dp: int, rank_of: Callable[[int, int], int],
-                     layout: str = "pairwise") -> List[tuple]:
-    """The process groups that carry the pipeline channels, in creation order (every rank must
-    call ``new_group`` for all of them, members or not), as ``(ranks, [(replica, spec), ...])``.
-
-    ``pairwise`` (the engine's layout): ONE 2-rank group per channel, i.e. per (edge,
-    direction, replica).  On RCCL with eager initialisation an unbatched send/recv is executed
-    like a collective, in issue order with every other op on its communicator; a group with a
-    single sender and a single receiver is therefore a true FIFO whose pre-posted receives can
-    never block a send of the same rank.  ``shared`` (round-2 layout, kept only so the transport
-    tests can show that it deadlocks): one S-rank group per channel kind and replica, where an
-    interior rank's sends queue behind its own pre-posted receives."""
-    specs = p2p_channel_specs(nstages, nchunks)
-    out = []
-    if layout == "pairwise":
-        for d in range(dp):
-            for sp in specs:
-                out.append(((rank_of(d, sp[2]), rank_of(d, sp[3])), [(d, sp)]))
-    elif layout == "shared":
-        kinds = ["act", "grad"] + (["act_wrap", "grad_wrap"] if nchunks > 1 else [])
-        for kind in kinds:
-            for d in range(dp):
-                carried = [(d, sp) for sp in specs if sp[0].replace("_out", "") == kind]
-                out.append((tuple(rank_of(d, s) for s in range(nstages)), carried))
-    else:
-        raise ValueError(f"unknown pipeline channel layout {layout!r}")
-    return out
+    sent: Dict[tuple, list] = {}
+    recvd: Dict[tuple, list] = {}
+    for s in range(S):
+        for item in issue_plan(kind, s, S, nmicro, nchunks):
+            if item[0] != "X":
+                continue
+            for d, k, c, m, peer in item[1]:
+                msg = _message(d, k, c, m, s, S)
+                if d == "send":
+                    sent.setdefault((s, peer), []).append(msg)
+                else:
+                    recvd.setdefault((peer, s), []).append(msg)
+    for pair in set(sent) | set(recvd):
+        if sent.get(pair, []) != recvd.get(pair, []):
+            raise RuntimeError(f"pipeline plan {kind} S={S} M={nmicro} V={nchunks}: pair {pair} receives "
+                               f"{recvd.get(pair)} but is sent {sent.get(pair)}")
+    return sum(len(v) for v in sent.values())
 
 
 def recv_plan(order, vstages: List[int], nvirtual: int) -> List[tuple]:
-    """Every receive one pipeline rank makes in a step, in issue order: ``("act", c, m)`` before
-    the forward of virtual stage c*S+rank (unless it is the first), ``("grad", c, m)`` before the
-    backward of every virtual stage but the last.  The engine pre-posts exactly this list."""
+    """Every receive of one pipeline rank's step in issue order (``("act", c, m)`` before the
+    forward of a non-first virtual stage, ``("grad", c, m)`` before the backward of a non-last
+    one): what the round-3 engine pre-posted at step start.  Kept for the transport model."""
     out = []
     for op, c, m in order:
         vs = vstages[c]
@@ -287,219 +350,265 @@ def recv_plan(order, vstages: List[int], nvirtual: int) -> List[tuple]:
     return out
 
 
-def _chan_names(stage: int, nstages: int):
-    """This rank's channel names: (act in, act out, grad in, grad out)."""
-    return ("act_in" if stage > 0 else "act_in_wrap", "act_out" if stage < nstages - 1 else "act_out_wrap",
-            "grad_in" if stage < nstages - 1 else "grad_in_wrap", "grad_out" if stage > 0 else "grad_out_wrap")
+def rank_streams(design: str, stage: int, nstages: int, dp: int = 1, tied: bool = False,
+                 nchunks: int = 1) -> List[str]:
+    """The HIP streams one pipeline rank drives, in creation order (the order in which HIP hands
+    out hardware queues): the compute (default) stream, one RCCL stream per communicator the
+    rank uses -- WORLD from ``init_process_group``, the mesh axis groups in ``AXES`` order with
+    singleton axes skipped (the pipeline group carries the activations; with dp == 1 it is
+    WORLD), the replica's gradient group (``split``), the tied-parameter group, the round-3
+    per-channel groups (``prepost``) -- and madnn's DP comm stream."""
+    S = nstages
+    out = ["compute", "world"]
+    if dp > 1:
+        out.append("dp")
+    if dp > 1:          # with dp == 1 the pipeline group IS the world group
+        out.append("pp")
+    if design == "split":
+        out.append("p2p_grad")
+    if tied and S > 1 and stage in (0, S - 1):
+        out.append("tied")
+    if design == "prepost":
+        edges = [(e, e + 1) for e in range(S - 1)] + [(e + 1, e) for e in range(S - 1)]
+        if nchunks > 1:
+            edges += [(S - 1, 0), (0, S - 1)]
+        out += [f"chan{a}-{b}" for a, b in edges if stage in (a, b)]
+    out.append("dpcomm")
+    return out
 
 
-def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, layout: str = "pairwise",
-                       prepost: bool = True, t_fwd: float = 1.0, t_bwd: float = 2.0, t_p2p: float = 0.0) -> dict:
-    """Replay one training step of every pipeline rank against the COMMUNICATORS
-    :func:`p2p_group_layout` builds, with RCCL's eager-initialisation semantics.
+def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, design: str = "split",
+                       queues=None, dp: int = 1, tied: bool = False, first_step: bool = False,
+                       queue_offset: int = 0, t_fwd: float = 1.0, t_bwd: float = 2.0, t_p2p: float = 0.0,
+                       t_coll: float = 0.0) -> dict:
+    """Replay one training step of every rank of a ``dp x nstages`` pipeline mesh against a model
+    of the GPU's execution: every HIP stream of a rank feeds a hardware queue, and a queue runs
+    its operations ONE AT A TIME in submission order (a compute kernel for ``t_fwd``/``t_bwd``, an
+    event wait blocks the queue until its event, a communication kernel occupies the queue until
+    it completes).
 
-    Model: each rank has a compute stream and one stream per communicator it belongs to; all of
-    a rank's operations on one communicator execute in issue order (unbatched P2P is serialised
-    like a collective).  The host issues, in program order, the receives of :func:`recv_plan`
-    (all up front when ``prepost``; otherwise each right before its consumer, preceded by the
-    shape header that the first step of a new input signature exchanges with a host-blocking
-    receive), every forward/backward on the compute stream (waiting on its receive), and each
-    send on its channel's communicator right after its producer.  A send completes only
-    together with the matching receive at the head of the peer's stream (rendezvous, the
-    conservative reading of RCCL's P2P protocol).  Raises RuntimeError on a deadlock or when a
-    receive would be matched with a message meant for another receive; otherwise returns
-    ``{"makespan", "bubble", "communicators"}``."""
+    ``queues``: ``None`` -- every stream its own queue; ``"serial"`` -- one queue per rank (every
+    operation of the rank serialised: the strongest constraint); an int Q -- stream i of
+    :func:`rank_streams` (creation order) on queue ``(i + queue_offset) % Q``, the round-robin
+    assignment HIP uses for a pool of Q hardware queues.
+
+    Communication follows RCCL: a batch kernel moves each of its messages once the matching
+    kernel on the peer is running too (rendezvous; the batch completes with its last message);
+    a collective completes once every member runs it; a kernel issued while a stream with
+    pending work is current waits for that work (ProcessGroupNCCL's stream sync).
+    ``design``: ``"split"`` is the engine (:func:`issue_plan`; each batch's activation part on
+    the replica's pipeline communicator and its gradient part on a second one; a part that only
+    receives is issued from an idle side stream, one that sends after the producing compute;
+    the consumer waits for its part; the DP all-reduce of each chunk's buckets on the dp
+    communicator during its last microbatch backward; the tied-gradient sum between the first
+    and last stage after the step); ``"batched"`` is the same plan on ONE communicator;
+    ``"prepost"`` is the round-3 engine (one 2-rank communicator per channel, every receive of
+    the step posted up front).  ``first_step`` adds the shape headers a new input signature
+    exchanges (host-blocking).
+
+    Raises RuntimeError on a deadlock (naming every stuck queue head) or a FIFO mismatch;
+    returns ``{"makespan", "bubble", "ops", "queues"}``."""
     S, M, V = nstages, nmicro, nchunks
     SV = S * V
-    groups = p2p_group_layout(S, V, 1, lambda d, s: s, layout)
-    comm_of: Dict[tuple, int] = {}
-    for gi, (_ranks, carried) in enumerate(groups):
-        for _d, (n_src, n_dst, a, b) in carried:
-            comm_of[(a, n_src)] = gi
-            comm_of[(b, n_dst)] = gi
-    ops: List[dict] = []           # every op: kind C/S/R, rank, stream, deps, payload
+    if design not in ("batched", "split", "prepost"):
+        raise ValueError(f"unknown transport design {design!r}")
+    ranks = [(d, s) for d in range(dp) for s in range(S)]
+    rid = {r: i for i, r in enumerate(ranks)}
+    ops: List[dict] = []
+    programs: List[list] = []
+    streams = [rank_streams(design, s, S, dp, tied, V) for (_d, s) in ranks]
+    pstream = "pp" if dp > 1 else "world"   # with dp == 1 the pipeline group is the world group
 
-    def new(kind_, rank, stream, **kw):
-        ops.append(dict(kind=kind_, rank=rank, stream=stream, done=None, **kw))
+    def new(kind_, r, stream, deps=(), **kw):
+        ops.append(dict(kind=kind_, rank=r, stream=stream, deps=[x for x in deps if x is not None], start=None,
+                        done=None, **kw))
         return len(ops) - 1
 
-    programs = []                  # per rank: list of ("issue", op id) / ("hostwait", op id)
-    for s in range(S):
-        order = native_runtime.pipeline_order(kind, s, S, M, V)
-        vst = [virtual_stage(c, s, S) for c in range(V)]
-        a_in, a_out, g_in, g_out = _chan_names(s, S)
+    sends: Dict[tuple, list] = {}   # (src, dst) -> [(op id, message)] in issue order
+    recvs: Dict[tuple, list] = {}
+
+    def xfer(oid, d, k, c, m, s, peer_stage, r, drep):
+        msg = _message(d, k, c, m, s, S) if k in ("act", "grad") else (k, c, m)
+        peer = rid[(drep, peer_stage)]
+        if d == "send":
+            sends.setdefault((r, peer), []).append((oid, msg))
+        else:
+            recvs.setdefault((peer, r), []).append((oid, msg))
+
+    for (d, s) in ranks:
+        r = rid[(d, s)]
         prog = []
-        recv_id: Dict[tuple, int] = {}
-        met_in, met_out = set(), set()
-
-        def post(key, s=s, a_in=a_in, g_in=g_in, vst=vst, recv_id=recv_id, prog=prog):
-            k, c, m = key
-            name = a_in if k == "act" else g_in
-            peer = (s - 1) % S if k == "act" else (s + 1) % S
-            msg = (k, vst[c], m)
-            recv_id[key] = new("R", s, ("comm", comm_of[(s, name)]), peer=peer, msg=msg)
-            prog.append(("issue", recv_id[key]))
-
-        if prepost:
-            for key in recv_plan(order, vst, SV):
-                post(key)
-        for op, c, m in order:
-            vs = vst[c]
-            dep = None
-            if op == "F" and vs > 0 or op == "B" and vs < SV - 1:
-                key = ("act" if op == "F" else "grad", c, m)
-                if not prepost:
-                    if op == "F" and c not in met_in:   # shape header, host-blocking
-                        met_in.add(c)
-                        h = new("R", s, ("comm", comm_of[(s, a_in)]), peer=(s - 1) % S, msg=("hdr", vs, c))
-                        prog.append(("issue", h))
-                        prog.append(("hostwait", h))
-                    post(key)
-                dep = recv_id[key]
-            cid = new("C", s, ("compute",), dep=dep, dur=t_fwd if op == "F" else t_bwd)
-            prog.append(("issue", cid))
-            if op == "F" and vs < SV - 1:
-                if not prepost and c not in met_out:
-                    met_out.add(c)
-                    prog.append(("issue", new("S", s, ("comm", comm_of[(s, a_out)]), peer=(s + 1) % S,
-                                              msg=("hdr", vs + 1, (vs + 1) // S), dep=cid)))
-                prog.append(("issue", new("S", s, ("comm", comm_of[(s, a_out)]), peer=(s + 1) % S,
-                                          msg=("act", vs + 1, m), dep=cid)))
-            elif op == "B" and vs > 0:
-                prog.append(("issue", new("S", s, ("comm", comm_of[(s, g_out)]), peer=(s - 1) % S,
-                                          msg=("grad", vs - 1, m), dep=cid)))
+        if design in ("batched", "split"):
+            last_c = None
+            need = None
+            met_in, met_out = set(), set()
+            for item in issue_plan(kind, s, S, M, V):
+                if item[0] == "X":
+                    batch = item[1]
+                    if first_step:
+                        hdr = [(dd, k, c, m, p) for dd, k, c, m, p in batch if k == "act" and
+                               ((dd == "recv" and c not in met_in) or (dd == "send" and c not in met_out))]
+                        if hdr:
+                            h = new("X", r, pstream, [last_c])
+                            for dd, k, c, m, p in hdr:
+                                (met_in if dd == "recv" else met_out).add(c)
+                                xfer(h, dd, "hdr", _message(dd, k, c, m, s, S)[1], m, s, p, r, d)
+                            prog += [("issue", h), ("hostwait", h)]
+                    if design == "batched":
+                        parts = [(pstream, batch)]
+                    else:                  # the engine: activations and gradients on two communicators
+                        parts = [(pstream if k == "act" else "p2p_grad", tuple(o for o in batch if o[1] == k))
+                                 for k in ("act", "grad")]
+                    for stream_name, part in parts:
+                        if not part:
+                            continue
+                        has_send = any(o[0] == "send" for o in part)
+                        x = new("X", r, stream_name, [last_c] if has_send else [], desc=part)
+                        for dd, k, c, m, p in part:
+                            xfer(x, dd, k, c, m, s, p, r, d)
+                        prog.append(("issue", x))
+                        if any(dd == "recv" for dd, *_ in part):
+                            need = x
+                else:
+                    _, op, c, m = item
+                    vs = c * S + s
+                    takes = (op == "F" and vs > 0) or (op == "B" and vs < SV - 1)
+                    last_c = new("C", r, "compute", [need] if takes else [], dur=t_fwd if op == "F" else t_bwd,
+                                 desc=(op, c, m))
+                    prog.append(("issue", last_c))
+                    if takes:
+                        need = None
+                    if op == "B" and m == M - 1 and dp > 1:
+                        a = new("A", r, "dp", [last_c], key=("dp", s, c), members=[rid[(e, s)] for e in range(dp)])
+                        prog.append(("issue", a))
+            if tied and S > 1 and s in (0, S - 1):
+                a = new("A", r, "tied", [last_c], key=("tied", d), members=[rid[(d, 0)], rid[(d, S - 1)]])
+                prog.append(("issue", a))
+        else:  # prepost: the round-3 engine
+            order = native_runtime.pipeline_order(kind, s, S, M, V)
+            vst = [virtual_stage(c, s, S) for c in range(V)]
+            rec = {}
+            for k, c, m in recv_plan(order, vst, SV):
+                peer = (s - 1) % S if k == "act" else (s + 1) % S
+                oid = new("X", r, f"chan{peer}-{s}")
+                xfer(oid, "recv", k, c, m, s, peer, r, d)
+                rec[(k, c, m)] = oid
+                prog.append(("issue", oid))
+            last_c = None
+            for op, c, m in order:
+                vs = vst[c]
+                key = ("act", c, m) if op == "F" and vs > 0 else (("grad", c, m) if op == "B" and vs < SV - 1 else None)
+                last_c = new("C", r, "compute", [rec[key]] if key else [], dur=t_fwd if op == "F" else t_bwd)
+                prog.append(("issue", last_c))
+                if op == "F" and vs < SV - 1:
+                    peer = (s + 1) % S
+                    oid = new("X", r, f"chan{s}-{peer}", [last_c])
+                    xfer(oid, "send", "act", c, m, s, peer, r, d)
+                    prog.append(("issue", oid))
+                elif op == "B" and vs > 0:
+                    peer = (s - 1) % S
+                    oid = new("X", r, f"chan{s}-{peer}", [last_c])
+                    xfer(oid, "send", "grad", c, m, s, peer, r, d)
+                    prog.append(("issue", oid))
+                if op == "B" and m == M - 1 and dp > 1:
+                    prog.append(("issue", new("A", r, "dp", [last_c], key=("dp", s, c),
+                                              members=[rid[(e, s)] for e in range(dp)])))
+            if tied and S > 1 and s in (0, S - 1):
+                prog.append(("issue", new("A", r, "tied", [last_c], key=("tied", d),
+                                          members=[rid[(d, 0)], rid[(d, S - 1)]])))
         programs.append(prog)
 
-    pc = [0] * S
-    queues: Dict[tuple, list] = {}   # (rank, stream) -> op ids in issue order (FIFO)
-    free: Dict[tuple, float] = {}
-    busy = [0.0] * S
+    # pair the k-th send of every ordered rank pair with the k-th receive (communicator FIFO)
+    xfers: List[list] = []          # transfer id -> [sender op, receiver op]
+    for pair in set(sends) | set(recvs):
+        a, b = sends.get(pair, []), recvs.get(pair, [])
+        if [msg for _, msg in a] != [msg for _, msg in b]:
+            raise RuntimeError(f"transport {design} {kind} S={S} M={M} V={V}: pair {pair} sends "
+                               f"{[msg for _, msg in a]} but receives {[msg for _, msg in b]}")
+        for (so, _), (ro, _) in zip(a, b):
+            tid = len(xfers)
+            xfers.append([so, ro])
+            ops[so].setdefault("xfers", []).append(tid)
+            ops[ro].setdefault("xfers", []).append(tid)
+    xdone: Dict[int, float] = {}
+    coll: Dict[tuple, list] = {}
+    for i, o in enumerate(ops):
+        if o["kind"] == "A":
+            coll.setdefault(o["key"], []).append(i)
+
+    def qid(r, stream):
+        if queues is None:
+            return stream
+        if queues == "serial":
+            return 0
+        return (streams[r].index(stream) + queue_offset) % int(queues)
+
+    pc = [0] * len(ranks)
+    fifo: Dict[tuple, list] = {}
+    qfree: Dict[tuple, float] = {}
+    busy = [0.0] * len(ranks)
     remaining = len(ops)
-
-    def head(rank, stream):
-        q = queues.get((rank, stream))
-        return q[0] if q else None
-
     while remaining:
         progressed = False
-        for s in range(S):               # the host issues until it reaches an unfinished wait
-            prog = programs[s]
-            while pc[s] < len(prog):
-                what, oid = prog[pc[s]]
+        for r, prog in enumerate(programs):        # the host issues until an unfinished host wait
+            while pc[r] < len(prog):
+                what, oid = prog[pc[r]]
                 if what == "hostwait":
                     if ops[oid]["done"] is None:
                         break
                 else:
-                    queues.setdefault((s, ops[oid]["stream"]), []).append(oid)
-                pc[s] += 1
+                    fifo.setdefault((r, qid(r, ops[oid]["stream"])), []).append(oid)
+                pc[r] += 1
                 progressed = True
-        for (s, stream), q in list(queues.items()):
-            while q:
-                o = ops[q[0]]
-                if o["kind"] == "C":
-                    if o["dep"] is not None and ops[o["dep"]]["done"] is None:
-                        break
-                    start = max(free.get((s, stream), 0.0), ops[o["dep"]]["done"] if o["dep"] is not None else 0.0)
-                    o["done"] = start + o["dur"]
-                    busy[s] += o["dur"]
-                elif o["kind"] == "S":
-                    if ops[o["dep"]]["done"] is None:
-                        break
-                    ph = head(o["peer"], stream)
-                    if ph is None or ops[ph]["kind"] != "R" or ops[ph]["peer"] != s:
-                        break
-                    r = ops[ph]
-                    if r["msg"] != o["msg"]:
-                        raise RuntimeError(f"transport {layout} {kind} S={S} M={M} V={V}: rank {o['peer']} "
-                                           f"receives {o['msg']} where it expects {r['msg']}")
-                    start = max(free.get((s, stream), 0.0), free.get((o["peer"], stream), 0.0),
-                                ops[o["dep"]]["done"])
-                    o["done"] = r["done"] = start + t_p2p
-                    free[(o["peer"], stream)] = r["done"]
-                    queues[(o["peer"], stream)].pop(0)
-                    remaining -= 1
-                else:
-                    break                # a receive completes with its matching send
-                free[(s, stream)] = o["done"]
-                q.pop(0)
+        for q, lst in fifo.items():
+            while lst:
+                o = ops[lst[0]]
+                if o["done"] is None:
+                    if o["start"] is None:
+                        if any(ops[x]["done"] is None for x in o["deps"]):
+                            break
+                        o["start"] = max([qfree.get(q, 0.0)] + [ops[x]["done"] for x in o["deps"]])
+                        progressed = True
+                    if o["kind"] == "C":
+                        o["done"] = o["start"] + o["dur"]
+                        busy[o["rank"]] += o["dur"]
+                    elif o["kind"] == "X":
+                        for tid in o.get("xfers", []):
+                            if tid in xdone:
+                                continue
+                            other = ops[xfers[tid][0] if xfers[tid][1] == lst[0] else xfers[tid][1]]
+                            if other["start"] is not None:
+                                xdone[tid] = max(o["start"], other["start"]) + t_p2p
+                        if any(tid not in xdone for tid in o.get("xfers", [])):
+                            break
+                        o["done"] = max([o["start"]] + [xdone[t] for t in o.get("xfers", [])])
+                    else:
+                        members = [ops[x] for x in coll[o["key"]]]
+                        if any(mo["start"] is None for mo in members):
+                            break
+                        end = max(mo["start"] for mo in members) + t_coll
+                        for mo in members:
+                            mo["done"] = end
+                qfree[q] = o["done"]
+                lst.pop(0)
                 remaining -= 1
                 progressed = True
         if not progressed:
-            stuck = {}
-            for (s, stream), q in queues.items():
-                if q:
-                    o = ops[q[0]]
-                    stuck.setdefault(s, []).append((stream, o["kind"], o.get("msg")))
-            raise RuntimeError(f"pipeline transport {layout} {kind} S={S} M={M} V={V} deadlocks; "
-                               f"stream heads: {stuck}")
+            heads = {}
+            for (r, q), lst in fifo.items():
+                if lst:
+                    o = ops[lst[0]]
+                    heads.setdefault(ranks[r], []).append((q, o["stream"], o["kind"], o.get("key") or o.get("desc")))
+            raise RuntimeError(f"pipeline transport {design} {kind} S={S} M={M} V={V} dp={dp} queues={queues} "
+                               f"deadlocks; queue heads: {heads}")
     makespan = max(o["done"] for o in ops)
-    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan if makespan else 0.0,
-            "communicators": len(groups)}
+    return {"makespan": makespan, "bubble": 1.0 - max(busy) / makespan if makespan else 0.0, "ops": len(ops),
+            "queues": queues}
 
 
 # ----------------------------------------------------------------------------
 # transport
 # ----------------------------------------------------------------------------
-class _SerialWork:
-    """Completion handle of an op run by :class:`_SerialComm` (wait() raises on a timeout)."""
-
-    __slots__ = ("event", "error", "timeout")
-
-    def __init__(self, timeout):
-        import threading
-
-        self.event = threading.Event()
-        self.error = None
-        self.timeout = timeout
-
-    def wait(self):
-        if not self.event.wait(self.timeout):
-            raise RuntimeError(f"emulated RCCL P2P: operation not complete after {self.timeout:.0f} s "
-                               "(the communicator's FIFO is blocked: transport deadlock)")
-        if self.error is not None:
-            raise self.error
-        return True
-
-
-class _SerialComm:
-    """CPU test double of an eagerly initialised RCCL communicator: every point-to-point
-    operation on the group runs to completion, one at a time, in issue order, on one worker
-    thread (``MADNN_EMULATE_RCCL_P2P=1`` on gloo).  Gloo alone completes sends and receives of
-    different peers independently, which hides the serialisation RCCL imposes."""
-
-    _by_group: Dict[int, "_SerialComm"] = {}
-
-    def __init__(self, timeout):
-        import queue
-        import threading
-
-        self.q = queue.Queue()
-        self.timeout = timeout
-        self.thread = threading.Thread(target=self._run, daemon=True)
-        self.thread.start()
-
-    @classmethod
-    def of(cls, group, timeout):
-        c = cls._by_group.get(id(group))
-        if c is None:
-            c = cls._by_group[id(group)] = cls(timeout)
-        return c
-
-    def _run(self):
-        while True:
-            fn, work = self.q.get()
-            try:
-                fn().wait()
-            except Exception as e:  # noqa: BLE001
-                work.error = e
-            work.event.set()
-
-    def submit(self, fn) -> _SerialWork:
-        w = _SerialWork(self.timeout)
-        self.q.put((fn, w))
-        return w
-
-
 def _emulated_p2p_timeout() -> Optional[float]:
     import os
 
@@ -507,85 +616,170 @@ def _emulated_p2p_timeout() -> Optional[float]:
     if v in ("", "0"):
         return None
     return float(os.environ.get("MADNN_EMULATE_RCCL_P2P_TIMEOUT", "60"))
-class _Pending:
-    """A posted receive; ``get()`` orders the consumer after it (RCCL: a stream wait, no
-    host block) and returns the tensor on the compute device."""
-
-    __slots__ = ("work", "buf", "device", "staged")
-
-    def __init__(self, work, buf, device, staged):
-        self.work, self.buf, self.device, self.staged = work, buf, device, staged
-
-    def get(self) -> torch.Tensor:
-        self.work.wait()
-        return self.buf.to(self.device, non_blocking=False) if self.staged else self.buf
 
 
-class Channel:
-    """One-directional point-to-point FIFO between two pipeline ranks.
+class P2PTransport:
+    """The point-to-point exchanges of one pipeline replica on TWO communicators: activations on
+    the replica's pipeline group (WORLD when dp == 1), gradients on a second group over the same
+    ranks -- so in 1F1B's steady state the gradient a rank waits for never queues behind the
+    activation it just sent (``simulate_transport``: ``split`` vs ``batched``).
 
-    Its process group has exactly two ranks, the sender and the receiver
-    (:func:`p2p_group_layout`), so its RCCL communicator -- which executes unbatched
-    send/recv in issue order on its own HIP stream -- only ever carries messages one way and
-    in one order: receives can be posted ahead of time (the transfer runs as soon as the
-    peer's send is enqueued, overlapping this rank's compute) and sends are never waited on
-    before the end of the step.  On a gloo group HIP tensors are staged through host memory
-    (tests run several ranks on one GPU that way; RCCL refuses that); with
-    ``MADNN_EMULATE_RCCL_P2P=1`` gloo ops run through :class:`_SerialComm`, which imposes
-    RCCL's per-communicator serialisation on the CPU tests."""
+    :meth:`exchange` issues one :func:`issue_plan` batch: per kind one ``batch_isend_irecv``
+    (on RCCL one ncclGroup: one kernel moving every message of that part, whichever peer it
+    goes to).  A part that sends is issued on the current (compute) stream, after the producer;
+    a part that only receives is issued from an idle side stream, so its kernel does not wait
+    for the compute issued before it and the transfer overlaps that compute.  The current
+    stream is then ordered after every part that received (a stream wait, no host block);
+    send-only parts are waited for at the end of the step (:meth:`drain`).
 
-    def __init__(self, group, src: int, dst: int, device, name: str = ""):
-        self.group, self.src, self.dst, self.name = group, src, dst, name
+    On a gloo group HIP tensors are staged through host memory (several ranks on one GPU in
+    tests; RCCL refuses that).  ``MADNN_EMULATE_RCCL_P2P=1`` makes the CPU tests execute every
+    part the way the strongest hardware-queue model does (``simulate_transport`` with
+    ``queues="serial"``): the part first rendezvouses with every peer it names (a token
+    exchange), then moves its data, and the host waits for it -- one operation at a time per
+    rank; a wait that outlasts ``MADNN_EMULATE_RCCL_P2P_TIMEOUT`` is reported as a transport
+    deadlock."""
+
+    def __init__(self, act_group, grad_group, stage_ranks: List[int], device):
+        self.groups = {"act": act_group, "grad": grad_group}
+        self.stage_ranks = list(stage_ranks)
         self.device = torch.device(device)
-        backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        backend = dist.get_backend(act_group) if dist.is_initialized() else "gloo"
         self.staged = backend == "gloo" and self.device.type == "cuda"
         self.buf_device = torch.device("cpu") if self.staged else self.device
-        t = _emulated_p2p_timeout() if backend == "gloo" else None
-        self.serial = _SerialComm.of(group, t) if t is not None else None
-        self._sends = []
+        self.emulate = _emulated_p2p_timeout() if backend == "gloo" else None
+        self.side = torch.cuda.Stream(self.device) if backend == "nccl" and self.device.type == "cuda" else None
+        self._inflight = []        # (works, tensors kept alive) of send-only parts not waited for yet
+        self._keep = []            # sent tensors of parts already waited for (alive until drain)
+        self._seq: Dict[tuple, int] = {}   # emulation: per (kind, direction, peer) message count
         self.bytes = 0
         self.messages = 0
+        self.batches = 0
 
-    def _isend(self, t):
-        if self.serial is not None:
-            return self.serial.submit(lambda: dist.isend(t, self.dst, group=self.group))
-        return dist.isend(t, self.dst, group=self.group)
+    def _wait(self, works):
+        if self.emulate is None:
+            for w in works:
+                w.wait()
+            return
+        import datetime
 
-    def _irecv(self, buf):
-        if self.serial is not None:
-            return self.serial.submit(lambda: dist.irecv(buf, self.src, group=self.group))
-        return dist.irecv(buf, self.src, group=self.group)
+        for w in works:
+            try:
+                ok = w.wait(timeout=datetime.timedelta(seconds=self.emulate))
+            except RuntimeError as e:
+                raise RuntimeError(f"emulated RCCL P2P: batch not complete after {self.emulate:.0f} s "
+                                   f"(transport deadlock): {e}") from e
+            if ok is False:
+                raise RuntimeError(f"emulated RCCL P2P: batch not complete after {self.emulate:.0f} s "
+                                   "(transport deadlock)")
 
-    def send(self, t: torch.Tensor) -> None:
-        t = t.detach().contiguous()
-        if self.staged:
-            t = t.cpu()
-        comm._record("send", self.group, t)
-        self._sends.append((self._isend(t), t))
-        self.bytes += t.numel() * t.element_size()
-        self.messages += 1
+    def exchange(self, sends, recvs, kind: str = "act") -> List[torch.Tensor]:
+        """One part on the ``kind`` communicator: ``sends`` = [(tensor, peer stage)], ``recvs`` =
+        [(shape, dtype, peer stage)].  Returns the received tensors on the compute device,
+        ordered after the part."""
+        group = self.groups[kind]
+        ops, keep, bufs = [], [], []
+        for t, peer in sends:
+            t = t.detach().contiguous()
+            if self.staged:
+                t = t.cpu()
+            keep.append(t)
+            comm._record("send", group, t)
+            ops.append(dist.P2POp(dist.isend, t, self.stage_ranks[peer], group))
+            self.bytes += t.numel() * t.element_size()
+            self.messages += 1
+        for shape, dtype, peer in recvs:
+            b = torch.empty(shape, dtype=dtype, device=self.buf_device)   # on the compute stream
+            comm._record("recv", group, b)
+            bufs.append(b)
+            ops.append(dist.P2POp(dist.irecv, b, self.stage_ranks[peer], group))
+        if not ops:
+            return []
+        self.batches += 1
+        if self.emulate is not None:
+            self._rendezvous(kind, group, [p for _, p in sends], [p for *_, p in recvs])
+            self._wait(dist.batch_isend_irecv(ops))
+        else:
+            if self.side is not None and not sends:
+                # receive only: issue from the idle side stream (no wait on the compute queued so far)
+                with torch.cuda.stream(self.side):
+                    works = dist.batch_isend_irecv(ops)
+            else:
+                works = dist.batch_isend_irecv(ops)
+            if bufs:
+                self._wait(works)      # RCCL: the current stream waits for the part's kernel
+                if keep:
+                    self._keep.append(keep)
+            else:
+                # never wait twice: a second wait on a finished gloo receive blocks for a new one
+                self._inflight.append((works, keep))
+        return [b.to(self.device, non_blocking=False) if self.staged else b for b in bufs]
 
-    def post_recv(self, shape, dtype) -> _Pending:
-        buf = torch.empty(shape, dtype=dtype, device=self.buf_device)
-        comm._record("recv", self.group, buf)
-        return _Pending(self._irecv(buf), buf, self.device, self.staged)
+    def exchange_batch(self, sends, recvs) -> List[torch.Tensor]:
+        """A whole :func:`issue_plan` batch: ``sends`` = [(kind, tensor, peer)], ``recvs`` =
+        [(kind, shape, dtype, peer)]; the activation part first, then the gradient part (the
+        order :func:`simulate_transport` verifies).  Returns the received tensors in ``recvs``
+        order."""
+        out = {}
+        for kind in ("act", "grad"):
+            idx = [i for i, r in enumerate(recvs) if r[0] == kind]
+            got = self.exchange([(t, p) for k, t, p in sends if k == kind],
+                                [recvs[i][1:] for i in idx], kind)
+            out.update(zip(idx, got))
+        return [out[i] for i in range(len(recvs))]
 
-    def send_meta(self, t: torch.Tensor) -> None:
-        hdr = torch.zeros(10, dtype=torch.int64)
-        hdr[0] = t.dim()
-        hdr[1] = _DT_CODE[t.dtype]
-        hdr[2:2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
-        self.send(hdr.to(self.buf_device))
+    def _rendezvous(self, kind, group, send_peers, recv_peers):
+        """Emulation only: meet every peer of this part and check that the peer's current part
+        carries exactly the complementary messages (by per-pair FIFO sequence number) -- the
+        condition for an RCCL batch kernel to finish while both ranks run one operation at a
+        time.  A mismatch is the deadlock the real transport would hang in; it raises here."""
+        me = self.stage_ranks.index(dist.get_rank()) if dist.get_rank() in self.stage_ranks else -1
+        mine: Dict[int, list] = {}
+        for p in send_peers:
+            k = self._seq.get((kind, "s", p), 0)
+            self._seq[(kind, "s", p)] = k + 1
+            mine.setdefault(p, []).append((me, p, k))
+        for p in recv_peers:
+            k = self._seq.get((kind, "r", p), 0)
+            self._seq[(kind, "r", p)] = k + 1
+            mine.setdefault(p, []).append((p, me, k))
+        peers = sorted(mine)
+        tok = [torch.tensor([hash(tuple(sorted(mine[p]))) & 0x7FFFFFFFFFFF], dtype=torch.int64) for p in peers]
+        got = [torch.zeros(1, dtype=torch.int64) for _ in peers]
+        ops = []
+        for p, t, g in zip(peers, tok, got):
+            ops.append(dist.P2POp(dist.isend, t, self.stage_ranks[p], group))
+            ops.append(dist.P2POp(dist.irecv, g, self.stage_ranks[p], group))
+        self._wait(dist.batch_isend_irecv(ops))
+        for p, t, g in zip(peers, tok, got):
+            if int(t) != int(g):
+                raise RuntimeError(f"emulated RCCL P2P: transport deadlock: stage {me} and stage {p} are in "
+                                   f"different {kind} batches (this side moves {sorted(mine[p])})")
 
-    def recv_meta(self):
-        h = self.post_recv((10,), torch.int64).get().tolist()
-        return tuple(int(v) for v in h[2:2 + h[0]]), _CODE_DT[h[1]]
+    def exchange_meta(self, sends, recv_peers) -> List[tuple]:
+        """Activation shape headers for the first step of an input signature: ``sends`` =
+        [(tensor, peer stage)] announce their shape/dtype; returns ``(shape, dtype)`` per entry of
+        ``recv_peers``.  Host-blocking (the receiver must size its buffer)."""
+        hdrs = []
+        for t, peer in sends:
+            h = torch.zeros(10, dtype=torch.int64)
+            h[0] = t.dim()
+            h[1] = _DT_CODE[t.dtype]
+            h[2:2 + t.dim()] = torch.tensor(t.shape, dtype=torch.int64)
+            hdrs.append((h.to(self.buf_device), peer))
+        got = self.exchange(hdrs, [((10,), torch.int64, p) for p in recv_peers], "act")
+        out = []
+        for g in got:
+            v = g.tolist()
+            out.append((tuple(int(x) for x in v[2:2 + v[0]]), _CODE_DT[v[1]]))
+        return out
 
     def drain(self) -> None:
-        """Wait for (RCCL: order the current stream after) every send of this step."""
-        for w, _ in self._sends:
-            w.wait()
-        self._sends.clear()
+        """Order the current stream after every part of this step (RCCL) / wait for them (gloo)."""
+        for works, _keep in self._inflight:
+            self._wait(works)
+        self._inflight.clear()
+        self._keep.clear()
 
 
 # ----------------------------------------------------------------------------
@@ -606,17 +800,18 @@ class PipelineEngine:
     """Runs one pipeline rank of a (dp x pp) mesh; ``train_step`` = fwd + bwd of all microbatches.
 
     The compute order comes from the C++ scheduler (GPipe, 1F1B or interleaved 1F1B with V
-    chunks per rank); all communication is derived from it: the activation input of every
-    non-first virtual stage arrives on the ``act`` channel from the previous rank (the ring
-    edge S-1 -> 0 between chunks), gradients flow back on the ``grad`` channels.  In steady
-    state every receive of the step is posted up front (shapes are known from the first step
-    of an input signature, which exchanges headers just in time), so each transfer overlaps
-    the compute that precedes its consumer; sends are fire-and-forget until the step ends."""
+    chunks per rank) and the rank executes :func:`issue_plan` of it: between two computes, one
+    batched exchange with the neighbours (the activation of the previous forward out, the input
+    of the next compute in), on the replica's pipeline communicator (the ring edge S-1 -> 0
+    carries activations between chunks when V > 1).  Every program is deadlock-free even fully
+    serialised, so no sharing of the GPU's hardware queues between its streams can stall it
+    (:func:`simulate_transport`).  The first step of an input signature exchanges shape headers
+    just before the data batches that need them."""
 
     def __init__(self, stage_module: PipelineStage, *, stage: int, nstages: int, groups: rt.ProcessGroups,
                  microbatches: int, schedule: str, loss_fn: Callable, dp_engine: DataParallel,
                  cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=(),
-                 channels: Optional[Dict[str, Channel]] = None, p2p_groups=()):
+                 transport: Optional[P2PTransport] = None):
         self.module = stage_module
         self.chunks = list(stage_module.chunks)
         self.V = len(self.chunks)
@@ -632,32 +827,36 @@ class PipelineEngine:
         self.tied = tied                      # [(param, group, first owner's global rank)] on this rank
         self.param_names = param_names
         self.buffer_refs = list(buffer_refs)   # (original name, owner module, local name)
-        self.channels = channels or {}
+        self.transport = transport
         self.order = native_runtime.pipeline_order(schedule, stage, nstages, microbatches, self.V)
+        self.plan_items = issue_plan(schedule, stage, nstages, microbatches, self.V)
         S, SV = nstages, nstages * self.V
         self._vs = [virtual_stage(c, stage, S) for c in range(self.V)]
         self.holds_first = 0 in self._vs
         self.holds_last = (SV - 1) in self._vs
         dev = rt.device()
-        # A collective over every group first: each RCCL communicator exists before its first
-        # point-to-point operation.
+        # A collective over every group first: each RCCL communicator exists (and has run a
+        # collective, which RCCL requires before a batch naming only some of its ranks) before
+        # the first point-to-point batch.
         if dist.is_initialized():
             probe = torch.zeros(1, device=dev)
             seen = set()
-            for g in [groups.pp_group, groups.dp_group] + list(p2p_groups):
+            extra = [transport.groups["grad"]] if transport is not None else []
+            for g in [groups.pp_group, groups.dp_group] + extra:
                 if id(g) not in seen:
                     seen.add(id(g))
                     comm.all_reduce(probe, "sum", group=g)
             for _, g, _ in tied:
                 comm.all_reduce(probe, "sum", group=g)
-            self._warm_channels()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
         self._sig = _UNSET
         self._in_meta: Dict[int, tuple] = {}    # chunk -> (shape, dtype) of its received activation
         self._out_meta: Dict[int, tuple] = {}   # chunk -> (shape, dtype) of its sent activation
         self._tied_works = []
         self._needs_tied = False
         self.last_loss = None
-        self.stats = {"steps": 0, "prefetched_recvs": 0}
+        self.stats = {"steps": 0, "p2p_batches": 0}
 
     @property
     def is_first(self):
@@ -666,52 +865,6 @@ class PipelineEngine:
     @property
     def is_last(self):
         return self.stage == self.nstages - 1
-
-    # ------------------------------------------------------------ channels
-    def _warm_channels(self):
-        """Create every channel's point-to-point communicator before the first step.
-
-        RCCL builds a two-rank communicator on a pair's first send/recv and that build is a
-        blocking rendezvous of the two ranks.  Doing it lazily inside the schedule would turn
-        the first message of every channel into a synchronous handshake (the schedule is only
-        proven deadlock-free for non-blocking sends); here every rank walks its channels in
-        the global group-creation order (then edge index inside a group), so the handshakes
-        form a chain that always completes."""
-        ranked = sorted(self.channels, key=lambda n: getattr(self.channels[n], "warm_key", (0, 0)))
-        for name in ranked:
-            ch = self.channels[name]
-            t = torch.zeros(1, device=ch.buf_device)
-            if name.endswith("_out") or name.endswith("_out_wrap"):
-                dist.isend(t, ch.dst, group=ch.group).wait()
-            else:
-                dist.irecv(t, ch.src, group=ch.group).wait()
-        if self.channels and torch.cuda.is_available() and rt.device().type == "cuda":
-            torch.cuda.synchronize()
-
-    def _act_in(self, c: int) -> Channel:
-        return self.channels["act_in" if self.stage > 0 else "act_in_wrap"]
-
-    def _act_out(self, c: int) -> Channel:
-        return self.channels["act_out" if self.stage < self.nstages - 1 else "act_out_wrap"]
-
-    def _grad_in(self, c: int) -> Channel:
-        return self.channels["grad_in" if self.stage < self.nstages - 1 else "grad_in_wrap"]
-
-    def _grad_out(self, c: int) -> Channel:
-        return self.channels["grad_out" if self.stage > 0 else "grad_out_wrap"]
-
-    def _prepost(self):
-        """Post every receive of the step (:func:`recv_plan`, the order
-        :func:`simulate_transport` proves deadlock-free on the channel groups)."""
-        q = {}
-        for key in recv_plan(self.order, self._vs, self.nstages * self.V):
-            k, c, _m = key
-            if k == "act":
-                q[key] = self._act_in(c).post_recv(*self._in_meta[c])
-            else:
-                q[key] = self._grad_in(c).post_recv(*self._out_meta[c])
-        self.stats["prefetched_recvs"] += len(q)
-        return q
 
     # ------------------------------------------------------------ training
     def train_step(self, inputs: Optional[torch.Tensor], targets: Optional[torch.Tensor] = None):
@@ -746,26 +899,50 @@ class PipelineEngine:
                 torch.cuda.current_stream().wait_stream(self.dp.comm_stream)
         if self._needs_tied:
             self._wait_tied()
-        pend = {} if new_sig else self._prepost()
+        inbox: Dict[tuple, torch.Tensor] = {}     # ("act"|"grad", c, m) -> received tensor
+        outbox: Dict[tuple, torch.Tensor] = {}    # ("act"|"grad", c, m) -> tensor to send
         acts_in: Dict[tuple, torch.Tensor] = {}
         acts_out: Dict[tuple, torch.Tensor] = {}
         losses: Dict[tuple, torch.Tensor] = {}
         total = torch.zeros((), device=rt.device(), dtype=torch.float32) if self.holds_last else None
         met_in, met_out = set(), set()
-        for op, c, m in self.order:
+        tp = self.transport
+        for item in self.plan_items:
+            if item[0] == "X":
+                batch = item[1]
+                if new_sig:
+                    hs, hr = [], []
+                    for d, k, c, m, p in batch:
+                        if k != "act":
+                            continue
+                        if d == "send" and c not in met_out:
+                            t = outbox[("act", c, m)]
+                            self._out_meta[c] = (tuple(t.shape), t.dtype)
+                            met_out.add(c)
+                            hs.append((t, p))
+                        elif d == "recv" and c not in met_in:
+                            met_in.add(c)
+                            hr.append((c, p))
+                    if hs or hr:
+                        for (c, _p), meta in zip(hr, tp.exchange_meta(hs, [p for _, p in hr])):
+                            self._in_meta[c] = meta
+                sends, recvs, keys = [], [], []
+                for d, k, c, m, p in batch:
+                    if d == "send":
+                        sends.append((k, outbox.pop((k, c, m)), p))
+                    else:
+                        keys.append((k, c, m))
+                        recvs.append((k, *(self._in_meta[c] if k == "act" else self._out_meta[c]), p))
+                for key, t in zip(keys, tp.exchange_batch(sends, recvs)):
+                    inbox[key] = t
+                continue
+            _, op, c, m = item
             vs = self._vs[c]
             if op == "F":
                 if vs == 0:
                     x = _cast_inputs(xs[m], self.cast_dtype, False)
                 else:
-                    if new_sig:
-                        ch = self._act_in(c)
-                        if c not in met_in:
-                            self._in_meta[c] = ch.recv_meta()
-                            met_in.add(c)
-                        x = ch.post_recv(*self._in_meta[c]).get()
-                    else:
-                        x = pend.pop(("act", c, m)).get()
+                    x = inbox.pop(("act", c, m))
                     x.requires_grad_(x.is_floating_point())
                 acts_in[(c, m)] = x
                 y = self.chunks[c](x)
@@ -775,29 +952,25 @@ class PipelineEngine:
                     total.add_(loss.detach().float())
                 else:
                     acts_out[(c, m)] = y
-                    ch = self._act_out(c)
-                    if new_sig and c not in met_out:
-                        self._out_meta[c] = (tuple(y.shape), y.dtype)
-                        ch.send_meta(y)
-                        met_out.add(c)
-                    ch.send(y)
+                    outbox[("act", c, m)] = y
             else:
                 ctx = self.dp.no_sync() if m != M - 1 else _null()  # reduce during each chunk's last backward
                 with ctx:
                     if vs == SV - 1:
                         losses.pop((c, m)).backward()
                     else:
-                        g = (self._grad_in(c).post_recv(*self._out_meta[c]) if new_sig
-                             else pend.pop(("grad", c, m))).get()
-                        torch.autograd.backward(acts_out.pop((c, m)), grad_tensors=g)
+                        torch.autograd.backward(acts_out.pop((c, m)), grad_tensors=inbox.pop(("grad", c, m)))
                 x = acts_in.pop((c, m))
                 if vs > 0:
-                    self._grad_out(c).send(x.grad if x.grad is not None else torch.zeros_like(x))
+                    outbox[("grad", c, m)] = x.grad if x.grad is not None else torch.zeros_like(x)
+        if outbox or inbox:
+            raise RuntimeError(f"pipeline plan left messages behind: out {sorted(outbox)} in {sorted(inbox)}")
         self._sig = sig
         self.dp.flush()                      # buckets of params that got no gradient, backward-end event
         self._launch_tied()
-        for ch in self.channels.values():
-            ch.drain()
+        if tp is not None:
+            tp.drain()
+            self.stats["p2p_batches"] = tp.batches
         self.stats["steps"] += 1
         self.last_loss = total
         return total
@@ -871,36 +1044,41 @@ class PipelineEngine:
         (simulated for the configured schedule; (S-1)/(M+S-1) for GPipe/1F1B)."""
         out = self.dp.comm_metrics()
         out["bubble_fraction"] = pipeline_bubble(self.schedule, self.nstages, self.M, self.V)
-        out["p2p_bytes"] = sum(ch.bytes for ch in self.channels.values())
+        tp = self.transport
+        out["p2p_bytes"] = tp.bytes if tp is not None else 0
+        out["p2p_batches_per_step"] = (tp.batches / max(self.stats["steps"], 1)) if tp is not None else 0
         return out
 
     # ------------------------------------------------------------ inference
     @torch.no_grad()
     def forward_step(self, inputs: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
-        """Pipelined forward only, microbatch-major then chunk order (every channel FIFO);
-        returns the full output on the rank holding the last virtual stage."""
+        """Pipelined forward only, microbatch-major then chunk order: each activation travels as
+        a header exchange and a data exchange with the next rank (every program a chain along
+        the virtual stages, so it completes fully serialised); returns the full output on the
+        rank holding the last virtual stage."""
         self.module.eval()
-        M, SV = self.M, self.nstages * self.V
+        M, S, SV = self.M, self.nstages, self.nstages * self.V
         xs = list(inputs.chunk(M)) if self.holds_first else [None] * M
         outs = []
+        tp = self.transport
         for m in range(M):
             for c in range(self.V):
                 vs = self._vs[c]
                 if vs == 0:
                     x = _cast_inputs(xs[m], self.cast_dtype, False)
                 else:
-                    ch = self._act_in(c)
-                    shape, dt = ch.recv_meta()
-                    x = ch.post_recv(shape, dt).get()
+                    prev = (self.stage - 1) % S
+                    shape, dt = tp.exchange_meta([], [prev])[0]
+                    x = tp.exchange([], [(shape, dt, prev)])[0]
                 y = self.chunks[c](x)
                 if vs == SV - 1:
                     outs.append(y)
                 else:
-                    ch = self._act_out(c)
-                    ch.send_meta(y)
-                    ch.send(y)
-        for ch in self.channels.values():
-            ch.drain()
+                    nxt = (self.stage + 1) % S
+                    tp.exchange_meta([(y, nxt)], [])
+                    tp.exchange([(y, nxt)], [])
+        if tp is not None:
+            tp.drain()
         return torch.cat(outs) if outs else None
 
     def state_dict(self):
@@ -967,6 +1145,12 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     if mesh.size != world:
         raise ValueError(f"plan {plan.dp}x{S} does not match world size {world}")
     groups = rt.ProcessGroups(mesh)
+    # the gradient communicator of every pipeline replica (same ranks as its pipeline group)
+    grad_groups = []
+    if S > 1:
+        for d in range(plan.dp):
+            ranks = [mesh.rank_of(d, s, 0) for s in range(S)]
+            grad_groups.append(dist.new_group(ranks) if dist.is_initialized() else None)
     stage = groups.pp_idx
     ranges = _chunk_layer_ranges(plan, stage, S, V)
     all_layers = plan.spine.layers
@@ -1015,27 +1199,9 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
             if rt.get_rank() in ranks:
                 tied_local.append((by_name[name], grp, ranks[0]))
 
-    # one-directional FIFO channels, one 2-rank process group each (p2p_group_layout); every
-    # rank creates every group in the same order
-    import os
-
-    layout = os.environ.get("MADNN_PP_P2P_LAYOUT", "pairwise")
-    channels: Dict[str, Channel] = {}
-    p2p_groups = []  # every channel group this rank belongs to (also those it sends nothing on)
-    me = rt.get_rank()
-    for gidx, (ranks, carried) in enumerate(p2p_group_layout(S, V, plan.dp, lambda d, s: mesh.rank_of(d, s, 0),
-                                                             layout)):
-        grp = dist.new_group(list(ranks)) if dist.is_initialized() else None
-        if me not in ranks:
-            continue
-        p2p_groups.append(grp)
-        for d, (n_src, n_dst, a, b) in carried:
-            src, dst = mesh.rank_of(d, a, 0), mesh.rank_of(d, b, 0)
-            for name, mine in ((n_src, src), (n_dst, dst)):
-                if mine == me:
-                    ch = Channel(grp, src, dst, dev, name)
-                    ch.warm_key = (gidx, min(a, b))
-                    channels[name] = ch
+    # activations travel on the replica's pipeline group, gradients on a second group over the
+    # same ranks (issue_plan / P2PTransport); every rank creates every replica's group, in order
+    transport = P2PTransport(groups.pp_group, grad_groups[groups.dp_idx], groups.pp_ranks, dev) if S > 1 else None
 
     dtype, dtype_of, cl = prepare_model(stage_mod, cfg, dev)
     stage_params = [p for p in stage_mod.parameters() if p.requires_grad]
@@ -1055,8 +1221,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                              rebuild_buckets=cfg.rebuild_buckets and optimizer is not None)
     engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
                             schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
-                            tied=tied_local, param_names=names, buffer_refs=buffer_refs, channels=channels,
-                            p2p_groups=p2p_groups)
+                            tied=tied_local, param_names=names, buffer_refs=buffer_refs, transport=transport)
     engine.plan = plan
     if optimizer is not None:
         if not _is_fused(optimizer):

@@ -54,7 +54,7 @@ def _world(group) -> int:
 
 
 def _rank(group) -> int:
-    return dist.get_rank(group) if dist.is_initialized() else 0
+    return rt.get_rank(group)
 
 
 def _gather_last(x: torch.Tensor, group) -> torch.Tensor:

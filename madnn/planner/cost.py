@@ -296,8 +296,10 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
         keys.append(key)
         first.setdefault(key, i)
     distinct = sorted(first, key=lambda k: first[k])
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
-    me, world = (dist.get_rank(group), dist.get_world_size(group)) if multi else (0, 1)
+    from .. import runtime as rt
+
+    multi = dist.is_available() and dist.is_initialized() and rt.get_world_size(group) > 1
+    me, world = (rt.get_rank(group), rt.get_world_size(group)) if multi else (0, 1)
     mine = {}
     for j, key in enumerate(distinct):
         if j % world != me:

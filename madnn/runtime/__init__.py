@@ -81,11 +81,35 @@ def shutdown() -> None:
     ProcessGroups._cache.clear()
 
 
+class LocalGroup:
+    """A mesh axis of size ONE inside a larger world (the tp and cp axes of a dp x pp layout, the
+    dp axis of a pure pipeline).  Every collective over it is the identity, so madnn creates no
+    process group for it: an eagerly initialised RCCL communicator would bring its own HIP stream
+    (and a share of the GPU's hardware queues) for nothing.  ``comm`` and this module treat it
+    as a world of one in which this rank is rank 0."""
+
+    __slots__ = ("rank",)
+
+    def __init__(self, rank: int):
+        self.rank = rank
+
+    def __repr__(self):
+        return f"LocalGroup(rank={self.rank})"
+
+
+def is_local_group(group) -> bool:
+    return isinstance(group, LocalGroup)
+
+
 def get_rank(group=None) -> int:
+    if isinstance(group, LocalGroup):
+        return 0
     return dist.get_rank(group) if dist.is_initialized() else 0
 
 
 def get_world_size(group=None) -> int:
+    if isinstance(group, LocalGroup):
+        return 1
     return dist.get_world_size(group) if dist.is_initialized() else 1
 
 
@@ -112,7 +136,7 @@ def barrier(group=None, monitored: Optional[bool] = None, timeout_s: Optional[fl
     ``monitored_barrier``: a rank that never arrives is NAMED in
     the error raised on rank 0 instead of every rank hanging silently.  Set
     ``monitored=False`` (or ``MADNN_MONITORED_BARRIER=0``) for a plain barrier."""
-    if not dist.is_initialized():
+    if not dist.is_initialized() or isinstance(group, LocalGroup):
         return
     be = dist.get_backend(group)
     if be == "nccl":
@@ -201,6 +225,8 @@ class ProcessGroups:
     On one MI355X node all 8 GPUs are xGMI peers (7 links each), so no axis is
     placed for hop count; the DP all-reduce (same stage, different replicas)
     and the PP send/recv (adjacent stages) use disjoint links.
+    An axis of size one gets a :class:`LocalGroup` (no communicator, no stream);
+    an axis spanning the whole world is the world group (``None``).
     """
 
     _cache: dict = {}
@@ -222,7 +248,12 @@ class ProcessGroups:
             for ranks in mesh.axis_groups(axis):
                 key = tuple(ranks)
                 if key not in ProcessGroups._cache:
-                    ProcessGroups._cache[key] = dist.new_group(list(ranks)) if len(ranks) < world else None
+                    if len(ranks) == world:
+                        ProcessGroups._cache[key] = None            # the world group itself
+                    elif len(ranks) == 1:
+                        ProcessGroups._cache[key] = LocalGroup(ranks[0])   # no communicator
+                    else:
+                        ProcessGroups._cache[key] = dist.new_group(list(ranks))
                 if self.rank in ranks:
                     setattr(self, f"{axis}_group", ProcessGroups._cache[key])
 

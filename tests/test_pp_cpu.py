@@ -216,3 +216,28 @@ def _w_accumulate(rank, world):
 
 def test_pp_gradient_accumulation_across_train_steps():
     run_dist(_w_accumulate, 2)
+
+
+def _w_emulated_transport_catches_unpaired_batches(rank, world):
+    import os
+
+    import torch.distributed as dist
+
+    from madnn.parallel.pp import P2PTransport
+
+    os.environ["MADNN_EMULATE_RCCL_P2P"] = "1"
+    os.environ["MADNN_EMULATE_RCCL_P2P_TIMEOUT"] = "30"
+    tp = P2PTransport(None, dist.new_group([0, 1]), [0, 1], "cpu")
+    peer = 1 - rank
+    # complementary parts (an exchange) pass
+    got = tp.exchange([(torch.full((3,), float(rank)), peer)], [((3,), torch.float32, peer)], "act")
+    assert got[0].eq(float(peer)).all()
+    # both ranks send first, each in a part of its own: gloo would buffer it, RCCL with a
+    # rendezvous send and one operation at a time per rank would hang -- the emulation raises
+    with pytest.raises(RuntimeError, match="transport deadlock"):
+        tp.exchange([(torch.ones(3), peer)], [], "grad")
+
+
+def test_emulated_serial_transport_detects_unpaired_batches():
+    """Regression check of the CPU emulation itself (MADNN_EMULATE_RCCL_P2P)."""
+    run_dist(_w_emulated_transport_catches_unpaired_batches, 2)

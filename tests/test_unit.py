@@ -106,51 +106,80 @@ def test_pipeline_orders_deadlock_free_and_fifo(kind, V, S, M):
         assert r["bubble"] == pytest.approx((S - 1) / (M + S - 1), abs=1e-9)
 
 
-@pytest.mark.parametrize("S,V,dp", [(2, 1, 1), (4, 1, 2), (4, 2, 2), (8, 2, 1), (2, 3, 4)])
-def test_every_pipeline_p2p_group_has_two_ranks(S, V, dp):
-    """Each channel (edge, direction, replica) owns a 2-rank group: one sender, one receiver."""
-    from madnn.parallel.pp import p2p_channel_specs, p2p_group_layout
-
-    groups = p2p_group_layout(S, V, dp, lambda d, s: d * S + s)
-    assert len(groups) == dp * len(p2p_channel_specs(S, V)) == dp * (2 * (S - 1) + (2 if V > 1 else 0))
-    for ranks, carried in groups:
-        assert len(ranks) == 2 and len(set(ranks)) == 2 and len(carried) == 1
-        d, (_, _, a, b) = carried[0]
-        assert ranks == (d * S + a, d * S + b)
-    # every rank sends on exactly the channels it needs: interior stages 2 out + 2 in
-    for r in range(S * dp):
-        outs = [g for g, _ in groups if g[0] == r]
-        ins = [g for g, _ in groups if g[1] == r]
-        assert len(outs) == len(ins)
+_PLANS = [(k, V, S, M) for S in (2, 4, 8) for k, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", 2))
+          for M in sorted({S, 8, 16, 32}) if k != "interleaved" or M % S == 0]
 
 
-@pytest.mark.parametrize("S", [2, 4, 8])
-@pytest.mark.parametrize("kind,V", [("gpipe", 1), ("1f1b", 1), ("interleaved", 2)])
-@pytest.mark.parametrize("M", [8, 16, 32])
-def test_pipeline_transport_serialised_per_communicator(S, kind, V, M):
-    """RCCL eager-init semantics (ops of one communicator execute in issue order, a send
-    completes only with its receive): the engine's 2-rank channel groups never deadlock, with
-    every receive of the step pre-posted (steady state) or posted just in time behind a
-    host-blocking shape header (first step of an input signature)."""
+@pytest.mark.parametrize("kind,V,S,M", _PLANS)
+def test_issue_plan_messages_pair_up_fifo(kind, V, S, M):
+    """Every message of every rank's issue plan is sent once and received once, in the same order
+    on both ends of each rank pair, and every compute's input comes from a batch before it."""
+    from madnn.parallel.pp import check_plan_fifo, issue_plan
+
+    assert check_plan_fifo(kind, S, M, V) == 2 * M * (S * V - 1)
+    for s in range(S):
+        have = set()
+        for item in issue_plan(kind, s, S, M, V):
+            if item[0] == "X":
+                assert 1 <= len(item[1]) <= 4
+                have |= {(k, c, m) for d, k, c, m, _p in item[1] if d == "recv"}
+            else:
+                _, op, c, m = item
+                vs = c * S + s
+                if op == "F" and vs > 0:
+                    assert ("act", c, m) in have
+                if op == "B" and vs < S * V - 1:
+                    assert ("grad", c, m) in have
+
+
+@pytest.mark.parametrize("kind,V,S,M", _PLANS)
+def test_pipeline_transport_safe_under_hw_queue_sharing(kind, V, S, M):
+    """The engine's program (issue_plan on the act/grad communicators, DP all-reduce, tied sum)
+    completes when every stream of a rank feeds ONE serialising hardware queue, on any rotation of
+    a 4-queue (HIP's GPU_MAX_HW_QUEUES default) and a 2-queue round-robin pool, and with
+    independent queues -- dp1 and dp2 meshes, steady state and the first step's host-blocking
+    shape headers."""
     from madnn.parallel.pp import simulate_schedule, simulate_transport
 
-    for prepost in (True, False):
-        r = simulate_transport(kind, S, M, V, "pairwise", prepost)
-        assert r["communicators"] == 2 * (S - 1) + (2 if V > 1 else 0)
-        # with free transfers the transport adds no bubble over the compute-only schedule
-        assert r["bubble"] == pytest.approx(simulate_schedule(kind, S, M, V)["bubble"], abs=1e-9)
+    for dp in (1, 2):
+        for first in (False, True):
+            for q, offs in (("serial", [0]), (4, range(4)), (2, range(2)), (None, [0])):
+                for off in offs:
+                    simulate_transport(kind, S, M, V, "split", q, dp=dp, tied=True, first_step=first,
+                                       queue_offset=off)
+    # with free transfers the transport adds no bubble over the compute-only schedule
+    r = simulate_transport(kind, S, M, V, "split", None)
+    assert r["bubble"] == pytest.approx(simulate_schedule(kind, S, M, V)["bubble"], abs=1e-9)
 
 
-@pytest.mark.parametrize("kind,V,S,M", [("1f1b", 1, 4, 16), ("interleaved", 2, 4, 16), ("1f1b", 1, 8, 32),
-                                        ("1f1b", 1, 3, 4)])
-def test_shared_pipeline_groups_deadlock_on_rccl(kind, V, S, M):
-    """Regression for the round-2 layout (one S-rank group per channel kind): an interior rank's
-    send queues behind its own pre-posted receives and the step deadlocks for S >= 3."""
+@pytest.mark.parametrize("kind,V,S,M", [("gpipe", 1, 2, 8), ("1f1b", 1, 3, 8), ("1f1b", 1, 4, 16),
+                                        ("interleaved", 2, 4, 16), ("1f1b", 1, 8, 32)])
+def test_round3_preposted_receives_deadlock_when_queues_serialise(kind, V, S, M):
+    """The round-3 transport (one 2-rank communicator per channel, every receive of the step posted
+    before the first compute) is fine with independent queues but deadlocks once a rank's streams
+    share one serialising queue; at pp >= 4 with dp2 it deadlocks on EVERY rotation of the default
+    4-queue pool -- the driver's dp2 x pp4 GPT-2 layout."""
     from madnn.parallel.pp import simulate_transport
 
+    simulate_transport(kind, S, M, V, "prepost", None)
     with pytest.raises(RuntimeError, match="deadlocks"):
-        simulate_transport(kind, S, M, V, "shared", True)
-    simulate_transport("1f1b", 2, M, 1, "shared", True)  # one sender + one receiver per group: fine
+        simulate_transport(kind, S, M, V, "prepost", "serial")
+    if S >= 4 and kind != "gpipe":
+        for off in range(4):
+            with pytest.raises(RuntimeError, match="deadlocks"):
+                simulate_transport(kind, S, M, V, "prepost", 4, dp=2, tied=True, queue_offset=off)
+
+
+def test_split_transport_keeps_1f1b_transfers_off_the_critical_path():
+    """With real transfer times (a quarter of a microbatch forward) the engine's act/grad split
+    prices 1F1B exactly like the unsafe round-3 pre-posting, and beats one shared communicator."""
+    from madnn.parallel.pp import simulate_transport
+
+    for S in (4, 8):
+        split = simulate_transport("1f1b", S, 16, 1, "split", None, dp=2, tied=True, t_p2p=0.25)["makespan"]
+        one = simulate_transport("1f1b", S, 16, 1, "batched", None, dp=2, tied=True, t_p2p=0.25)["makespan"]
+        pre = simulate_transport("1f1b", S, 16, 1, "prepost", None, dp=2, tied=True, t_p2p=0.25)["makespan"]
+        assert split == pytest.approx(pre) and split < one
 
 
 def test_interleaving_shrinks_the_bubble():
