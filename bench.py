@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--schedule", default="auto",
                     help="pipeline schedule (auto: the planner prices gpipe / 1f1b / interleaved V=2,4 at every "
                          "microbatch count and picks the cheapest | gpipe | 1f1b | interleaved)")
+    ap.add_argument("--strategy", default="auto",
+                    help="ResNet-50 placement: auto (the planner's choice, BASELINE's 'auto data-parallel') or a "
+                         "pinned dp | pp | dp_pp | tp")
+    ap.add_argument("--gpt2-strategy", default="auto",
+                    help="GPT-2 placement: auto (planner; only the stage count is pinned) or pp / dp_pp")
     ap.add_argument("--no-pg", action="store_true", help="no world-1 process group when run without a launcher")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
@@ -118,8 +123,21 @@ def bench_resnet(args, world, rank):
     kw = {}
     if args.bucket_mb:
         kw["bucket_mb"] = args.bucket_mb
-    dmodel, opt = madnn.distribute(model, opt, strategy="dp", overlap=not args.no_overlap,
-                                   channels_last=bool(args.channels_last), **kw)
+    # the automatic path (BASELINE "ResNet-50 auto data-parallel"): the planner traces and costs
+    # the model on this job's GPUs (and, at N > 1, measures the job's RCCL links) and picks the
+    # placement.  The metric is ResNet-50 DATA parallel, whose ranks each draw their own images:
+    # a non-DP choice is recorded as rejected and data parallelism runs instead.  --strategy dp
+    # pins it without planning.
+    kw.update(overlap=not args.no_overlap, channels_last=bool(args.channels_last), global_batch=per_gpu * world)
+    example = torch.zeros(1, 3, args.image_size, args.image_size)
+    plan, rejected, planned = None, None, None
+    if args.strategy == "auto":
+        plan = planned = madnn.plan(model, opt, example_input=example, **kw)
+        if plan.strategy != "dp":
+            rejected, plan = _plan_info(plan), None
+            print(f"bench: the planner chose {rejected} for ResNet-50; running data parallel", file=sys.stderr)
+    dmodel, opt = madnn.distribute(model, opt, strategy=None if plan is not None else "dp", plan=plan,
+                                   example_input=example, **kw)
     dev = madnn.device()
     x, y = madnn.data.synthetic_batch("image", per_gpu, dev, dtype=torch.bfloat16 if dev.type == "cuda" else
                                       torch.float32, channels_last=bool(args.channels_last), seed=1234 + rank,
@@ -143,11 +161,62 @@ def bench_resnet(args, world, rank):
     dt = time.perf_counter() - t0
     out = (dt, per_gpu * world, {"warmup_s": round(t0 - tw, 1), "model": "resnet50", "global_batch": per_gpu * world,
                                  "per_gpu_batch": per_gpu, "seq_len": None,
-                                 "image": [3, args.image_size, args.image_size], "parallelism": f"dp{world}",
+                                 "image": [3, args.image_size, args.image_size],
+                                 "parallelism": _parallelism(plan, world),
                                  "optimizer": "FusedSGD(momentum=0.9)", "loss": float(loss.detach()),
                                  "process_group": dist.get_backend() if dist.is_initialized() else None,
-                                 "peak_mem_gib": _peak_gib()})
+                                 "peak_mem_gib": _peak_gib(), "plan": _plan_info(plan), "plan_rejected": rejected,
+                                 "tuning_timings": _tuning_timings(), **_comm_fields(dmodel, planned)})
     dmodel.remove_hooks()
+    return out
+
+
+def _parallelism(plan, world: int) -> str:
+    if plan is None:
+        return f"dp{world}"
+    if plan.pp > 1:
+        return f"pp{plan.pp}" if plan.dp == 1 else f"dp{plan.dp}xpp{plan.pp}"
+    return f"dp{plan.dp}" if plan.tp == 1 else f"dp{plan.dp}xtp{plan.tp}"
+
+
+def _plan_info(plan):
+    """What the planner chose (None when the strategy was pinned without a plan)."""
+    if plan is None:
+        return None
+    return {"strategy": plan.strategy, "dp": plan.dp, "pp": plan.pp, "tp": plan.tp,
+            "schedule": plan.schedule if plan.pp > 1 else None, "virtual": plan.virtual if plan.pp > 1 else None,
+            "microbatches": plan.microbatches if plan.pp > 1 else None, "est_step_ms": round(plan.est_step_s * 1e3, 2),
+            "costs": "measured" if plan.measured else "analytic", "candidates": len(plan.candidates),
+            "comm_measured": bool(getattr(plan, "comm_probe", None))}
+
+
+def _tuning_timings():
+    import madnn.ops as ops
+
+    return ops.tuning_timings()
+
+
+def _comm_fields(engine, plan) -> dict:
+    """The numbers that explain an N > 1 result: the last step's exposed gradient all-reduce and
+    its achieved bus bandwidth (``DataParallel.comm_metrics``), the job-start link probe's
+    all-reduce busbw and P2P rate (``comm.probe``, what the planner priced with)."""
+    out = {"comm_exposed_ms": None, "busbw_gbps": None, "p2p_gbps": None}
+    try:
+        m = engine.comm_metrics() if hasattr(engine, "comm_metrics") else {}
+    except Exception:  # noqa: BLE001 - metrics never fail the bench
+        m = {}
+    if m.get("comm_exposed_ms") is not None:
+        out["comm_exposed_ms"] = round(m["comm_exposed_ms"], 3)
+    if m.get("busbw_gbps") is not None:
+        out["busbw_gbps"] = round(m["busbw_gbps"], 2)
+    probe = getattr(plan, "comm_probe", None) if plan is not None else None
+    if probe:
+        out["p2p_gbps"] = round(probe["p2p_gbps"], 2)
+        out["probe_allreduce_busbw_gbps"] = round(probe["allreduce_busbw_gbps"], 2)
+    if "bubble_fraction" in m:
+        out["bubble_fraction"] = round(m["bubble_fraction"], 4)
+    if "p2p_bytes" in m:
+        out["p2p_bytes"] = m["p2p_bytes"]
     return out
 
 
@@ -180,9 +249,16 @@ def bench_gpt2(args, world, rank):
         if sched == "interleaved" and micro and micro % stages:
             sched = "1f1b"  # interleaving needs microbatches % stages == 0
         kw["schedule"] = sched
-    engine, opt = madnn.distribute(model, opt, strategy=strategy, pp_stages=stages if stages > 1 else None,
-                                   microbatches=micro, checkpointing="none", global_batch=gbatch,
+    # the automatic path (BASELINE "GPT-2 medium auto pipeline-parallel, 4 stages"): only the stage
+    # count is pinned; the planner picks schedule, microbatches, chunks and checkpointing from
+    # layer costs measured on this job's GPUs and (N > 1) the job's measured P2P / all-reduce rates
+    engine, opt = madnn.distribute(model, opt, strategy=args.gpt2_strategy if stages > 1 else args.strategy,
+                                   pp_stages=stages if stages > 1 else None, microbatches=micro,
+                                   checkpointing="none", global_batch=gbatch,
                                    example_input=torch.zeros(1, args.seq_len, dtype=torch.long), **kw)
+    plan = getattr(engine, "plan", None)
+    if plan is not None and plan.pp != stages:
+        raise RuntimeError(f"GPT-2 bench pins {stages} pipeline stages, the planner built {_plan_info(plan)}")
     dev = madnn.device()
     # every dp replica draws its own token batch; pipeline stages of one replica share it
     g = torch.Generator(device="cpu").manual_seed(4321 + (rank // stages))
@@ -213,7 +289,7 @@ def bench_gpt2(args, world, rank):
             "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
             "virtual_stages": getattr(engine, "V", None) if stages > 1 else None,
             "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "loss_last_stage": lv,
-            "peak_mem_gib": _peak_gib()}
+            "peak_mem_gib": _peak_gib(), "plan": _plan_info(plan), **_comm_fields(engine, plan)}
     return dt, steps, gbatch, info
 
 
@@ -281,15 +357,19 @@ def main():
             "data": "synthetic (random ImageNet-shaped images / random tokens, random-init weights)",
             "config": config,
         }
+        config["per_gpu_value"] = round(res["value"] / world, 2)
         _release()
         if args.std_batch and args.std_batch != config["per_gpu_batch"]:
             # the same measurement at a standard per-GPU batch, so rounds compare like for like
             sargs = argparse.Namespace(**dict(vars(args), batch=args.std_batch))
-            sdt, sps_step, _ = bench_resnet(sargs, world, rank)
+            sdt, sps_step, sconf = bench_resnet(sargs, world, rank)
             sdt = _max_over_ranks(sdt)
+            sval = round(sps_step * args.steps / sdt, 2)
             res["config"]["std_batch"] = {"per_gpu_batch": args.std_batch, "global_batch": sps_step,
-                                          "value": round(sps_step * args.steps / sdt, 2),
-                                          "ms_per_step": round(sdt / args.steps * 1000.0, 3)}
+                                          "value": sval, "per_gpu_value": round(sval / world, 2),
+                                          "ms_per_step": round(sdt / args.steps * 1000.0, 3),
+                                          "warmup_s": sconf["warmup_s"], "parallelism": sconf["parallelism"],
+                                          **{k: sconf.get(k) for k in ("comm_exposed_ms", "busbw_gbps", "p2p_gbps")}}
             _release()
     if args.model in ("all", "gpt2-medium"):
         if args.model == "all":

@@ -10,13 +10,14 @@ kept under the same names.
 """
 from .config import Config
 from .runtime import init, shutdown, get_rank, get_world_size, device, barrier, seed_all
-from .api import distribute, parallelize, synchronize_model, Trainer
+from .api import distribute, plan, parallelize, synchronize_model, Trainer
 from . import ops, optim, data, comm, models
 from .ckpt import save, load, consolidate
 
 __version__ = "0.1.0"
 
 __all__ = [
+    "plan",
     "Config", "init", "shutdown", "get_rank", "get_world_size", "device", "barrier", "seed_all",
     "distribute", "parallelize", "synchronize_model", "Trainer", "ops", "optim", "data", "comm", "models",
     "save", "load", "consolidate",

@@ -96,13 +96,39 @@ def build_space(model: nn.Module, optimizer, cfg: Config, device, dtype_of, chan
                           channels_last_of=(lambda p: channels_last and p.dim() == 4))
 
 
+def plan(model: nn.Module, optimizer=None, *, strategy: str = "auto", config: Optional[Config] = None,
+         example_input=None, **kwargs):
+    """The planner's placement for ``model`` on this job (``madnn.planner.Plan``) without applying
+    it: trace, cost (measured on the job's GPUs) and, at W > 1, the measured links.  Pass it back
+    with ``distribute(model, opt, plan=p)`` to use it, or inspect ``p.describe()`` /
+    ``p.table()`` first."""
+    from .planner import plan_model
+
+    cfg = config or Config.from_env(**kwargs)
+    cfg.strategy = strategy
+    rt.init(timeout_s=cfg.timeout_s)
+    _swap_kernels(model, cfg)
+    return plan_model(model, cfg, world=rt.get_world_size(), example_input=example_input, optimizer=optimizer)
+
+
+def _swap_kernels(model: nn.Module, cfg: Config) -> None:
+    device = rt.device()
+    if cfg.fused_kernels == "on" or (cfg.fused_kernels == "auto" and device.type == "cuda"):
+        from .nn.swap import use_madnn_kernels
+
+        swapped = use_madnn_kernels(model)
+        if swapped:
+            get_logger().info("madnn: hand-written kernels swapped in: %s", swapped)
+
+
 def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = None, config: Optional[Config] = None,
-               example_input=None, loss_fn: Optional[Callable] = None, **kwargs):
+               example_input=None, loss_fn: Optional[Callable] = None, plan=None, **kwargs):
     """Place ``model`` across the GPUs of this node and return ``(engine, optimizer)``.
 
     ``strategy``: ``"auto"`` (the planner traces and costs the model and picks
     DP, PP or DP x PP for the available ranks and 288 GB per GPU), or force
-    ``"dp"``, ``"pp"``, ``"dp_pp"``, ``"tp"``.  ``kwargs`` override
+    ``"dp"``, ``"pp"``, ``"dp_pp"``, ``"tp"``.  ``plan``: a placement from
+    :func:`plan` to apply as is (no re-planning).  ``kwargs`` override
     :class:`~madnn.config.Config` fields (e.g. ``bucket_mb=32``,
     ``pp_stages=4``, ``microbatches=8``, ``dtype="bfloat16"``).
     """
@@ -112,15 +138,13 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
     rt.init(timeout_s=cfg.timeout_s)
     apply_debug_flags(cfg)
     device = rt.device()
-    if cfg.fused_kernels == "on" or (cfg.fused_kernels == "auto" and device.type == "cuda"):
-        from .nn.swap import use_madnn_kernels
-
-        swapped = use_madnn_kernels(model)
-        if swapped:
-            get_logger().info("madnn: hand-written kernels swapped in: %s", swapped)
+    _swap_kernels(model, cfg)
     strat = cfg.strategy
-    plan = None
-    if strat in ("auto", "pp", "dp_pp"):
+    if plan is not None:
+        strat = plan.strategy
+        if strat == "tp":
+            cfg.tp_size = plan.tp
+    elif strat in ("auto", "pp", "dp_pp"):
         from .planner import plan_model
 
         try:
@@ -144,7 +168,9 @@ def distribute(model: nn.Module, optimizer=None, *, strategy: Optional[str] = No
     if strat == "tp":
         from .parallel.tp import apply_tensor_parallel
 
-        return apply_tensor_parallel(model, optimizer, cfg)
+        engine, optimizer = apply_tensor_parallel(model, optimizer, cfg)
+        engine.plan = plan
+        return engine, optimizer
     if strat == "none":
         return model, optimizer
     engine, optimizer = _distribute_dp(model, optimizer, cfg, device, loss_fn=loss_fn, plan=plan)

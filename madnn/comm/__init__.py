@@ -231,6 +231,18 @@ def recv(t: torch.Tensor, src: int, group=None):
     return dist.irecv(t, src, group=group)
 
 
+def all_agree(ok: bool, group=None) -> bool:
+    """True on every rank iff ``ok`` is true on every rank of ``group`` (a MIN all-reduce).  Ranks
+    call it after a step that may fail locally and BEFORE any collective that depends on it, so a
+    local failure becomes a common decision instead of peers blocked in a gather."""
+    if _local(group) or not dist.is_initialized():
+        return bool(ok)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 def log_backend_once():
     if dist.is_initialized():
         get_logger().info("comm backend=%s world=%d", dist.get_backend(), dist.get_world_size())

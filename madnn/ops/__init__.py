@@ -1180,6 +1180,67 @@ def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
 
 WGRAD = os.environ.get("MADNN_WGRAD", "auto")  # weight-gradient GEMM: auto (timed per shape) | lt | k12
 _WGRAD_CHOICE: dict = {}
+_GELU_FWD_CHOICE: dict = {}
+_TUNE = {"timed": 0, "table": None}   # run-time timings taken; the shipped table that was loaded
+
+# Per-shape implementation choices measured on MI355X and shipped in-tree, so a job starts
+# without timing anything (a first-use timing runs BOTH implementations, and a library kernel's
+# first use can cost seconds of MIOpen problem search) and every replica of a multi-GPU job
+# runs the same kernels.  ``scripts/record_tuning.py`` regenerates it on a GPU box.
+TUNE_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                          "choices_gfx950.json")
+
+
+def load_tuning_table(path: Optional[str] = None) -> int:
+    """Adopt the shipped per-shape choices (``MADNN_TUNE_TABLE=0`` disables; ``MADNN_TUNE_TABLE_PATH``
+    overrides the file).  Returns the number of entries loaded."""
+    import ast
+    import json
+
+    if os.environ.get("MADNN_TUNE_TABLE", "1") == "0":
+        return 0
+    path = path or os.environ.get("MADNN_TUNE_TABLE_PATH") or TUNE_TABLE
+    try:
+        with open(path) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        return 0
+    n = 0
+    for name, dst in (("wgrad", _WGRAD_CHOICE), ("gelu_fwd", _GELU_FWD_CHOICE)):
+        for k, v in data.get(name, {}).items():
+            dst.setdefault(ast.literal_eval(k), v)
+            n += 1
+    _TUNE["table"] = path
+    return n
+
+
+def export_choices(path: str) -> None:
+    """Write every per-shape choice this process holds (shipped + timed) in the table format."""
+    import json
+
+    data = {"arch": "gfx950", "wgrad": {repr(k): v for k, v in sorted(_WGRAD_CHOICE.items(), key=repr)},
+            "gelu_fwd": {repr(k): v for k, v in sorted(_GELU_FWD_CHOICE.items(), key=repr)}}
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1)
+        f.write("\n")
+
+
+def sync_choices(group=None, src: int = 0) -> None:
+    """Every rank of ``group`` adopts global rank ``src``'s per-shape choices, so replicas that
+    timed a shape missing from the table independently still run identical kernels from here on."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(group) <= 1:
+        return
+    obj = [(dict(_WGRAD_CHOICE), dict(_GELU_FWD_CHOICE))]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    _WGRAD_CHOICE.update(obj[0][0])
+    _GELU_FWD_CHOICE.update(obj[0][1])
+
+
+def tuning_timings() -> int:
+    """How many per-shape timings this process ran (0 when the table covered every shape)."""
+    return _TUNE["timed"]
 
 
 def _wgrad_k12_ok(g2, x2, out) -> bool:
@@ -1217,9 +1278,10 @@ def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.T
 
 
 def tuned_wgrad(key, lib, k12):
-    """Run the weight-gradient implementation that was faster for ``key`` (timed once, on first
-    use, outside graph capture): ``lib`` (the library kernel: hipBLASLt / MIOpen) or ``k12`` (K12
-    split-K).  ``MADNN_WGRAD=lt`` / ``k12`` pin one."""
+    """Run the weight-gradient implementation that was faster for ``key``: ``lib`` (the library
+    kernel: hipBLASLt / MIOpen) or ``k12`` (K12 split-K) -- from the shipped table
+    (:func:`load_tuning_table`), else timed once on first use (outside graph capture).
+    ``MADNN_WGRAD=lt`` / ``k12`` pin one."""
     if WGRAD == "lt":
         return lib()
     if WGRAD == "k12":
@@ -1228,6 +1290,7 @@ def tuned_wgrad(key, lib, k12):
     if choice is None:
         if torch.cuda.is_current_stream_capturing():
             return lib()
+        _TUNE["timed"] += 1
         t_lib = _time_wgrad(lib)
         t_k12 = _time_wgrad(k12)
         choice = _WGRAD_CHOICE[key] = "k12" if t_k12 < t_lib else "lib"
@@ -1280,7 +1343,6 @@ def _lt_linear(x2, weight, bias, residual, gelu):
 
 
 GELU_FWD = os.environ.get("MADNN_GELU_FWD", "auto")  # GELU Linear forward: auto (timed per shape) | lt | k12
-_GELU_FWD_CHOICE: dict = {}
 
 
 def _k12_fwd_ok(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> bool:
@@ -1321,6 +1383,7 @@ def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
                 if torch.cuda.is_current_stream_capturing():
                     choice = "lt"
                 else:
+                    _TUNE["timed"] += 1
                     t_lt, t_k12 = _time_wgrad(lt), _time_wgrad(k12)
                     choice = _GELU_FWD_CHOICE[key] = "k12" if t_k12 < t_lt else "lt"
     elif choice == "k12" and not _k12_fwd_ok(x2, weight, bias):
@@ -1432,3 +1495,6 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         y = F.gelu(y, approximate="tanh") if gelu else y
         return y + residual if residual is not None else y
     return _LinearFn.apply(x, weight, bias, gelu, residual)
+
+
+load_tuning_table()

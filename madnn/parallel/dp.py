@@ -323,6 +323,12 @@ class DataParallel(nn.Module):
         """Called by the fused optimizer after each step: the sync="params" period, then the
         robustness hooks (fault injection, collective-order check)."""
         self._steps += 1
+        if self._steps == 1 and self.world > 1 and not comm._local(self.group):
+            # shapes missing from the shipped tuning table were timed on each replica on its own:
+            # adopt the source rank's choices so every replica runs the same kernels from now on
+            from .. import ops
+
+            ops.sync_choices(self.group, src=self.src_rank)
         if self._observe is not None:
             self._maybe_relayout()
         if self.sync == "params" and self._steps % self.sync_every == 0:

@@ -1096,6 +1096,23 @@ class PipelineEngine:
 
 
 _BUBBLE_CACHE: Dict[tuple, float] = {}
+_TRANSPORT_CACHE: Dict[tuple, float] = {}
+
+
+def transport_time(schedule: str, nstages: int, nmicro: int, nchunks: int, chunk_s: float, p2p_s: float) -> float:
+    """Seconds of one pipelined step of ``nmicro`` microbatches when one chunk's forward +
+    backward of one microbatch takes ``chunk_s`` (split 1 : 2) and one activation / gradient
+    transfer ``p2p_s``: the makespan of :func:`simulate_transport` on the engine's transport
+    (independent queues), so the planner prices exactly the communication this engine exposes.
+    Cached on the transfer / compute ratio (2 significant digits)."""
+    if nstages <= 1 or chunk_s <= 0:
+        return nmicro * nchunks * max(chunk_s, 0.0)
+    ratio = float(f"{p2p_s / chunk_s:.2g}") if p2p_s > 0 else 0.0
+    key = (schedule, nstages, nmicro, nchunks, ratio)
+    if key not in _TRANSPORT_CACHE:
+        _TRANSPORT_CACHE[key] = simulate_transport(schedule, nstages, nmicro, nchunks, "split", None,
+                                                   t_fwd=1.0, t_bwd=2.0, t_p2p=3.0 * ratio)["makespan"] / 3.0
+    return _TRANSPORT_CACHE[key] * chunk_s
 
 
 def pipeline_bubble(schedule: str, nstages: int, nmicro: int, nchunks: int = 1) -> float:

@@ -18,11 +18,12 @@ Step-time model for ``W = dp x pp x tp`` GPUs, global batch B, M microbatches:
   does not hide -- a bucket-by-bucket timeline: buckets fill in backward
   order, each is reduced when its last gradient lands, one after another on
   the comm stream; exposed = reductions still running after backward ends;
-* PP (GPipe / 1F1B / interleaved with V chunks per rank):
-  M x max-rank-time-per-microbatch / (1 - bubble), where the bubble is the
-  idle fraction of the simulated schedule, plus the fill/drain P2P latency
-  (steady-state transfers run under compute); with dp > 1 the stage-local
-  all-reduce overlaps only the last microbatch's backward (same timeline);
+* PP (GPipe / 1F1B / interleaved with V chunks per rank): the makespan of the
+  engine's own transport (``parallel.pp.simulate_transport``: the boundary-batched
+  issue plan with the node's measured P2P time), i.e. the schedule's bubble plus
+  whatever transfers the schedule leaves on the critical path; with dp > 1 the
+  stage-local all-reduce overlaps only the last microbatch's backward (same
+  timeline);
 * TP (row-parallel large Linears, ``strategy="tp"``): the sharded GEMM share of
   compute divided by T, plus the per-layer activation all-reduce and
   input-gradient all-gather on the critical path.
@@ -46,7 +47,8 @@ from torch import nn
 from ..config import Config, torch_dtype
 from ..ops import native_runtime
 from ..utils.logging import get_logger
-from .cost import LayerCost, divisors, estimate, measure_chain, measure_layers, param_state_bytes, stage_estimate
+from .cost import (LayerCost, MeasurementFailed, divisors, estimate, measure_chain, measure_layers, param_state_bytes,
+                   stage_estimate)
 from .hw import Machine, load
 from .trace import Spine, find_block_list, trace
 
@@ -143,7 +145,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     lowest modelled step time that fits in HBM.  ``global_batch``: samples per optimizer step
     over the whole job (default ``cfg.extra['global_batch']``, else the example input's
     batch per GPU x ``world``)."""
-    hw = machine or load()
+    hw = machine or _job_machine()
     spine = trace(model)
     explicit_input = example_input is not None
     if example_input is None:
@@ -162,18 +164,20 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         import torch.distributed as dist
 
         multi = dist.is_initialized() and dist.get_world_size() > 1
-        ok = 1
         if _want_measure(cfg):
+            per_gpu = max(int(B) // max(world, 1), 1) if (explicit_input or global_batch
+                                                          or cfg.extra.get("global_batch")) else None
+            mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input, per_gpu)
             try:
-                per_gpu = max(int(B) // max(world, 1), 1) if (explicit_input or global_batch
-                                                              or cfg.extra.get("global_batch")) else None
-                mb = int(cfg.extra.get("measure_batch", 0)) or _default_measure_batch(example_input, per_gpu)
-                # every rank times its share of the distinct layers (all-gathered inside)
-                costs = measure_layers(spine, example_input, costs, batch=mb, dtype=dtype)
-                calib = _calibrate_chain(spine, example_input, costs, mb, dtype, cfg, hw)
-            except Exception as e:  # noqa: BLE001 - the analytic model still plans
+                # every rank times its share of the distinct layers; the ranks agree on success
+                # before the results are all-gathered (MeasurementFailed on every rank otherwise)
+                costs = measure_layers(spine, example_input, costs, batch=mb, dtype=dtype,
+                                       device=None if torch.cuda.is_available() else torch.device("cpu"))
+            except MeasurementFailed as e:
                 get_logger().warning("madnn planner: layer measurement failed (%s); using analytic costs", e)
-                ok = 0
+                costs = estimate(spine, example_input, dtype=dtype, machine=hw)
+            else:
+                calib = _calibrate_chain(spine, example_input, costs, mb, dtype, cfg, hw)
         if multi:
             # every rank must choose the SAME placement: rank 0's (measured) costs are the plan input
             obj = [[(c.fwd_s, c.bwd_s, c.fixed_s, c.measured) for c in costs], calib]
@@ -182,6 +186,11 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
                 c.fwd_s, c.bwd_s, c.fixed_s, c.measured = f, b, fx, m
             calib = obj[1]
     measured = all(c.measured for c in costs)
+    comm_probe = _probe_comm(cfg, world)
+    if comm_probe:
+        from ..comm import probe as _probe
+
+        hw = _probe.apply(hw, comm_probe)
     opt = _opt_kind(optimizer)
     cap = hw.hbm_gb * cfg.mem_headroom * 1e9
     L = len(spine)
@@ -198,7 +207,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
                 c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode, schedule, V, M)
                 if c is not None:
                     cands.append(c)
-    if forced in ("auto", "tp") and world > 1:
+    if (forced == "tp" or forced == "auto" and not cfg.pp_stages) and world > 1:
         for tp in divisors(world):
             if tp == 1 or (forced == "tp" and cfg.tp_size > 1 and tp != cfg.tp_size):
                 continue
@@ -215,10 +224,44 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
                 best["mem_list"], spine, costs, cands, B, schedule=best.get("schedule", "1f1b"),
                 virtual=best.get("V", 1), tp=best.get("tp", 1), measured=measured)
     plan.calibration = calib
+    plan.comm_probe = comm_probe
+    plan.machine = hw
     log = get_logger()
     log.info("madnn plan: %s", plan.describe())
     log.info("madnn plan candidates (world=%d, global batch %d):\n%s", world, B, plan.table())
     return plan
+
+
+def _job_machine() -> Machine:
+    """The machine profile of THIS job: the MI355X profile (``hw.load``), or the host-CPU one when
+    the job really runs on CPU tensors over gloo."""
+    import torch.distributed as dist
+
+    from .. import runtime as rt
+    from .hw import host_cpu
+
+    if dist.is_initialized() and dist.get_backend() == "gloo" and rt.device().type == "cpu":
+        return host_cpu()
+    return load()
+
+
+def _probe_comm(cfg: Config, world: int) -> Optional[dict]:
+    """Measured all-reduce / P2P numbers of THIS job's world group (``comm.probe``), when the
+    job really runs ``world`` > 1 ranks on RCCL or gloo; None otherwise (single GPU, a fake
+    process group planning a hypothetical node, or ``MADNN_PLAN_COMM=0``)."""
+    import torch.distributed as dist
+
+    from ..comm import probe as _probe
+
+    if not (dist.is_initialized() and world > 1 and dist.get_world_size() == world
+            and dist.get_backend() in ("nccl", "gloo") and _probe.wanted(cfg)):
+        return None
+    res = _probe.measure()
+    if res:
+        get_logger().info("madnn planner: measured comm world=%d: all-reduce %.1f GB/s busbw, %.0f us small, "
+                          "P2P %.1f GB/s", world, res["allreduce_busbw_gbps"], res["allreduce_small_us"],
+                          res["p2p_gbps"])
+    return res or None
 
 
 def _default_measure_batch(example_input: torch.Tensor, per_gpu: Optional[int] = None) -> int:
@@ -237,6 +280,8 @@ def _default_measure_batch(example_input: torch.Tensor, per_gpu: Optional[int] =
 
 
 def _allowed(forced: str, pp: int, dp: int, world: int, pp_stages) -> bool:
+    if forced == "auto" and pp_stages:   # automatic everything except the pinned stage count
+        return pp == pp_stages
     if forced == "dp":
         return pp == 1
     if forced == "tp":
@@ -334,15 +379,24 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
     need = nparams * 6 + sum(c.act_bytes for c in costs) * batch   # weights + grads, saved activations
     if need > 0.5 * hw.hbm_gb * 1e9:
         return None
-    t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype)
-    if not t:
-        return None
     import torch.distributed as dist
 
-    if dist.is_initialized() and dist.get_world_size() > 1:  # every GPU timed it: average
+    from .. import comm
+
+    try:
+        t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype)
+    except Exception as e:  # noqa: BLE001 - decided together below
+        get_logger().warning("madnn planner: chain timing failed (%s)", e)
+        t = None
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        # all ranks agree before the averaging collective: one failed timing drops it everywhere
+        if not comm.all_agree(bool(t), None):
+            return None
         v = torch.tensor([t], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(v)
+        dist.all_reduce(v)   # every GPU timed it: average
         t = float(v) / dist.get_world_size()
+    if not t:
+        return None
     layers = sum(c.call_s(batch) for c in costs)
     if layers <= 0:
         return None
@@ -355,7 +409,7 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
 
 
 def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="none", V=1, M=1):
-    from ..parallel.pp import pipeline_bubble, simulate_schedule
+    from ..parallel.pp import pipeline_bubble, simulate_schedule, transport_time
 
     L = len(costs)
     per_replica = max(B // dp, 1)
@@ -397,18 +451,21 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
         comm_s = dp_exposed_s(bwd, [c.params * rb for c in costs], dp, hw, bucket_bytes)
         step = compute + comm_s + opt_s
     else:
-        bubble = pipeline_bubble(schedule, pp, M, V)
         compute = M * max(rank_t)
         p2p = max((costs[bounds[v + 1] - 1].out_bytes * mb for v in range(nst - 1)), default=0.0)
-        comm_s = 2 * (nst - 1) * hw.p2p_s(p2p)  # fill + drain; steady-state hops run under compute
+        # the engine's transport simulated with this node's (measured) P2P time: bubble AND the
+        # transfers the schedule leaves on the critical path
+        pipe = transport_time(schedule, pp, M, V, max(rank_t) / V, hw.p2p_s(p2p))
+        bubble = pipeline_bubble(schedule, pp, M, V)
+        comm_s = max(pipe - compute / max(1.0 - bubble, 1e-3), 0.0)   # transfers left on the critical path
+        dp_s = 0.0
         if dp > 1:  # stage-local reduction overlaps the last microbatch's backward only
-            worst = 0.0
             for vs in ranks:
                 idx = [i for v in vs for i in range(bounds[v], bounds[v + 1])]
                 bwd = [(costs[i].bwd_s * mb + costs[i].fixed_s * 2.0 / 3.0) * rfac for i in idx]
-                worst = max(worst, dp_exposed_s(bwd, [costs[i].params * rb for i in idx], dp, hw, bucket_bytes))
-            comm_s += worst
-        step = compute / max(1.0 - bubble, 1e-3) + comm_s + opt_s
+                dp_s = max(dp_s, dp_exposed_s(bwd, [costs[i].params * rb for i in idx], dp, hw, bucket_bytes))
+        comm_s += dp_s
+        step = pipe + dp_s + opt_s
     fits = max(mem_list) * 1e9 <= cap
     strategy = "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp")
     return {"strategy": strategy, "dp": dp, "pp": pp, "tp": 1, "M": M, "V": V, "schedule": schedule,

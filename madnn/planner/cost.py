@@ -12,6 +12,8 @@ FLOPs (``torch.utils.flop_counter``) and the bytes every op writes.  On a GPU,
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass, field
 from typing import Any, List, Optional
@@ -126,6 +128,10 @@ def estimate(spine: Spine, example_input: torch.Tensor, dtype: Optional[torch.dt
              machine: Optional[Machine] = None) -> List[LayerCost]:
     """Analytic per-sample costs of every spine layer (meta device, no allocation)."""
     hw = machine or load()
+    if example_input.dim() > 0 and example_input.shape[0] == 1:
+        # costs are per sample; two samples keep training-mode BatchNorm (one value per channel
+        # after a global pool) valid
+        example_input = example_input.expand(2, *example_input.shape[1:])
     batch = example_input.shape[0] if example_input.dim() > 0 else 1
     x = _to_meta(example_input, dtype)
     seen = {}
@@ -247,6 +253,19 @@ def _time_call(fn, xin, iters: int):
         y = fn(xin)
         if y.requires_grad:
             y.backward(torch.ones_like(y))
+    if xin.device.type != "cuda":      # host tensors (CPU jobs): wall clock
+        import time
+
+        fw = bw = 0.0
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            y = fn(xin)
+            t1 = time.perf_counter()
+            if y.requires_grad:
+                y.backward(torch.ones_like(y))
+            fw += (t1 - t0) * 1e3
+            bw += (time.perf_counter() - t1) * 1e3
+        return fw / iters, bw / iters
     start, mid, end = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     fw = bw = 0.0
     for _ in range(iters):
@@ -260,6 +279,11 @@ def _time_call(fn, xin, iters: int):
         fw += start.elapsed_time(mid)
         bw += mid.elapsed_time(end)
     return fw / iters, bw / iters
+
+
+class MeasurementFailed(RuntimeError):
+    """A layer / chain timing failed on this rank or on a peer; every rank of the group raises it
+    together (the planner then uses analytic costs everywhere)."""
 
 
 def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: Optional[int] = None,
@@ -279,7 +303,7 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
     so no rank idles while one GPU times the whole model.  Returns ``costs`` unchanged without
     a GPU.  This is the working version of the reference's dead ``comm_speed`` probe
     (datamodule.lua:280-303)."""
-    if not torch.cuda.is_available():
+    if device is None and not torch.cuda.is_available():
         return costs
     import torch.distributed as dist
 
@@ -301,25 +325,40 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
     multi = dist.is_available() and dist.is_initialized() and rt.get_world_size(group) > 1
     me, world = (rt.get_rank(group), rt.get_world_size(group)) if multi else (0, 1)
     mine = {}
-    for j, key in enumerate(distinct):
-        if j % world != me:
-            continue
-        i = first[key]
-        rep, cl = _replica(spine.layers[i], dev, dtype)
-        res = []
-        for n in ([b] + ([b2] if b2 else [])):
-            x = _layer_input(i, costs, example_input, n, dtype, dev)
-            if cl and x.dim() == 4:
-                x = x.contiguous(memory_format=torch.channels_last)
-            # the model input needs no gradient (a conv stem's data grad is a large, slow pass the
-            # training step never runs); every later layer's input does
-            xin = x.detach().requires_grad_(x.is_floating_point() and i > 0)
-            res.append((n,) + _time_call(rep, xin, iters))
-            del x, xin
-        for p in rep.parameters():
-            p.grad = None
-        del rep
-        mine[j] = res
+    err = None
+    try:
+        for j, key in enumerate(distinct):
+            if j % world != me:
+                continue
+            i = first[key]
+            rep, cl = _replica(spine.layers[i], dev, dtype)
+            res = []
+            for n in ([b] + ([b2] if b2 else [])):
+                x = _layer_input(i, costs, example_input, n, dtype, dev)
+                if cl and x.dim() == 4:
+                    x = x.contiguous(memory_format=torch.channels_last)
+                # the model input needs no gradient (a conv stem's data grad is a large, slow pass
+                # the training step never runs); every later layer's input does
+                xin = x.detach().requires_grad_(x.is_floating_point() and i > 0)
+                res.append((n,) + _time_call(rep, xin, iters))
+                del x, xin
+            for p in rep.parameters():
+                p.grad = None
+            del rep
+            mine[j] = res
+        if os.environ.get("MADNN_FAULT_MEASURE") == str(me):   # test hook: this rank's timing fails
+            raise RuntimeError(f"injected layer-measurement failure on rank {me}")
+    except Exception as e:  # noqa: BLE001 - decided together below
+        err = e
+    if multi:
+        from .. import comm
+
+        # every rank learns whether ALL measured before anyone enters the gather: a rank that
+        # failed alone would otherwise leave its peers blocked in all_gather_object
+        if not comm.all_agree(err is None, group):
+            raise MeasurementFailed(f"layer measurement failed on some rank ({err or 'a peer'})")
+    elif err is not None:
+        raise MeasurementFailed(str(err)) from err
     if multi:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine, group=group)

@@ -47,6 +47,15 @@ class Machine:
         return nbytes / (self.p2p_gbps * 1e9) + self.collective_latency_us * 1e-6
 
 
+def host_cpu() -> Machine:
+    """A rough host-CPU profile for jobs that really run on CPU over gloo (tests, the MLP
+    config): pricing their compute with MI355X numbers would make every collective look
+    expensive and push the planner to tensor parallelism for convolutional nets."""
+    return Machine(name="host-cpu", hbm_gb=64.0, hbm_tbps=0.02, bf16_tflops=0.2, fp32_tflops=0.2, link_gbps=1.0,
+                   links=1, allreduce_eff=1.0, p2p_gbps=1.0, collective_latency_us=300.0, kernel_launch_us=20.0,
+                   source="host-cpu")
+
+
 _CACHE = {}
 SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "hw_mi355x.json")
 

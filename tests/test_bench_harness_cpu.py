@@ -34,6 +34,17 @@ def test_bench_py_two_ranks_cpu():
     assert res["config"]["parallelism"] == "dp2" and res["value"] > 0
     assert abs(res["value"] - 4 * 2 / (res["ms_per_step"] * 2 / 1000)) / res["value"] < 0.01
     assert res["config"]["process_group"] == "gloo"
+    # the automatic path and the numbers that explain an N > 1 result
+    c = res["config"]
+    # (on CPU the planner prices gloo against host compute: for 2 tiny images per rank it may
+    # prefer a pipeline, which the bench records as rejected -- the metric is ResNet-50 DP)
+    chosen = c["plan"] or c["plan_rejected"]
+    assert chosen["comm_measured"] and chosen["dp"] * chosen["pp"] * chosen["tp"] == 2
+    assert c["plan"] is None or c["plan"]["strategy"] == "dp"
+    assert c["per_gpu_value"] == pytest.approx(res["value"] / 2, rel=1e-3)
+    assert c["comm_exposed_ms"] is None or c["comm_exposed_ms"] >= 0
+    assert c["p2p_gbps"] > 0 and c["probe_allreduce_busbw_gbps"] > 0
+    assert "busbw_gbps" in c and c["tuning_timings"] == 0
     # the GPT-2 pipeline half of the BASELINE metric rides in the same line
     g = res["gpt2_pp"]
     assert g["parallelism"] == "pp2" and g["n_gpus"] == 2 and g["global_batch"] == 8 and g["microbatches"] == 4
@@ -89,7 +100,11 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 4 and res["scaling"] == "weak" and res["value"] > 0
     assert res["config"]["parallelism"] == "pp4" and res["config"]["global_batch"] == 4
-    assert res["gpt2_pp"]["microbatches"] == 4 and res["gpt2_pp"]["model"] == "gpt2-medium"
+    pp = res["gpt2_pp"]
+    assert pp["microbatches"] == 4 and pp["model"] == "gpt2-medium"
+    # the planner's choice and the transport numbers ride in the line
+    assert pp["plan"]["pp"] == 4 and pp["plan"]["strategy"] == "pp" and pp["plan"]["comm_measured"]
+    assert 0 < pp["bubble_fraction"] < 1 and pp["p2p_gbps"] > 0 and pp["p2p_bytes"] > 0
 
 
 def _gpt2_8rank(extra_env=None, timeout=900, extra_args=()):

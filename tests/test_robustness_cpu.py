@@ -300,3 +300,33 @@ def _w_corrupt(rank, world, policy):
 @pytest.mark.parametrize("policy", ["skip", "raise"])
 def test_corrupt_gradients_skipped_or_raised_on_every_rank(policy):
     run_dist(_w_corrupt, 2, policy)
+
+
+def _w_plan_measure(rank, world, fault_rank):
+    import torch.distributed as dist
+
+    from madnn.config import Config
+    from madnn.planner import plan_model
+
+    if fault_rank is not None:
+        os.environ["MADNN_FAULT_MEASURE"] = str(fault_rank)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.Tanh(), torch.nn.Linear(64, 64), torch.nn.Tanh(),
+                                torch.nn.Linear(64, 4))
+    cfg = Config.from_env(strategy="auto", measure=True, dtype="float32")
+    plan = plan_model(model, cfg, world=world, example_input=torch.zeros(8, 16), global_batch=16)
+    assert plan.measured == (fault_rank is None)
+    # the measured links of this job priced the plan, identically on every rank
+    assert plan.comm_probe["world"] == world and plan.comm_probe["p2p_gbps"] > 0
+    mine = [(round(c.fwd_s, 12), round(c.bwd_s, 12)) for c in plan.costs] + [plan.describe()]
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    assert all(g == got[0] for g in got)
+
+
+@pytest.mark.parametrize("fault_rank", [None, 1, 0])
+def test_planner_measurement_failure_is_agreed_not_hung(fault_rank):
+    """One rank's layer timing raising (MADNN_FAULT_MEASURE) makes EVERY rank fall back to the
+    analytic costs -- no rank is left blocked in the results all-gather -- and all ranks plan the
+    same placement; without a fault the CPU timings are used."""
+    run_dist(_w_plan_measure, 2, fault_rank)
