@@ -272,9 +272,11 @@ def _after_plain_step(engine: DataParallel):
 # Reference-compatible surface
 # --------------------------------------------------------------------------
 def _flat_collective(tensors, op: str, group=None, src: int = 0, scale: float = 1.0) -> int:
-    """One collective per (device, dtype) class of ``tensors``: K4 pack into a flat buffer of
-    the class's own dtype (a bf16 model moves bf16 bytes), the collective chosen by the
-    selector (R9), K4 unpack with ``scale`` fused.  Returns the number of collectives issued."""
+    """One collective per (device, dtype) class of ``tensors``: K4 pack into a flat buffer, the
+    collective chosen by the selector (R9), K4 unpack with ``scale`` fused.  A broadcast moves
+    the class's own dtype (a bf16 model moves bf16 bytes: the values are copied, not combined);
+    a SUM all-reduce packs into fp32 (the K4 cast is free), so a bf16 model's W-rank sum is not
+    rounded to bf16 before the 1/W scale.  Returns the number of collectives issued."""
     classes = {}
     for t in tensors:
         if t is not None:
@@ -285,7 +287,8 @@ def _flat_collective(tensors, op: str, group=None, src: int = 0, scale: float = 
         for t in ts:
             offs.append(n)
             n += (t.numel() + 15) // 16 * 16
-        flat = torch.zeros(n, dtype=dt if dt.is_floating_point else torch.float32, device=dev)
+        fdt = dt if (dt.is_floating_point and op == "broadcast") else torch.float32
+        flat = torch.zeros(n, dtype=fdt, device=dev)
         ops.bucket_pack(ts, flat, offs, 1.0)
         coll = comm.select(flat, op, group)
         if op == "broadcast":
@@ -436,8 +439,10 @@ def parallelize(data, targets, model: nn.Module, size: Optional[int] = None, syn
 class Trainer:
     """Minibatch SGD trainer with the reference trainer's knobs and hooks (R8,
     datamodule.lua:117-184): ``learning_rate``, ``learning_rate_decay``, ``max_iteration``
-    (epochs), ``shuffle``, ``on_example`` (after every minibatch; reference ``hookExample``) and
-    ``on_iteration`` (after every epoch; ``hookIteration``).  Synchronisation is whatever the
+    (epochs; ``<= 0`` = no limit, stop by raising ``StopIteration`` from ``on_iteration``),
+    ``shuffle``, ``on_example`` (after every minibatch; reference ``hookExample``) and
+    ``on_iteration(trainer, iteration, error)`` (after every epoch, 1-based ``iteration``;
+    ``hookIteration``).  Synchronisation is whatever the
     model carries: a ``parallelize`` periodic hook, a ``distribute`` engine, or nothing.
 
     Reference fidelity:
@@ -509,9 +514,15 @@ class Trainer:
         self._partial = tuple(sd.get("partial", (0.0, 0)))
 
     def train(self, data, targets) -> list:
+        """Epochs over (``data``, ``targets``) in minibatches of ``batch_size``.  ``max_iteration``
+        epochs, or -- ``max_iteration <= 0``, as the reference (datamodule.lua:178) -- until
+        ``on_iteration`` raises ``StopIteration``.  ``on_iteration(trainer, iteration, error)`` gets
+        the 1-based epoch number (reference ``hookIteration(self, iteration, currentError)``,
+        datamodule.lua:169-170)."""
         n = len(data)
         log = get_logger()
-        for epoch in range(self.epoch, self.max_iteration):
+        epoch = self.epoch
+        while self.max_iteration <= 0 or epoch < self.max_iteration:
             lr = self._lr(epoch)
             for g in self.optimizer.param_groups:
                 g["lr"] = lr
@@ -554,8 +565,13 @@ class Trainer:
                 log.info("# current error = %.6f (epoch %d, lr %.5g)", err, epoch + 1, lr)
             self.epoch = epoch + 1
             self.cursor, self._partial = 0, (0.0, 0)
+            epoch += 1
             if self.on_iteration is not None:
-                self.on_iteration(self, epoch, err)
+                try:
+                    self.on_iteration(self, epoch, err)     # 1-based, like the reference
+                except StopIteration:
+                    return self.history
         if self.verbose:
             log.info("# StochasticGradient: you have reached the maximum number of iterations")
+            log.info("# training error = %.6f", self.history[-1] if self.history else float("nan"))
         return self.history

@@ -401,15 +401,39 @@ def load(path: str, engine, optimizer=None, strict: bool = True, sampler=None, t
 def _load_resume_state(path: str, engine, meta: dict) -> Optional[dict]:
     c = _coords(engine)
     f = os.path.join(path, f"state-{_coord_name(c)}.pt")
+    mapped = None
     if not os.path.exists(f):
         saved = meta.get("mesh") or {"dp": meta.get("world", 1), "pp": 1, "tp": 1}
-        c = {"dp": c["dp"] % max(int(saved["dp"]), 1), "pp": min(c["pp"], int(saved["pp"]) - 1),
-             "tp": c["tp"] % max(int(saved["tp"]), 1)}
-        f = os.path.join(path, f"state-{_coord_name(c)}.pt")
+        mapped = {"dp": c["dp"] % max(int(saved["dp"]), 1), "pp": min(c["pp"], int(saved["pp"]) - 1),
+                  "tp": c["tp"] % max(int(saved["tp"]), 1)}
+        f = os.path.join(path, f"state-{_coord_name(mapped)}.pt")
     if not os.path.exists(f):
         legacy = os.path.join(path, f"rng-rank{rt.get_rank()}.pt")   # round-2 checkpoints
         if not os.path.exists(legacy):
             return None
         rng = torch.load(legacy, weights_only=True)
         return {"rng_cpu": rng["cpu"], **({"rng_cuda": rng["cuda"]} if "cuda" in rng else {})}
-    return torch.load(f, weights_only=True)
+    st = torch.load(f, weights_only=True)
+    if mapped is not None and mapped != c:
+        # a rank with no saved state of its own (resumed on a larger mesh) borrows another
+        # coordinate's state: fold ITS coordinates into the RNG streams, or it would draw the
+        # same dropout masks as the rank it borrowed from
+        st["rng_cpu"] = _fold_rng(st["rng_cpu"], c)
+        if "rng_cuda" in st:
+            st["rng_cuda"] = _fold_rng(st["rng_cuda"], c)
+    return st
+
+
+def _fold_rng(state: torch.Tensor, coords: dict) -> torch.Tensor:
+    """A new generator state derived from ``state`` and the mesh coordinates (deterministic)."""
+    import hashlib
+
+    h = hashlib.sha256(state.numpy().tobytes() + repr(sorted(coords.items())).encode()).digest()
+    g = torch.Generator()
+    g.manual_seed(int.from_bytes(h[:8], "little") & ((1 << 63) - 1))
+    if state.numel() == g.get_state().numel():
+        return g.get_state()
+    # a device generator state (philox seed + offset): reseed its seed field
+    out = state.clone()
+    out[:8] = torch.tensor(list(h[:8]), dtype=torch.uint8)
+    return out

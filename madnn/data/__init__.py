@@ -107,10 +107,15 @@ def synthetic_batch(kind: str, batch: int, device, dtype=torch.bfloat16, **kw):
 class DistributedSampler(torch.utils.data.Sampler):
     """Contiguous-stripe sampler with per-epoch shuffling inside the shard.
 
-    Resumable: it counts the indices it has handed out this epoch (``cursor``); after
-    :meth:`load_state_dict` the next iteration continues mid-epoch exactly where the saved
-    one stopped (same permutation: it is a function of seed + epoch only).  Restored at a
-    different world size the position is carried over in GLOBAL samples consumed."""
+    Resumable: after :meth:`load_state_dict` the next iteration continues mid-epoch exactly
+    where the saved one stopped (same permutation: it is a function of seed + epoch only).
+    Restored at a different world size the position is carried over in GLOBAL samples.
+
+    What is saved is the number of samples the TRAINING LOOP consumed this epoch, not the
+    indices handed out: a DataLoader with workers, or madnn's :class:`DevicePrefetcher`, pulls
+    batches ahead of the one being trained on, and saving the hand-out position would skip
+    those on resume.  Iterate through :meth:`track` (it counts a batch when it reaches the loop)
+    or call :meth:`advance` after each step; without either, the hand-out position is saved."""
 
     def __init__(self, n: int, rank: Optional[int] = None, world: Optional[int] = None, shuffle: bool = True,
                  remainder: str = "drop", seed: int = 0):
@@ -119,15 +124,41 @@ class DistributedSampler(torch.utils.data.Sampler):
         self.world = rt.get_world_size() if world is None else world
         self.shuffle, self.remainder, self.seed = shuffle, remainder, seed
         self.epoch = 0
-        self.cursor = 0          # indices of this epoch already yielded
+        self.cursor = 0          # indices of this epoch already yielded (may run ahead of training)
+        self.consumed = 0        # samples of this epoch the training loop has taken (track / advance)
+        self._tracked = False
 
     def set_epoch(self, e: int):
         if e != self.epoch:
             self.cursor = 0
+            self.consumed = 0
         self.epoch = e
 
+    def advance(self, n: int) -> None:
+        """The training loop finished ``n`` more samples of this epoch."""
+        self._tracked = True
+        self.consumed += int(n)
+
+    def track(self, batches, batch_size: Optional[int] = None):
+        """Yield from ``batches`` (a DataLoader / DevicePrefetcher over this sampler), counting
+        each batch as consumed when it reaches the caller: a checkpoint taken in the loop body
+        after the step resumes at the next unseen batch, however far the loader prefetched."""
+        self._tracked = True
+        for b in batches:
+            if batch_size is not None:
+                n = batch_size
+            else:
+                first = b[0] if isinstance(b, (list, tuple)) else b
+                n = len(first)
+            self.consumed += n
+            yield b
+
+    def position(self) -> int:
+        """The resume position: consumed samples when the loop reports them, else handed out."""
+        return min(self.consumed, self.cursor) if self._tracked else self.cursor
+
     def state_dict(self) -> dict:
-        return {"n": self.n, "epoch": self.epoch, "cursor": self.cursor, "seed": self.seed, "world": self.world,
+        return {"n": self.n, "epoch": self.epoch, "cursor": self.position(), "seed": self.seed, "world": self.world,
                 "shuffle": self.shuffle, "remainder": self.remainder}
 
     def load_state_dict(self, sd: dict) -> None:
@@ -138,6 +169,7 @@ class DistributedSampler(torch.utils.data.Sampler):
         if int(sd.get("world", self.world)) != self.world:
             cur = cur * int(sd["world"]) // self.world   # same global position
         self.cursor = min(cur, len(self))
+        self.consumed = self.cursor
 
     def _indices(self):
         if self.remainder == "pad":

@@ -198,7 +198,7 @@ class _NormFn(torch.autograd.Function):
                                                   ctx.colsum, ctx.colsum_bf16)
         dx = dx.view(ctx.shape)
         if ctx.colsum:
-            dx._madnn_colsum = cs
+            _attach(dx, "_madnn_colsum", cs)
         return dx, (dx if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None, None
 
 
@@ -248,6 +248,34 @@ def rms_norm(x, weight, eps: float = 1e-6, residual: Optional[torch.Tensor] = No
     return _norm(x, weight, None, eps, True, residual, fork)
 
 
+def _attach(t: torch.Tensor, name: str, value) -> None:
+    """Side-channel a by-product (a column sum, a bit mask, BN partial sums) onto the gradient
+    tensor ``t`` it describes, stamped with ``t``'s version counter: if autograd later accumulates
+    another consumer's gradient into ``t`` in place, the stamp no longer matches."""
+    setattr(t, name, (value, t._version))
+
+
+def _attached(t: Optional[torch.Tensor], name: str, strict: bool = False):
+    """The by-product :func:`_attach` put on ``t`` (or on the base ``t`` views), or None when
+    there is none or ``t`` was modified since; ``strict`` raises instead for by-products whose
+    absence changes the meaning of ``t`` (a deferred ReLU mask)."""
+    if t is None:
+        return None
+    rec = getattr(t, name, None)
+    if rec is None and t._base is not None and t.numel() == t._base.numel():
+        rec = getattr(t._base, name, None)
+    if rec is None:
+        return None
+    value, version = rec
+    if t._version != version:
+        if strict:
+            raise RuntimeError(f"madnn: gradient carrying {name} was modified in place after it was produced "
+                               "(a second consumer's gradient accumulated into it); disable the deferral "
+                               "(MADNN_DEFER_RES_MASK=0) for this model")
+        return None
+    return value
+
+
 # ---------------------------------------------------------------------- K5
 class _BNFn(torch.autograd.Function):
     @staticmethod
@@ -277,7 +305,7 @@ class _BNFn(torch.autograd.Function):
         x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         defer = ctx.defer and dy.dtype == x.dtype and dy.stride() == x.stride()
-        part = getattr(dy, "_madnn_bnpart", None)
+        part = _attached(dy, "_madnn_bnpart")
         if part is not None and ctx.has_res and dy.dtype == x.dtype and dy.stride() == x.stride():
             # the reduction came from the K9 data grad that produced dy (_Conv1x1Fn, conv1x1_dgrad_bnres)
             dx, dw, db, dres = torch.ops.madnn.bn_bwd_ext_res(dy, x, weight, mean, invstd, scale, shift, part,
@@ -287,7 +315,7 @@ class _BNFn(torch.autograd.Function):
                                                       mean, invstd, scale, shift, ctx.relu, need_w, not defer)
         if defer:
             dres = dy.view_as(dy)
-            dres._madnn_resmask = mask
+            _attach(dres, "_madnn_resmask", mask)
         return (dx, dw if need_w else None, db if need_w else None, dres if ctx.has_res else None,
                 None, None, None, None, None, None, None, None)
 
@@ -552,7 +580,7 @@ class _AttnPackedFn(torch.autograd.Function):
             cs = torch.empty((heads + 2 * kv_heads) * qkv.size(-1), dtype=ctx.colsum_dtype, device=qkv.device)
         torch.ops.madnn.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, causal, scale, cs)
         if cs is not None:
-            dqkv._madnn_colsum = cs
+            _attach(dqkv, "_madnn_colsum", cs)
         return dqkv, None, None, None, None
 
 
@@ -661,7 +689,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.fork == 2:
             sub, dfork = dfork, None
         # a deferred ReLU mask (_BNFn): the identity gradient is dfork where its bit is set
-        resmask = getattr(dfork, "_madnn_resmask", None) if dfork is not None else None
+        resmask = _attached(dfork, "_madnn_resmask", strict=True)
         res = _nhwc(dfork.to(x.dtype)) if dfork is not None else None
         if resmask is not None and not (ctx.needs_input_grad[0] and dgrad == "k9"):
             res, resmask = _apply_bit_mask(res, resmask), None
@@ -672,7 +700,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 # this epilogue, over the gradient it writes (no reduction pass over dx and y)
                 bny, bnmask = ctx.saved_tensors[2:]
                 dx, part = torch.ops.madnn.conv1x1_dgrad_bnres(dy, w, res, resmask, bny, bnmask)
-                dx._madnn_bnpart = part
+                _attach(dx, "_madnn_bnpart", part)
             elif dgrad == "k9" and sub is not None and res is None and SUB_IN_DGRAD and x.dim() == 4:
                 # the downsample path's compact gradient is added at the even pixels in the epilogue
                 dx = torch.ops.madnn.conv1x1_dgrad(dy, w, _nhwc(sub.to(x.dtype)), None, True)
@@ -1450,9 +1478,7 @@ class _LinearFn(torch.autograd.Function):
                 db = None
         elif ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
             # from the consumer's backward (_NormFn, _AttnPackedFn); a reshaped view keeps it on its base
-            cs = getattr(g, "_madnn_colsum", None)
-            if cs is None and g._base is not None and g.numel() == g._base.numel():
-                cs = getattr(g._base, "_madnn_colsum", None)
+            cs = _attached(g, "_madnn_colsum")
             if cs is not None and cs.numel() == g.shape[-1]:
                 db = cs.to(ctx.bias_dtype)
             else:

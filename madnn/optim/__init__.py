@@ -161,9 +161,19 @@ class _FlatOptimizer(torch.optim.Optimizer):
             else:
                 gs.finalize_grads()
         cached = getattr(self, "_grads_cached", None)
-        if self.nonfinite != "ignore" and not self._grads_finite(late, cached):
+        if self.nonfinite != "ignore":
+            finite = self._grads_finite(late, cached)
+            cached = getattr(self, "_grads_cached", None)   # packed by the check in local-pack mode
+        else:
+            finite = True
+        if not finite:
             self.skipped_steps += 1
             if self.nonfinite == "raise":
+                # nothing of this step survives into the next one: a caller that catches the
+                # error, zeroes its gradients and continues must not get these packed NaN flats
+                # (or the NaN clip scale) back
+                self._grads_cached = None
+                self._dscale = None
                 raise NonFiniteGradients(f"non-finite gradients at optimizer step {self.skipped_steps}")
             from ..utils.logging import get_logger
 

@@ -176,6 +176,14 @@ def _w_mid_epoch(rank, world, path, phase):
         return
     meta = ckpt.load(path, eng, opt, sampler=sampler)
     assert meta["step"] == 11
+    if phase == "replan":
+        # ranks 2 and 3 borrow the saved states of ranks 0 and 1 but must not share their
+        # random streams (dropout masks), ADVICE r3
+        import torch.distributed as dist
+
+        states = [None] * world
+        dist.all_gather_object(states, torch.get_rng_state().tolist())
+        assert len({tuple(st) for st in states}) == world
     gen = batches()
     losses = torch.stack([step(next(gen)) for _ in range(5 if phase == "resume" else 2)])
     if phase == "resume":
@@ -233,3 +241,35 @@ def test_parallelize_trainer_resume_mid_epoch(tmp_path):
     path = str(tmp_path / "tr")
     run_dist(_w_trainer_resume, 2, path, "save")
     run_dist(_w_trainer_resume, 2, path, "resume")
+
+
+def test_sampler_resume_counts_consumed_not_prefetched():
+    """A DataLoader with workers pulls batches ahead of training; the saved position is what the
+    loop consumed (``DistributedSampler.track``), so resume continues at the first UNtrained
+    batch instead of skipping the prefetched ones."""
+    from madnn.data import DistributedSampler
+
+    data = torch.arange(64)
+    ds = torch.utils.data.TensorDataset(data)
+    s = DistributedSampler(64, rank=0, world=1, shuffle=True, seed=3)
+    loader = torch.utils.data.DataLoader(ds, batch_size=4, sampler=s, num_workers=2, prefetch_factor=2)
+    seen = []
+    for i, (b,) in enumerate(s.track(loader)):
+        seen += b.tolist()
+        if i == 4:
+            sd = s.state_dict()
+            ahead = s.cursor
+            break
+    assert sd["cursor"] == 20 and ahead > 20          # the workers had handed out more
+    r = DistributedSampler(64, rank=0, world=1, shuffle=True, seed=3)
+    r.load_state_dict(sd)
+    rest = list(iter(r))
+    full = list(iter(DistributedSampler(64, rank=0, world=1, shuffle=True, seed=3)))
+    assert seen == full[:20] and rest == full[20:]
+    # the hand-loop API: advance() after each step
+    a = DistributedSampler(64, rank=0, world=1, shuffle=False)
+    it = iter(a)
+    for _ in range(8):
+        next(it)                  # 8 handed out (a prefetching loop) ...
+    a.advance(4)                  # ... 4 trained
+    assert a.state_dict()["cursor"] == 4

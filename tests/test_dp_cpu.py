@@ -202,10 +202,14 @@ def _w_parallelize(rank, world, sync_every):
     torch.testing.assert_close(d, data[rank * size:(rank + 1) * size])  # contiguous stripe, remainder dropped
     if sync_every is None:
         assert model._madnn_sync.period == 1  # heuristic: local size < 1000
-    lrs = []
+    lrs, iters = [], []
+
+    def hook(tr, it, err):
+        lrs.append(tr.optimizer.param_groups[0]["lr"])
+        iters.append(it)
+
     trainer = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.5, learning_rate_decay=0.1,
-                            max_iteration=6, batch_size=16, verbose=False,
-                            on_iteration=lambda tr, ep, err: lrs.append(tr.optimizer.param_groups[0]["lr"]))
+                            max_iteration=6, batch_size=16, verbose=False, on_iteration=hook)
     from madnn.optim import FusedSGD
 
     assert isinstance(trainer.optimizer, FusedSGD)  # the reference's fused accUpdateGradParameters
@@ -214,6 +218,19 @@ def _w_parallelize(rank, world, sync_every):
     assert trainer.optimizer.space is not None and len(trainer.optimizer.space.buckets) >= 1
     # reference schedule (datamodule.lua:176-177): epoch 1 at lr, epoch k >= 2 at lr / (1 + k * decay)
     assert lrs == pytest.approx([0.5] + [0.5 / (1 + k * 0.1) for k in range(2, 7)])
+    # hookIteration receives the 1-based iteration (datamodule.lua:169-170)
+    assert iters == [1, 2, 3, 4, 5, 6]
+    # maxIteration <= 0: no limit (datamodule.lua:178); the hook ends training with StopIteration
+    seen = []
+
+    def stop_at_3(tr, it, err):
+        seen.append(it)
+        if it == 3:
+            raise StopIteration
+
+    t2 = madnn.Trainer(model, torch.nn.CrossEntropyLoss(), learning_rate=0.05, max_iteration=0, batch_size=16,
+                       verbose=False, on_iteration=stop_at_3)
+    assert len(t2.train(d, t)) == 3 and seen == [1, 2, 3] and t2.epoch == 3
     if sync_every == -1:
         madnn.synchronize_model(model)
     for p in model.parameters():
@@ -421,3 +438,25 @@ def _w_bf16_reduce(rank, world, out_dir):
 
 def test_bf16_reduce_tracks_fp32_reduce_at_8_ranks(tmp_path):
     run_dist(_w_bf16_reduce, 8, str(tmp_path))
+
+
+def _w_bf16_sync(rank, world):
+    import madnn
+
+    torch.manual_seed(0)
+    base = torch.randn(257, 33)
+    m = torch.nn.Linear(33, 257).to(torch.bfloat16)
+    with torch.no_grad():
+        m.weight.copy_((base * (1 + rank / 7.0)).to(torch.bfloat16))
+        m.bias.fill_(1.0 + rank * 2 ** -9)
+    want_w = sum((base * (1 + r / 7.0)).to(torch.bfloat16).float() for r in range(world)) / world
+    want_b = sum(torch.tensor(1.0 + r * 2 ** -9).to(torch.bfloat16).float() for r in range(world)) / world
+    madnn.synchronize_model(m, grads=False)
+    # one rounding of the fp32 mean, not a bf16 running sum
+    assert torch.equal(m.weight, want_w.to(torch.bfloat16))
+    assert torch.equal(m.bias, want_b.to(torch.bfloat16).expand_as(m.bias))
+
+
+def test_bf16_synchronize_model_sums_in_fp32():
+    """averaging a bf16 model reduces the W-rank sum in fp32 (8 ranks)."""
+    run_dist(_w_bf16_sync, 8)

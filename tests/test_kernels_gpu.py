@@ -741,3 +741,34 @@ def test_norm_colsum_feeds_linear_bias_grad(cuda, monkeypatch, mode):
 
     run(xf, wf, bf, rf, torch.nn.functional.linear, fnorm).backward()
     assert _rel(b.grad, bf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2 and _rel(x.grad, xf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("second", ["add", "inplace"])
+def test_linear_bias_grad_with_two_consumers(cuda, second):
+    """A biased Linear whose output feeds the LayerNorm (which hands the Linear its bias gradient
+    as a column sum of the gradient it produces) AND another op: the accumulated gradient is no
+    longer the one the column sum describes, so the bias gradient must come from the sum (ADVICE
+    r3: version-stamped side channels)."""
+    torch.manual_seed(0)
+    M, K, N = 256, 128, 256
+    x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * K ** -0.5).requires_grad_()
+    b = (torch.randn(N, device=cuda, dtype=torch.float32) * 0.1).requires_grad_()
+    lw = torch.ones(N, device=cuda, dtype=torch.float32, requires_grad=True)
+    lb = torch.zeros(N, device=cuda, dtype=torch.float32, requires_grad=True)
+
+    def fwd(xx, ww, bb, lww, lbb, ref):
+        y = madnn.ops.linear(xx, ww, bb) if not ref else torch.nn.functional.linear(xx, ww, bb)
+        z = madnn.ops.layer_norm(y, lww, lbb) if not ref else torch.nn.functional.layer_norm(y, (N,), lww, lbb)
+        if second == "add":
+            return z.float().sum() + (y.float() * 3.0).sum()
+        y2 = y * 1.0
+        y2.mul_(3.0)
+        return z.float().sum() + y2.float().sum()
+
+    fwd(x, w, b, lw, lb, False).backward()
+    xf, wf, bf = (t.detach().float().requires_grad_() for t in (x, w, b))
+    lwf, lbf = lw.detach().clone().requires_grad_(), lb.detach().clone().requires_grad_()
+    fwd(xf, wf, bf, lwf, lbf, True).backward()
+    assert _rel(b.grad, bf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 3e-2
