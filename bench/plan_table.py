@@ -21,16 +21,20 @@ def cases():
     from madnn.models.gpt2 import GPT2, gpt2_config
     from madnn.models.llama import Llama, llama_config
 
-    # (name, builder, example input per sample batch, global batch per GPU, optimizer kind, checkpointing)
+    # (name, builder, example input per sample batch, global batch per GPU, optimizer kind, checkpointing,
+    #  config overrides)
     return [
         ("ResNet-50 (bench: 2048 images/GPU)", lambda: resnet50(),
-         lambda b: torch.randn(b, 3, 224, 224), 2048, "sgd", "none"),
-        ("GPT-2 medium (bench: 64 x 1024 tokens/GPU)", lambda: GPT2(gpt2_config("gpt2-medium")),
-         lambda b: torch.zeros(b, 1024, dtype=torch.long), 64, "adam", "none"),
+         lambda b: torch.randn(b, 3, 224, 224), 2048, "sgd", "none", {}),
+        ("GPT-2 medium (64 x 1024 tokens/GPU, unconstrained)", lambda: GPT2(gpt2_config("gpt2-medium")),
+         lambda b: torch.zeros(b, 1024, dtype=torch.long), 64, "adam", "none", {}),
+        ("GPT-2 medium (bench's pipeline half: 4 stages pinned, everything else automatic)",
+         lambda: GPT2(gpt2_config("gpt2-medium")), lambda b: torch.zeros(b, 1024, dtype=torch.long), 64, "adam",
+         "none", {"pp_stages": 4}),
         ("BERT-large (64 x 512/GPU, checkpointing auto)", lambda: BertForPreTraining(bert_config("bert-large")),
-         lambda b: torch.zeros(b, 512, dtype=torch.long), 64, "adam", "auto"),
+         lambda b: torch.zeros(b, 512, dtype=torch.long), 64, "adam", "auto", {}),
         ("Llama-3 8B (4 x 2048/GPU, checkpointing auto)", lambda: Llama(llama_config("llama3-8b")),
-         lambda b: torch.zeros(b, 2048, dtype=torch.long), 4, "adam", "auto"),
+         lambda b: torch.zeros(b, 2048, dtype=torch.long), 4, "adam", "auto", {}),
     ]
 
 
@@ -46,7 +50,7 @@ def main():
     lines = [f"# Planner placements at {a.world} GPUs "
              f"({'measured layer costs on ' + torch.cuda.get_device_name(0) if torch.cuda.is_available() else 'analytic costs'})",
              ""]
-    for name, build, example, per_gpu, opt, ckpt in cases():
+    for name, build, example, per_gpu, opt, ckpt, over in cases():
         if a.only and a.only.lower() not in name.lower():
             continue
         t0 = time.time()
@@ -54,11 +58,16 @@ def main():
             model = build()
         cfg = Config()
         cfg.checkpointing = ckpt
+        for k, v in over.items():
+            setattr(cfg, k, v)
         optim = torch.optim.SGD if opt == "sgd" else torch.optim.AdamW
         plan = plan_model(model, cfg, a.world, example_input=example(1), global_batch=per_gpu * a.world,
                           optimizer=optim([torch.nn.Parameter(torch.zeros(1))], lr=0.1))
-        lines += [f"## {name}", "", f"choice: **{plan.strategy}** dp={plan.dp} pp={plan.pp} "
-                  f"(planned in {time.time() - t0:.1f} s)", "", plan.table(), ""]
+        hw = getattr(plan, "machine", None)
+        lines += [f"## {name}", "", f"choice: **{plan.describe()}** (planned in {time.time() - t0:.1f} s)", "",
+                  f"links priced at: all-reduce eff {hw.allreduce_eff:.2f} x {hw.link_gbps:.0f} GB/s per link, "
+                  f"P2P {hw.p2p_gbps:.0f} GB/s ({hw.source}; a job at W > 1 replaces these with its own "
+                  "measurement, comm.probe)" if hw else "", "", plan.table(), ""]
         print("\n".join(lines[-6:]), flush=True)
     txt = "\n".join(lines) + "\n"
     if a.out:
