@@ -683,3 +683,43 @@ def test_step_profiler_writes_a_trace(tmp_path):
     trace = (tmp_path / "trace-rank0.json").read_text()
     assert "addmm" in trace or "linear" in trace
     assert isinstance(kernel_table(prof), str)
+
+
+def test_shipped_tuning_table_covers_bench_shapes(monkeypatch):
+    """The shipped per-shape table (madnn/tuning/choices_gfx950.json) holds every weight-gradient
+    and GELU-Linear shape of the bench configurations, so a bench process times nothing at start
+    (round 3: 76 s of first-step timing + MIOpen search, profiles/r4_first_steps_*.json)."""
+    import madnn.ops as ops
+
+    assert ops._TUNE["table"] and ops._TUNE["table"].endswith("choices_gfx950.json")
+    # ResNet-50 at 2048 and 512 images: the layer1 1x1 conv3 weight gradient, the 3x3 of layer4
+    for b in (2048, 512):
+        assert ("conv1x1", b * 56 * 56, 256, 64) in ops._WGRAD_CHOICE
+        assert ("conv3x3", b, 512, 7, 7, 512) in ops._WGRAD_CHOICE
+    # GPT-2 medium at every microbatch the pipeline planner may pick (4 .. 64 sequences)
+    for b in (4, 8, 16, 32, 64):
+        assert ("linear", b * 1024, 4096, 1024) in ops._WGRAD_CHOICE
+
+    def boom(*a, **k):
+        raise AssertionError("a shipped shape was timed")
+
+    monkeypatch.setattr(ops, "_time_wgrad", boom)
+    called = []
+    key = ("conv1x1", 2048 * 56 * 56, 256, 64)
+    ops.tuned_wgrad(key, lambda: called.append("lib"), lambda: called.append("k12"))
+    assert called == [ops._WGRAD_CHOICE[key]] and ops.tuning_timings() == 0
+
+
+def test_tuning_table_roundtrip(tmp_path):
+    import madnn.ops as ops
+
+    p = tmp_path / "t.json"
+    ops.export_choices(str(p))
+    saved = dict(ops._WGRAD_CHOICE)
+    ops._WGRAD_CHOICE.clear()
+    try:
+        assert ops.load_tuning_table(str(p)) >= len(saved)
+        assert ops._WGRAD_CHOICE == saved
+    finally:
+        ops._WGRAD_CHOICE.update(saved)
+        ops.load_tuning_table()
