@@ -200,7 +200,7 @@ class DataParallel(nn.Module):
             ev.record(torch.cuda.current_stream(bk.model.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                if "comm_start" not in self._ev:
+                if "comm_start" not in self._ev and self._timing():
                     self._ev["comm_start"] = torch.cuda.Event(enable_timing=True)
                     self._ev["comm_start"].record(self.comm_stream)
                 for p in bk.params:
@@ -237,7 +237,7 @@ class DataParallel(nn.Module):
         no gradient and mark the step for finalisation.  Runs from the autograd end callback,
         or -- with ``defer_flush`` (the pipeline engine, whose chunks finish their last
         microbatch at different times) -- explicitly after the LAST backward."""
-        if self.is_cuda:
+        if self._timing():
             self._ev["bwd_end"] = torch.cuda.Event(enable_timing=True)
             self._ev["bwd_end"].record()
         for bk in self.space.buckets:
@@ -258,7 +258,7 @@ class DataParallel(nn.Module):
                     if bk.work is not None:
                         bk.work.wait()  # comm stream waits for the collective
                         bk.work = None
-                if record_end and "comm_start" in self._ev:
+                if record_end and "comm_start" in self._ev and self._timing():
                     self._ev["comm_end"] = torch.cuda.Event(enable_timing=True)
                     self._ev["comm_end"].record(self.comm_stream)
             cur.wait_stream(self.comm_stream)
@@ -281,7 +281,7 @@ class DataParallel(nn.Module):
         if not self._needs_finalize:
             return
         cur = self._wait_works(record_end=True)
-        if self.is_cuda and "bwd_end" in self._ev:
+        if self._timing() and "bwd_end" in self._ev:
             self._ev["final"] = torch.cuda.Event(enable_timing=True)
             self._ev["final"].record(cur)
         self._last_ev, self._ev = (self._ev, self._step_bytes), {}
@@ -293,6 +293,12 @@ class DataParallel(nn.Module):
                 for p in bk.params:
                     p.grad = None
         self._needs_finalize = False
+
+    def _timing(self) -> bool:
+        """Per-step timing events (comm_metrics) -- not while the step is captured in a graph."""
+        from ..utils.graphs import capturing
+
+        return self.is_cuda and not capturing()
 
     def comm_metrics(self) -> dict:
         """Comm numbers of the last finalized step (blocks on that step's events only):

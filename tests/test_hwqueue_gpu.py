@@ -1,0 +1,44 @@
+"""The hardware-queue probe kernels (madnn/ops/csrc/probe.hip) on the device.
+
+The probe is what showed that HIP streams of one process share GPU_MAX_HW_QUEUES hardware
+queues and serialise across them (profiles/r4_hwqueue_probe_q4.json), the reason the pipeline
+transport is built to complete even fully serialised (madnn/parallel/pp.py: issue_plan).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(wait_stream, set_stream, value, timeout_us):
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.zeros(2, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(wait_stream):
+        torch.ops.madnn.hwq_wait(flag, value, timeout_us, out)
+    with torch.cuda.stream(set_stream):
+        torch.ops.madnn.hwq_set(flag, value)
+    torch.cuda.synchronize()
+    return out.tolist()
+
+
+def test_probe_wait_is_bounded_behind_its_own_setter(cuda):
+    """Waiter and setter on ONE stream: the setter runs only after the waiter gave up, so the
+    waiter reports a timeout after ~timeout_us -- the bounded spin cannot hang the queue."""
+    import madnn.ops as ops
+
+    assert ops.load_kernels()
+    s = torch.cuda.Stream()
+    ok, ticks = _pair(s, s, 7, 2000)
+    assert ok == 0 and 150_000 <= ticks <= 2_000_000   # 100 MHz ticks: >= 1.5 ms waited
+
+
+def test_probe_sees_a_setter_on_another_priority_queue(cuda):
+    """The high-priority stream pool has hardware queues of its own (measured: default and
+    low-priority streams never share one with it), so a setter there reaches a waiter on the
+    compute stream within microseconds."""
+    import madnn.ops as ops
+
+    assert ops.load_kernels()
+    ok, ticks = _pair(torch.cuda.default_stream(), torch.cuda.Stream(priority=-1), 11, 200_000)
+    assert ok == 1 and ticks < 10_000_000
