@@ -70,6 +70,8 @@ def parse():
                          "pinned dp | pp | dp_pp | tp")
     ap.add_argument("--gpt2-strategy", default="auto",
                     help="GPT-2 placement: auto (planner; only the stage count is pinned) or pp / dp_pp")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="ResNet-50: replay the whole training step as one hipGraph (madnn.utils.graphs)")
     ap.add_argument("--no-pg", action="store_true", help="no world-1 process group when run without a launcher")
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
@@ -151,15 +153,28 @@ def bench_resnet(args, world, rank):
         return loss
 
     tw = time.perf_counter()
-    for _ in range(args.warmup):
-        step()
+    run = step
+    if args.graph and dev.type == "cuda":
+        # the whole step (forward, backward with the bucketed all-reduce, optimizer) as ONE
+        # hipGraph replay: the warm-up steps run eagerly inside capture_step, then one replay
+        from madnn.utils.graphs import capture_step
+
+        run = capture_step(step, warmup=max(args.warmup, 3))
+        run()
+    else:
+        for _ in range(args.warmup):
+            step()
     _sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     _sync_all()
     dt = time.perf_counter() - t0
+    if run is not step:
+        step()   # one eager step after the timed region: its comm events feed comm_metrics
+        _sync_all()
     out = (dt, per_gpu * world, {"warmup_s": round(t0 - tw, 1), "model": "resnet50", "global_batch": per_gpu * world,
+                                 "graph": run is not step,
                                  "per_gpu_batch": per_gpu, "seq_len": None,
                                  "image": [3, args.image_size, args.image_size],
                                  "parallelism": _parallelism(plan, world),
