@@ -44,6 +44,15 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
+    import threading
+
+    def heartbeat():      # measured layer costs take minutes per model: show progress
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            print(f"[plan_table] still planning ({time.time() - t0:.0f} s)", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     from madnn.config import Config
     from madnn.planner import plan_model
 

@@ -112,6 +112,8 @@ hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int,
                               hipStream_t);
 hipError_t madnn_hwq_wait(const int*, int, int64_t, int*, hipStream_t);
 hipError_t madnn_hwq_set(int*, int, hipStream_t);
+hipError_t madnn_hwq_batch(const int*, const int*, int, int*, int*, int, int64_t, int*, const int*, hipStream_t);
+hipError_t madnn_hwq_spin(int64_t, hipStream_t);
 }
 
 namespace {
@@ -1315,9 +1317,36 @@ void hwq_set(at::Tensor flag, int64_t val) {
   check(madnn_hwq_set(flag.data_ptr<int>(), (int)val, cur_stream(flag)), "hwq_set");
 }
 
+// Pipeline replay (probe.hip): one rendezvous batch of P2P messages / a compute stand-in.
+void hwq_batch(const at::Tensor& kinds, const at::Tensor& msgs, at::Tensor a, at::Tensor b, int64_t epoch,
+               int64_t timeout_us, at::Tensor ok, const at::Tensor& ok_index) {
+  for (const at::Tensor* t : {&kinds, &msgs, static_cast<const at::Tensor*>(&a), static_cast<const at::Tensor*>(&b),
+                              static_cast<const at::Tensor*>(&ok), &ok_index}) {
+    check_dev(*t, "hwq_batch operand");
+    TORCH_CHECK(t->scalar_type() == at::kInt && t->is_contiguous(), "hwq_batch: contiguous int32 operands");
+  }
+  const int64_t n = kinds.numel();
+  TORCH_CHECK(msgs.numel() == n && ok_index.numel() == n && timeout_us > 0 && timeout_us <= 2000000,
+              "hwq_batch: kinds / msgs / ok_index of one length, 0 < timeout_us <= 2 s");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  check(madnn_hwq_batch(kinds.data_ptr<int>(), msgs.data_ptr<int>(), (int)n, a.data_ptr<int>(), b.data_ptr<int>(),
+                        (int)epoch, timeout_us, ok.data_ptr<int>(), ok_index.data_ptr<int>(), cur_stream(a)),
+        "hwq_batch");
+}
+
+void hwq_spin(const at::Tensor& like, int64_t spin_us) {
+  check_dev(like, "like");
+  TORCH_CHECK(spin_us >= 0 && spin_us <= 100000, "hwq_spin: 0 <= spin_us <= 100 ms");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  check(madnn_hwq_spin(spin_us, cur_stream(like)), "hwq_spin");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(madnn, m) {
+  m.def("hwq_batch(Tensor kinds, Tensor msgs, Tensor(a!) a, Tensor(b!) b, int epoch, int timeout_us, Tensor(c!) ok, "
+        "Tensor ok_index) -> ()");
+  m.def("hwq_spin(Tensor like, int spin_us) -> ()");
   m.def("hwq_wait(Tensor flag, int expect, int timeout_us, Tensor(a!) out) -> ()");
   m.def("hwq_set(Tensor(a!) flag, int val) -> ()");
   m.def(
@@ -1441,4 +1470,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("conv3x3_wgrad", conv3x3_wgrad);
   m.impl("hwq_wait", hwq_wait);
   m.impl("hwq_set", hwq_set);
+  m.impl("hwq_batch", hwq_batch);
+  m.impl("hwq_spin", hwq_spin);
 }

@@ -56,3 +56,60 @@ extern "C" hipError_t madnn_hwq_set(int* flag, int val, hipStream_t s) {
   hipLaunchKernelGGL(hwq_set_kernel, dim3(1), dim3(madnn::kWave), 0, s, flag, val);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Pipeline replay on the hardware queues: a "batch" of point-to-point messages with RCCL's
+// rendezvous semantics, one wave per message.  send: publish flag a[msg] = epoch, then wait
+// until the receiver acknowledges (b[msg] == epoch); recv: wait for a[msg] == epoch, then
+// acknowledge.  The batch kernel finishes only when every message of it met its peer -- as an
+// RCCL batch kernel does -- and every wait is bounded (timeout_us), so a program that would
+// deadlock shows up as timed-out messages instead of a hung queue.  ok[op] = 1 if the op met its
+// peer in time.  hwq_spin is the stand-in for a compute kernel (one wave, busy for spin_us).
+namespace {
+
+__device__ __forceinline__ bool wait_eq(const int* f, int v, long long t0, long long limit) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != v) {
+    if (wall_clock64() - t0 > limit) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+__global__ void hwq_batch_kernel(const int* __restrict__ kinds, const int* __restrict__ msgs, int nops,
+                                 int* __restrict__ a, int* __restrict__ b, int epoch, long long limit,
+                                 int* __restrict__ ok, const int* __restrict__ ok_index) {
+  const int op = blockIdx.x;
+  if (op >= nops || threadIdx.x != 0) return;
+  const int m = msgs[op];
+  const long long t0 = wall_clock64();
+  bool good;
+  if (kinds[op] == 0) {  // send
+    __hip_atomic_store(&a[m], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    good = wait_eq(&b[m], epoch, t0, limit);
+  } else {               // recv
+    good = wait_eq(&a[m], epoch, t0, limit);
+    if (good) __hip_atomic_store(&b[m], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ok[ok_index[op]] = good ? 1 : 0;
+}
+
+__global__ void hwq_spin_kernel(long long ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+}  // namespace
+
+extern "C" hipError_t madnn_hwq_batch(const int* kinds, const int* msgs, int nops, int* a, int* b, int epoch,
+                                      int64_t timeout_us, int* ok, const int* ok_index, hipStream_t s) {
+  if (nops <= 0) return hipSuccess;
+  hipLaunchKernelGGL(hwq_batch_kernel, dim3(nops), dim3(madnn::kWave), 0, s, kinds, msgs, nops, a, b, epoch,
+                     static_cast<long long>(timeout_us) * 100, ok, ok_index);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t madnn_hwq_spin(int64_t spin_us, hipStream_t s) {
+  hipLaunchKernelGGL(hwq_spin_kernel, dim3(1), dim3(madnn::kWave), 0, s, static_cast<long long>(spin_us) * 100);
+  return hipGetLastError();
+}

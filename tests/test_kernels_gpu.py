@@ -753,7 +753,7 @@ def test_linear_bias_grad_with_two_consumers(cuda, second):
     M, K, N = 256, 128, 256
     x = torch.randn(M, K, device=cuda, dtype=torch.bfloat16, requires_grad=True)
     w = (torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * K ** -0.5).requires_grad_()
-    b = (torch.randn(N, device=cuda, dtype=torch.float32) * 0.1).requires_grad_()
+    b = (torch.randn(N, device=cuda, dtype=torch.bfloat16) * 0.1).requires_grad_()
     lw = torch.ones(N, device=cuda, dtype=torch.float32, requires_grad=True)
     lb = torch.zeros(N, device=cuda, dtype=torch.float32, requires_grad=True)
 
