@@ -53,6 +53,12 @@ def main():
             print(f"[plan_table] still planning ({time.time() - t0:.0f} s)", flush=True)
 
     threading.Thread(target=heartbeat, daemon=True).start()
+    if torch.cuda.is_available():
+        # the shipped MIOpen find-db, as madnn.init() seeds it for every job: without it every
+        # convolution the layer timing touches is searched first (ResNet-50: 317 s instead of seconds)
+        from madnn.utils.miopen import setup_find_db
+
+        setup_find_db()
     from madnn.config import Config
     from madnn.planner import plan_model
 
