@@ -723,3 +723,21 @@ def test_tuning_table_roundtrip(tmp_path):
     finally:
         ops._WGRAD_CHOICE.update(saved)
         ops.load_tuning_table()
+
+
+def test_planner_prices_pipelines_with_the_engine_transport():
+    """transport_time = the simulated makespan of the engine's own transport: with free transfers
+    it is the compute-only schedule (M*chunk / (1 - bubble)); with transfers it grows, and the
+    1F1B exposure stays below GPipe's at the same transfer cost."""
+    from madnn.parallel.pp import pipeline_bubble, transport_time
+
+    chunk = 3e-3
+    for kind, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", 2)):
+        free = transport_time(kind, 4, 16, V, chunk / V, 0.0)
+        ideal = 16 * chunk / (1 - pipeline_bubble(kind, 4, 16, V))
+        assert free == pytest.approx(ideal, rel=1e-9)
+        assert transport_time(kind, 4, 16, V, chunk / V, 0.25 * chunk / V) > free
+    # a transfer of a quarter of a microbatch forward (chunk = forward + backward = 3 forwards)
+    exp = {k: transport_time(k, 4, 16, 1, chunk, chunk / 12) / transport_time(k, 4, 16, 1, chunk, 0.0)
+           for k in ("gpipe", "1f1b")}
+    assert 1.0 < exp["1f1b"] < exp["gpipe"]
