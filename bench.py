@@ -14,7 +14,7 @@ Default (the driver's contract) measures BOTH halves of the metric in one run:
   12.65k at 1536 vs 12.85k at 2048, profiles/r2_resnet_b2048.md);
 * ``gpt2_pp``: GPT-2 medium (seq 1024, bf16, FusedAdam), pipeline parallel over
   RCCL P2P -- ``pp2`` at 2 GPUs, ``pp4`` at 4, ``dp2 x pp4`` at 8; data parallel at 1 GPU
-  (a pipeline needs two stages); 64 sequences per GPU (weak scaling).  The schedule (GPipe,
+  (a pipeline needs two stages); 128 sequences per GPU (weak scaling).  The schedule (GPipe,
   1F1B, interleaved with 2 or 4 chunks per rank) and the microbatch count are the planner's
   choice (``--schedule auto``): it prices every variant with layer costs measured on the
   GPUs of the job (per-call fixed cost + per-sample slope, so small microbatches pay for
@@ -56,7 +56,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="all", choices=["all", "resnet50", "gpt2-medium"])
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
-    ap.add_argument("--gpt2-batch-per-gpu", type=int, default=64, help="GPT-2 sequences per GPU (global = this x N)")
+    ap.add_argument("--gpt2-batch-per-gpu", type=int, default=128,
+                    help="GPT-2 sequences per GPU (global = this x N); 128: 369k tok/s vs 360k at 64 on one "
+                         "MI355X, 130 of 288 GB (profiles/r4_batch_size_resnet3072_gpt2_128_96.json)")
     ap.add_argument("--gpt2-config", default="gpt2-medium", help="GPT-2 size (gpt2-tiny for CPU harness tests)")
     ap.add_argument("--gpt2-mb", type=int, default=0,
                     help="GPT-2 sequences per pipeline microbatch (0: the planner picks the microbatch count)")
@@ -117,7 +119,8 @@ def bench_resnet(args, world, rank):
     # 2048 images per GPU: sized for 288 GB HBM3E (80 GB peak), and large enough that the
     # per-step fixed costs (kernel boundaries, MIOpen workspace memsets, the optimizer pass) are
     # amortised (same box: 12650 img/s at 1536 -> 12850 at 2048, profiles/r2_resnet_b2048.md); the
-    # shipped find-db holds the tuned solvers for this shape (and for 512 / 1024 / 1536)
+    # shipped find-db holds the tuned solvers for this shape (and for 512 / 1024 / 1536 / 3072);
+    # 3072 is slower again: 249 ms/step = 12.3k img/s (profiles/r4_batch_size_resnet3072_gpt2_128_96.json)
     per_gpu = args.batch or 2048
     torch.manual_seed(0)
     model = resnet50()
