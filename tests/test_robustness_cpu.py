@@ -330,3 +330,29 @@ def test_planner_measurement_failure_is_agreed_not_hung(fault_rank):
     analytic costs -- no rank is left blocked in the results all-gather -- and all ranks plan the
     same placement; without a fault the CPU timings are used."""
     run_dist(_w_plan_measure, 2, fault_rank)
+
+
+def _w_local_groups(rank, world):
+    import torch.distributed as dist
+
+    import madnn
+    from madnn import comm
+    from madnn import runtime as rt
+
+    groups = rt.ProcessGroups(rt.Mesh(dp=world, pp=1, tp=1))
+    # size-one axes get no communicator (no RCCL stream); the dp axis spans the world
+    for g in (groups.pp_group, groups.tp_group, groups.cp_group):
+        assert isinstance(g, rt.LocalGroup) and rt.get_world_size(g) == 1 and rt.get_rank(g) == 0
+    assert groups.dp_group is None
+    t = torch.full((3,), float(rank + 1))
+    assert comm.all_reduce(t, "sum", group=groups.pp_group) is None and t.eq(rank + 1).all()
+    assert comm.select(t, "all_reduce", groups.tp_group).transport == "local"
+    rt.barrier(groups.cp_group)
+    assert comm.verify_order(groups.pp_group)
+    comm.all_reduce(t, "sum", group=groups.dp_group)
+    assert t.eq(sum(range(1, world + 1))).all()
+    assert dist.get_world_size() == world
+
+
+def test_singleton_axes_create_no_process_group():
+    run_dist(_w_local_groups, 2)
