@@ -205,7 +205,8 @@ def _plan_info(plan):
             "schedule": plan.schedule if plan.pp > 1 else None, "virtual": plan.virtual if plan.pp > 1 else None,
             "microbatches": plan.microbatches if plan.pp > 1 else None, "est_step_ms": round(plan.est_step_s * 1e3, 2),
             "costs": "measured" if plan.measured else "analytic", "candidates": len(plan.candidates),
-            "comm_measured": bool(getattr(plan, "comm_probe", None))}
+            "comm_measured": bool(getattr(plan, "comm_probe", None)),
+            "est_mem_gb": round(max(plan.est_mem_gb), 1), "plan_s": round(getattr(plan, "plan_s", 0.0), 1)}
 
 
 def _tuning_timings():

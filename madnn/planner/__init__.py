@@ -145,6 +145,9 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     lowest modelled step time that fits in HBM.  ``global_batch``: samples per optimizer step
     over the whole job (default ``cfg.extra['global_batch']``, else the example input's
     batch per GPU x ``world``)."""
+    import time
+
+    t_start = time.perf_counter()
     hw = machine or _job_machine()
     spine = trace(model)
     explicit_input = example_input is not None
@@ -180,10 +183,10 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
                 calib = _calibrate_chain(spine, example_input, costs, mb, dtype, cfg, hw)
         if multi:
             # every rank must choose the SAME placement: rank 0's (measured) costs are the plan input
-            obj = [[(c.fwd_s, c.bwd_s, c.fixed_s, c.measured) for c in costs], calib]
+            obj = [[(c.fwd_s, c.bwd_s, c.fixed_s, c.measured, c.act_bytes) for c in costs], calib]
             dist.broadcast_object_list(obj, src=0)
-            for c, (f, b, fx, m) in zip(costs, obj[0]):
-                c.fwd_s, c.bwd_s, c.fixed_s, c.measured = f, b, fx, m
+            for c, (f, b, fx, m, ab) in zip(costs, obj[0]):
+                c.fwd_s, c.bwd_s, c.fixed_s, c.measured, c.act_bytes = f, b, fx, m, ab
             calib = obj[1]
     measured = all(c.measured for c in costs)
     comm_probe = _probe_comm(cfg, world)
@@ -226,6 +229,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     plan.calibration = calib
     plan.comm_probe = comm_probe
     plan.machine = hw
+    plan.plan_s = time.perf_counter() - t_start
     log = get_logger()
     log.info("madnn plan: %s", plan.describe())
     log.info("madnn plan candidates (world=%d, global batch %d):\n%s", world, B, plan.table())
@@ -383,8 +387,9 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
 
     from .. import comm
 
+    saved = {}
     try:
-        t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype)
+        t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype, saved=saved)
     except Exception as e:  # noqa: BLE001 - decided together below
         get_logger().warning("madnn planner: chain timing failed (%s)", e)
         t = None
@@ -405,7 +410,18 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
         c.fwd_s *= r
         c.bwd_s *= r
         c.fixed_s *= r
-    return {"ratio": r, "chain_s": t, "layers_s": layers, "batch": batch}
+    out = {"ratio": r, "chain_s": t, "layers_s": layers, "batch": batch}
+    est = sum(c.act_bytes for c in costs) * batch
+    if saved.get("bytes", 0) > 0 and est > 0:
+        # the meta-device count of bytes written by forward ops includes temporaries that never
+        # live until the backward (the fused kernels' internals, views): scale it to the measured
+        # saved-activation memory (every rank measured it; ranks agree through the cost broadcast)
+        m = min(max(saved["bytes"] / est, 0.05), 2.0)
+        for c in costs:
+            c.act_bytes *= m
+        out["act_ratio"] = m
+        out["saved_bytes"] = saved["bytes"]
+    return out
 
 
 def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="none", V=1, M=1):

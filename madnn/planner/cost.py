@@ -388,10 +388,12 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
 
 def measure_chain(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: int,
                   dtype: Optional[torch.dtype] = torch.bfloat16, iters: int = 3,
-                  device: Optional[torch.device] = None) -> Optional[float]:
+                  device: Optional[torch.device] = None, saved: Optional[dict] = None) -> Optional[float]:
     """fwd+bwd seconds of the WHOLE spine, layer after layer as the model runs them, at
     ``batch`` samples -- the one-step calibration of the per-layer sum (isolated layer timings
-    miss the cache/launch interplay between neighbours).  None without a GPU."""
+    miss the cache/launch interplay between neighbours).  With ``saved`` (a dict), also the
+    device bytes one forward keeps alive for the backward (``saved["bytes"]``).  None without
+    a GPU."""
     if not torch.cuda.is_available():
         return None
     dev = device or torch.device("cuda", torch.cuda.current_device())
@@ -408,6 +410,16 @@ def measure_chain(spine: Spine, example_input: torch.Tensor, costs: List[LayerCo
         x = x.contiguous(memory_format=torch.channels_last)
     xin = x.detach()  # the model input: no data gradient, as in the training step
     fw, bw = _time_call(chain, xin, iters)
+    if saved is not None and dev.type == "cuda":
+        # what one forward keeps alive for its backward: the saved activations, measured
+        torch.cuda.synchronize(dev)
+        before = torch.cuda.memory_allocated(dev)
+        y = chain(xin)
+        torch.cuda.synchronize(dev)
+        saved["bytes"] = float(torch.cuda.memory_allocated(dev) - before)
+        if y.requires_grad:
+            y.backward(torch.ones_like(y))
+        del y
     del reps, x, xin
     torch.cuda.empty_cache()
     return (fw + bw) / 1e3
