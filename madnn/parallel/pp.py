@@ -688,8 +688,16 @@ class P2PTransport:
             ops.append(dist.P2POp(dist.isend, t, self.stage_ranks[peer], group))
             self.bytes += t.numel() * t.element_size()
             self.messages += 1
+        side = self.side is not None and not sends and self.emulate is None
         for shape, dtype, peer in recvs:
-            b = torch.empty(shape, dtype=dtype, device=self.buf_device)   # on the compute stream
+            if side:
+                # a receive-only part runs unordered with the compute stream, so its buffer must
+                # not come from blocks the compute stream freed but may still be reading: allocate
+                # it on the side stream (record_stream below hands it to the compute stream)
+                with torch.cuda.stream(self.side):
+                    b = torch.empty(shape, dtype=dtype, device=self.buf_device)
+            else:
+                b = torch.empty(shape, dtype=dtype, device=self.buf_device)   # ordered after the producer
             comm._record("recv", group, b)
             bufs.append(b)
             ops.append(dist.P2POp(dist.irecv, b, self.stage_ranks[peer], group))
@@ -700,7 +708,7 @@ class P2PTransport:
             self._rendezvous(kind, group, [p for _, p in sends], [p for *_, p in recvs])
             self._wait(dist.batch_isend_irecv(ops))
         else:
-            if self.side is not None and not sends:
+            if side:
                 # receive only: issue from the idle side stream (no wait on the compute queued so far)
                 with torch.cuda.stream(self.side):
                     works = dist.batch_isend_irecv(ops)
@@ -708,6 +716,10 @@ class P2PTransport:
                 works = dist.batch_isend_irecv(ops)
             if bufs:
                 self._wait(works)      # RCCL: the current stream waits for the part's kernel
+                if side:
+                    cur = torch.cuda.current_stream(self.device)
+                    for b in bufs:
+                        b.record_stream(cur)
                 if keep:
                     self._keep.append(keep)
             else:
