@@ -26,10 +26,10 @@ def cases():
     return [
         ("ResNet-50 (bench: 2048 images/GPU)", lambda: resnet50(),
          lambda b: torch.randn(b, 3, 224, 224), 2048, "sgd", "none", {}),
-        ("GPT-2 medium (64 x 1024 tokens/GPU, unconstrained)", lambda: GPT2(gpt2_config("gpt2-medium")),
-         lambda b: torch.zeros(b, 1024, dtype=torch.long), 64, "adam", "none", {}),
-        ("GPT-2 medium (bench's pipeline half: 4 stages pinned, everything else automatic)",
-         lambda: GPT2(gpt2_config("gpt2-medium")), lambda b: torch.zeros(b, 1024, dtype=torch.long), 64, "adam",
+        ("GPT-2 medium (128 x 1024 tokens/GPU, unconstrained)", lambda: GPT2(gpt2_config("gpt2-medium")),
+         lambda b: torch.zeros(b, 1024, dtype=torch.long), 128, "adam", "none", {}),
+        ("GPT-2 medium (bench's pipeline half: 128 x 1024 tokens/GPU, 4 stages pinned, everything else automatic)",
+         lambda: GPT2(gpt2_config("gpt2-medium")), lambda b: torch.zeros(b, 1024, dtype=torch.long), 128, "adam",
          "none", {"pp_stages": 4}),
         ("BERT-large (64 x 512/GPU, checkpointing auto)", lambda: BertForPreTraining(bert_config("bert-large")),
          lambda b: torch.zeros(b, 512, dtype=torch.long), 64, "adam", "auto", {}),

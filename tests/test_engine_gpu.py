@@ -282,3 +282,36 @@ def test_calibrate_single_gpu(cuda, tmp_path):
     m = calibrate(str(out), quick=True)
     assert out.exists() and 1.0 < m.hbm_tbps < 10.0 and 100.0 < m.bf16_tflops < 2600.0
     hw.invalidate()
+
+
+def _w_rccl_world1_transport(rank, world):
+    import torch.distributed as dist
+
+    from madnn.parallel.pp import P2PTransport
+
+    dev = torch.device("cuda", 0)
+    grad_group = dist.new_group([0])
+    probe = torch.zeros(1, device=dev)
+    dist.all_reduce(probe)                      # a collective on each communicator first
+    dist.all_reduce(probe, group=grad_group)
+    # both "stages" are this rank: every part must carry its send and its receive (self P2P)
+    tp = P2PTransport(None, grad_group, [0, 0], dev)
+    assert tp.side is not None and not tp.staged
+    x = torch.randn(64, 1024, device=dev, dtype=torch.bfloat16)
+    for kind in ("act", "grad"):
+        got = tp.exchange([(x * (2 if kind == "grad" else 1), 1)], [((64, 1024), torch.bfloat16, 0)], kind)
+        torch.testing.assert_close(got[0], x * (2 if kind == "grad" else 1))
+    # a whole batch through exchange_batch, then the step-end drain
+    out = tp.exchange_batch([("act", x + 1, 1), ("grad", x - 1, 0)],
+                            [("grad", (64, 1024), torch.bfloat16, 1), ("act", (64, 1024), torch.bfloat16, 0)])
+    torch.testing.assert_close(out[0], x - 1)
+    torch.testing.assert_close(out[1], x + 1)
+    tp.drain()
+    torch.cuda.synchronize()
+    assert tp.batches == 4 and tp.messages == 4
+
+
+def test_p2p_transport_on_rccl_world1(cuda):
+    """madnn's pipeline transport on a real RCCL communicator (world 1, self point-to-point):
+    batched parts on the activation / gradient groups, stream-ordered receives, drain."""
+    run_dist(_w_rccl_world1_transport, 1, device="cuda", backend="nccl")
