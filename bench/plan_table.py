@@ -79,11 +79,16 @@ def main():
         plan = plan_model(model, cfg, a.world, example_input=example(1), global_batch=per_gpu * a.world,
                           optimizer=optim([torch.nn.Parameter(torch.zeros(1))], lr=0.1))
         hw = getattr(plan, "machine", None)
+        cal = getattr(plan, "calibration", None) or {}
+        cal_line = ("calibration: " + ", ".join(
+            f"{k} {v:.3g}" if isinstance(v, float) else f"{k} {v}" for k, v in cal.items())) if cal else \
+            "calibration: none"
         lines += [f"## {name}", "", f"choice: **{plan.describe()}** (planned in {time.time() - t0:.1f} s)", "",
+                  cal_line, "",
                   f"links priced at: all-reduce eff {hw.allreduce_eff:.2f} x {hw.link_gbps:.0f} GB/s per link, "
                   f"P2P {hw.p2p_gbps:.0f} GB/s ({hw.source}; a job at W > 1 replaces these with its own "
                   "measurement, comm.probe)" if hw else "", "", plan.table(), ""]
-        print("\n".join(lines[-6:]), flush=True)
+        print("\n".join(lines[-8:]), flush=True)
     txt = "\n".join(lines) + "\n"
     if a.out:
         with open(a.out, "w") as f:

@@ -21,6 +21,7 @@
 namespace madnn {
 
 constexpr int kNormThreads = 256;
+typedef unsigned int nu32x4 __attribute__((ext_vector_type(4)));
 
 template <int TPR>
 __device__ __forceinline__ float row_sum(float v, float* red) {
@@ -42,6 +43,40 @@ __device__ __forceinline__ float row_sum(float v, float* red) {
   }
 }
 
+// 8 elements of a row as loaded (one 16-byte access for bf16/f16, two for f32): the forward
+// keeps the NEXT row of its grid-stride loop in flight in these while it reduces the current one
+template <int DT>
+struct Raw8 {
+  static constexpr int N = DT == kF32 ? 2 : 1;
+  nu32x4 r[N];
+  __device__ __forceinline__ void load(const void* base, int64_t i) {
+    const nu32x4* p = DT == kF32 ? reinterpret_cast<const nu32x4*>(static_cast<const float*>(base) + i)
+                                : reinterpret_cast<const nu32x4*>(static_cast<const unsigned short*>(base) + i);
+#pragma unroll
+    for (int k = 0; k < N; ++k) r[k] = p[k];
+  }
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int k = 0; k < N; ++k) r[k] = nu32x4{0u, 0u, 0u, 0u};
+  }
+  __device__ __forceinline__ void unpack(float (&v)[8]) const {
+    if constexpr (DT == kF32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __uint_as_float(r[j >> 2][j & 3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned short h = (unsigned short)(r[0][j >> 1] >> (16 * (j & 1)));
+        v[j] = DT == kBF16 ? bf16_to_f32(h) : f16_to_f32(h);
+      }
+    }
+  }
+};
+
+// Forward: the weight / bias columns of a lane never change across its grid-stride rows, so they
+// are loaded once before the loop (loading them after the row reductions exposed an L2 round trip
+// per row), and the next row's x (and residual) loads are issued before the current row's two
+// reductions, so every wave keeps a row of loads in flight while it reduces.
 template <int XDT, int WDT, int TPR, int NC>
 __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, const void* __restrict__ w, const void* __restrict__ b,
@@ -51,23 +86,56 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
   constexpr int RPB = kNormThreads / TPR;
   const int sub = threadIdx.x / TPR;
   const int t = threadIdx.x % TPR;
-  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += (int64_t)gridDim.x * RPB) {
+  float wv[NC][8], bv[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col = c * TPR * 8 + t * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wv[c][j] = bv[c][j] = 0.f;
+    if (col < H) {
+      load8<WDT>(w, col, wv[c]);
+      if (b) load8<WDT>(b, col, bv[c]);
+    }
+  }
+  const int64_t rstep = (int64_t)gridDim.x * RPB;
+  Raw8<XDT> nx[NC], nr[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    nx[c].zero();
+    nr[c].zero();
+  }
+  auto fetch = [&](int64_t row) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (row < rows && col < H) {
+        nx[c].load(x, row * H + col);
+        if (res) nr[c].load(res, row * H + col);
+      }
+    }
+  };
+  fetch((int64_t)blockIdx.x * RPB + sub);
+  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += rstep) {
     const int64_t row = row0 + sub;
     const bool live = row < rows;  // uniform per row group; all lanes still join the LDS reduction
     float v[NC][8];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      nx[c].unpack(v[c]);
+      if (res) {
+        float r[8];
+        nr[c].unpack(r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+      }
+    }
+    fetch(row + rstep);  // the next row's loads fly under this row's reductions
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (live && col < H) {
-        load8<XDT>(x, row * H + col, v[c]);
-        if (res) {
-          float r[8];
-          load8<XDT>(res, row * H + col, r);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[c][j] += r[j];
-          store8<XDT>(sum_out, row * H + col, v[c]);
-        }
+        if (res) store8<XDT>(sum_out, row * H + col, v[c]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[c][j];
       } else {
@@ -95,11 +163,9 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (live && col < H) {
-        float wv[8], bv[8], o[8];
-        load8<WDT>(w, col, wv);
-        if (b) load8<WDT>(b, col, bv);
+        float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[j] + (b ? bv[j] : 0.f);
+        for (int j = 0; j < 8; ++j) o[j] = (v[c][j] - mean) * rstd * wv[c][j] + bv[c][j];
         store8<XDT>(y, row * H + col, o);
       }
     }
@@ -117,8 +183,8 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
 // bias gradient of the Linear that produced this norm's input (the transformer residual stream),
 // so that Linear's backward needs no column-sum pass of its own (ops._LinearFn, `_madnn_colsum`).
 // EARLY: the weight is loaded once per lane (its columns never change across the grid-stride
-// rows) and the residual gradient is loaded together with x and dy, so its latency hides under
-// the row reduction instead of following it (A/B: madnn_norm_tune key 2).
+// rows) and the next row's x, dy, residual gradient and statistics are loaded before this row's
+// reductions, so their latency hides under them instead of following them (A/B: madnn_norm_tune key 2).
 template <int XDT, int WDT, int TPR, int NC, bool EARLY, bool CS>
 __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ w,
@@ -155,25 +221,72 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     }
   }
 
-  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += (int64_t)gridDim.x * RPB) {
+  // EARLY: the next row's x / dy / residual gradient / statistics are loaded into these before the
+  // current row's reductions (as in the forward), so a wave always has a row of loads in flight
+  constexpr int NP = EARLY ? NC : 1;
+  Raw8<XDT> px[NP], pg[NP], pr[NP];
+  float pmean = 0.f, prstd = 0.f;
+#pragma unroll
+  for (int c = 0; c < NP; ++c) {
+    px[c].zero();
+    pg[c].zero();
+    pr[c].zero();
+  }
+  const int64_t rstep = (int64_t)gridDim.x * RPB;
+  auto fetch = [&](int64_t r) {
+    if constexpr (EARLY) {
+      if (r < rows) {
+        pmean = rms ? 0.f : mean_in[r];
+        prstd = rstd_in[r];
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int col = c * TPR * 8 + t * 8;
+        if (r < rows && col < H) {
+          px[c].load(x, r * H + col);
+          pg[c].load(dy, r * H + col);
+          if (dres) pr[c].load(dres, r * H + col);
+        }
+      }
+    }
+  };
+  fetch((int64_t)blockIdx.x * RPB + sub);
+  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += rstep) {
     const int64_t row = row0 + sub;
     const bool live = row < rows;
-    const float mean = (live && !rms) ? mean_in[row] : 0.f;
-    const float rstd = live ? rstd_in[row] : 0.f;
+    float mean, rstd;
     float xh[NC][8], wdy[NC][8], rv[EARLY ? NC : 1][8];
+    float xcur[NP][8], gcur[NP][8];
+    if constexpr (EARLY) {
+      mean = live ? pmean : 0.f;
+      rstd = live ? prstd : 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        px[c].unpack(xcur[c]);
+        pg[c].unpack(gcur[c]);
+        if (dres) pr[c].unpack(rv[c]);
+      }
+      fetch(row + rstep);  // the next row's loads fly under this row's math and reductions
+    } else {
+      mean = (live && !rms) ? mean_in[row] : 0.f;
+      rstd = live ? rstd_in[row] : 0.f;
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (live && col < H) {
         float xv[8], gv[8], wv[8];
-        load8<XDT>(x, row * H + col, xv);
-        load8<XDT>(dy, row * H + col, gv);
         if constexpr (EARLY) {
-          if (dres) load8<XDT>(dres, row * H + col, rv[c]);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) wv[j] = wk[c][j];
+          for (int j = 0; j < 8; ++j) {
+            xv[j] = xcur[c][j];
+            gv[j] = gcur[c][j];
+            wv[j] = wk[c][j];
+          }
         } else {
+          load8<XDT>(x, row * H + col, xv);
+          load8<XDT>(dy, row * H + col, gv);
           load8<WDT>(w, col, wv);
         }
 #pragma unroll

@@ -375,13 +375,23 @@ def optimizer_s(params: float, opt: str, hw: Machine) -> float:
 def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw: Machine):
     """Scale the per-layer costs so their sum matches ONE timing of the whole spine at the
     measurement batch (isolated layer timings miss what neighbouring layers do to each other).
-    Skipped for models whose weights would take more than a quarter of HBM.  Returns
-    ``{"ratio", "chain_s", "layers_s", "batch"}`` or None."""
+    The same forward also measures the saved-activation bytes and rescales every layer's
+    ``act_bytes`` to them.  When weights + gradients + the (estimated) activations of ``batch``
+    samples would not fit half of HBM, the chain runs at the largest batch that does: the memory
+    ratio is taken there, the timing ratio is not (a smaller batch has other neighbour effects) --
+    the activation estimate over-counts most exactly when it is large, and that is when the
+    planner most needs it corrected (GPT-2 medium at 128 sequences: 328 GB estimated, 129 GB
+    measured).  Skipped when the weights alone take more than a quarter of HBM.  Returns
+    ``{"ratio", "chain_s", "layers_s", "batch", "act_ratio", "saved_bytes", "chain_batch"}`` or None."""
     if not cfg.extra.get("calibrate_chain", True):
         return None
     nparams = sum(c.params for c in costs)
-    need = nparams * 6 + sum(c.act_bytes for c in costs) * batch   # weights + grads, saved activations
-    if need > 0.5 * hw.hbm_gb * 1e9:
+    act = sum(c.act_bytes for c in costs)
+    budget = 0.5 * hw.hbm_gb * 1e9 - nparams * 6   # weights + grads, then saved activations
+    if nparams * 6 > 0.25 * hw.hbm_gb * 1e9 or budget <= 0:
+        return None
+    cb = batch if act * batch <= budget else int(budget // max(act, 1.0))
+    if cb < 1:
         return None
     import torch.distributed as dist
 
@@ -389,7 +399,7 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
 
     saved = {}
     try:
-        t = measure_chain(spine, example_input, costs, batch=batch, dtype=dtype, saved=saved)
+        t = measure_chain(spine, example_input, costs, batch=cb, dtype=dtype, saved=saved)
     except Exception as e:  # noqa: BLE001 - decided together below
         get_logger().warning("madnn planner: chain timing failed (%s)", e)
         t = None
@@ -402,16 +412,16 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
         t = float(v) / dist.get_world_size()
     if not t:
         return None
-    layers = sum(c.call_s(batch) for c in costs)
-    if layers <= 0:
-        return None
-    r = t / layers
-    for c in costs:
-        c.fwd_s *= r
-        c.bwd_s *= r
-        c.fixed_s *= r
-    out = {"ratio": r, "chain_s": t, "layers_s": layers, "batch": batch}
-    est = sum(c.act_bytes for c in costs) * batch
+    out = {"batch": batch, "chain_batch": cb, "chain_s": t}
+    layers = sum(c.call_s(cb) for c in costs)
+    if cb == batch and layers > 0:
+        r = t / layers
+        for c in costs:
+            c.fwd_s *= r
+            c.bwd_s *= r
+            c.fixed_s *= r
+        out.update(ratio=r, layers_s=layers)
+    est = act * cb
     if saved.get("bytes", 0) > 0 and est > 0:
         # the meta-device count of bytes written by forward ops includes temporaries that never
         # live until the backward (the fused kernels' internals, views): scale it to the measured

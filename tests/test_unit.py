@@ -741,3 +741,36 @@ def test_planner_prices_pipelines_with_the_engine_transport():
     exp = {k: transport_time(k, 4, 16, 1, chunk, chunk / 12) / transport_time(k, 4, 16, 1, chunk, 0.0)
            for k in ("gpipe", "1f1b")}
     assert 1.0 < exp["1f1b"] < exp["gpipe"]
+
+
+def test_chain_calibration_rescales_activation_memory_at_a_batch_that_fits(monkeypatch):
+    """When the estimated activations of the timing batch would not fit half of HBM, the chain
+    forward runs at the largest batch that does: its measured saved bytes rescale every layer's
+    act_bytes (the estimate over-counts most exactly when it is large), and the timing ratio,
+    which a smaller batch would distort, is left alone."""
+    import madnn.planner as planner
+    from madnn.planner.cost import LayerCost
+    from madnn.planner.hw import load
+
+    hw = load()
+    costs = [LayerCost(name=f"l{i}", params=1000, shared_params=0, flops=1.0, act_bytes=1e9, out_bytes=1.0,
+                       fwd_s=1e-3, bwd_s=2e-3, measured=True) for i in range(4)]
+    seen = {}
+
+    def fake_chain(spine, example_input, costs_, *, batch, dtype=None, saved=None, **kw):
+        seen["batch"] = batch
+        saved["bytes"] = 0.4 * 4e9 * batch       # 40 % of the estimate is really kept
+        return 1.0
+
+    monkeypatch.setattr(planner, "measure_chain", fake_chain)
+    cal = planner._calibrate_chain(None, None, costs, 256, torch.bfloat16, Config(), hw)
+    budget = 0.5 * hw.hbm_gb * 1e9 - 4 * 1000 * 6
+    assert seen["batch"] == int(budget // 4e9) < 256 and cal["chain_batch"] == seen["batch"]
+    assert "ratio" not in cal and all(c.fwd_s == 1e-3 for c in costs)
+    assert cal["act_ratio"] == pytest.approx(0.4) and all(c.act_bytes == pytest.approx(0.4e9) for c in costs)
+    # a batch that fits: measured there, and the timing ratio applies
+    for c in costs:
+        c.act_bytes = 1e9
+    layers = sum(c.call_s(8) for c in costs)
+    cal = planner._calibrate_chain(None, None, costs, 8, torch.bfloat16, Config(), hw)
+    assert seen["batch"] == 8 and cal["ratio"] == pytest.approx(1.0 / layers)
