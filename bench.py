@@ -376,7 +376,7 @@ def main():
             "data": "synthetic (random ImageNet-shaped images / random tokens, random-init weights)",
             "config": config,
         }
-        config["per_gpu_value"] = round(res["value"] / world, 2)
+        config["per_gpu_value"] = float(f"{res['value'] / world:.6g}")
         _release()
         if args.std_batch and args.std_batch != config["per_gpu_batch"]:
             # the same measurement at a standard per-GPU batch, so rounds compare like for like
@@ -385,7 +385,7 @@ def main():
             sdt = _max_over_ranks(sdt)
             sval = round(sps_step * args.steps / sdt, 2)
             res["config"]["std_batch"] = {"per_gpu_batch": args.std_batch, "global_batch": sps_step,
-                                          "value": sval, "per_gpu_value": round(sval / world, 2),
+                                          "value": sval, "per_gpu_value": float(f"{sval / world:.6g}"),
                                           "ms_per_step": round(sdt / args.steps * 1000.0, 3),
                                           "warmup_s": sconf["warmup_s"], "parallelism": sconf["parallelism"],
                                           **{k: sconf.get(k) for k in ("comm_exposed_ms", "busbw_gbps", "p2p_gbps")}}

@@ -377,7 +377,7 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
     measurement batch (isolated layer timings miss what neighbouring layers do to each other).
     The same forward also measures the saved-activation bytes and rescales every layer's
     ``act_bytes`` to them.  When weights + gradients + the (estimated) activations of ``batch``
-    samples would not fit half of HBM, the chain runs at the largest batch that does: the memory
+    samples would not fit 3/4 of the free HBM, the chain runs at batch / 2^k that does: the memory
     ratio is taken there, the timing ratio is not (a smaller batch has other neighbour effects) --
     the activation estimate over-counts most exactly when it is large, and that is when the
     planner most needs it corrected (GPT-2 medium at 128 sequences: 328 GB estimated, 129 GB
@@ -387,11 +387,17 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
         return None
     nparams = sum(c.params for c in costs)
     act = sum(c.act_bytes for c in costs)
-    budget = 0.5 * hw.hbm_gb * 1e9 - nparams * 6   # weights + grads, then saved activations
+    held = torch.cuda.memory_allocated() if torch.cuda.is_available() else 0
+    # weights + grads, then the saved activations, within 3/4 of what the device has left
+    budget = 0.75 * hw.hbm_gb * 1e9 - held - nparams * 6
     if nparams * 6 > 0.25 * hw.hbm_gb * 1e9 or budget <= 0:
         return None
-    cb = batch if act * batch <= budget else int(budget // max(act, 1.0))
-    if cb < 1:
+    # halve until it fits: batch / 2^k keeps to the shapes the shipped tuning records hold more
+    # often than an arbitrary batch would (every new convolution shape costs an MIOpen search)
+    cb = batch
+    while cb > 1 and act * cb > budget:
+        cb //= 2
+    if act * cb > budget:
         return None
     import torch.distributed as dist
 
