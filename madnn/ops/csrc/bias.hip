@@ -60,19 +60,19 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return x * (RCP ? __builtin_amdgcn_rcpf(1.f + e) : 1.f / (1.f + e));
 }
 
-// 8 elements per lane per access (16-byte loads/stores), 4 accesses in flight per lane,
+// 8 elements per lane per access (16-byte loads/stores), U accesses in flight per lane,
 // grid-stride over the flat tensor.  HBM-bound: reads x, writes y, nothing else.
-template <int DT, bool RCP = true>
+template <int DT, bool RCP = true, int U = 4>
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                        int64_t n8) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n8; i += 4 * stride) {
-    float v[4][8];
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    float v[U][8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) load8<DT>(x, (i + u * stride) * 8, v[u]);
+    for (int u = 0; u < U; ++u) load8<DT>(x, (i + u * stride) * 8, v[u]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh<RCP>(v[u][j]);
       store8<DT>(y, (i + u * stride) * 8, v[u]);
@@ -233,16 +233,39 @@ int madnn_bias_grad_rows(int64_t M, int N, int gelu) {
   return (int)r;
 }
 
+// GELU forward launch knobs (madnn_gelu_tune): key 0 = workgroups per CU (grid cap), key 1 = 16-byte
+// accesses in flight per lane (4, 8 or 16).  Swept at GPT-2 medium's [65536, 4096]
+// (bench/stream_tune.py, profiles/r4_stream_tune.json): 1 workgroup per CU with 8 accesses in flight
+// 184 us (5.8 TB/s) against 245 us at the former 8 x 4 -- one narrow sweep front through the tensor
+// beats many resident waves each walking its own far-apart addresses.
+static int g_gelu_wg = 1, g_gelu_unroll = 8;
+
+int madnn_gelu_tune(int key, int value) {
+  int* f = key == 0 ? &g_gelu_wg : key == 1 ? &g_gelu_unroll : nullptr;
+  if (f == nullptr) return -1;
+  const int old = *f;
+  if (value > 0) *f = value;
+  return old;
+}
+
 hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t stream) {
   if (n % 8) return hipErrorInvalidValue;
   const int64_t n8 = n / 8;
-  int64_t grid = (n8 + 4 * 256 - 1) / (4 * 256);
-  const int64_t cap = 8 * (int64_t)kNumCU;  // a few waves per CU, grid-stride beyond that
+  const int U = g_gelu_unroll >= 16 ? 16 : g_gelu_unroll >= 8 ? 8 : 4;
+  int64_t grid = (n8 + U * 256 - 1) / (U * 256);
+  const int64_t cap = (int64_t)g_gelu_wg * kNumCU;  // a few waves per CU, grid-stride beyond that
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
   MADNN_DISPATCH_DT(dt, DT, {
-    if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-    else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    if (U == 16) {
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 16>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    } else if (U == 8) {
+      if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+      else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    } else {
+      if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+      else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+    }
   });
   return hipGetLastError();
 }

@@ -183,14 +183,24 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const float* __restr
     default: return hipErrorInvalidValue;                                        \
   }
 
+// optimizer launch knob (madnn_optim_tune key 0): workgroups per CU of the SGD / Adam passes
+static int g_opt_wg = 4;
+
 extern "C" {
+
+int madnn_optim_tune(int key, int value) {
+  if (key != 0) return -1;
+  const int old = g_opt_wg;
+  if (value > 0) g_opt_wg = value;
+  return old;
+}
 
 hipError_t madnn_sgd_step(float* master, const void* grad, int grad_dt, float* mom, void* model, int model_dt,
                           int64_t n, float lr, float momentum, float dampening, float weight_decay, int nesterov,
                           int first_step, float grad_scale, const float* dscale, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   madnn::SGDHyper h{lr, momentum, dampening, weight_decay, grad_scale, nesterov, first_step};
-  const int grid = madnn::stream_grid(n, madnn::kOptThreads * madnn::kOptVec, 4 * madnn::kNumCU);
+  const int grid = madnn::stream_grid(n, madnn::kOptThreads * madnn::kOptVec, g_opt_wg * madnn::kNumCU);
   MADNN_DISPATCH_DT(grad_dt, GDT, MADNN_DISPATCH_MODEL(model_dt, MDT, {
     hipLaunchKernelGGL((madnn::sgd_kernel<GDT, MDT>), dim3(grid), dim3(madnn::kOptThreads), 0, stream, master, grad,
                        mom, model, n, h, dscale);
@@ -204,7 +214,7 @@ hipError_t madnn_adam_step(float* master, const void* grad, int grad_dt, float* 
                            hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   madnn::AdamHyper h{lr, beta1, beta2, eps, weight_decay, grad_scale, bias_corr1, bias_corr2_sqrt, adamw};
-  const int grid = madnn::stream_grid(n, madnn::kOptThreads * madnn::kOptVec, 4 * madnn::kNumCU);
+  const int grid = madnn::stream_grid(n, madnn::kOptThreads * madnn::kOptVec, g_opt_wg * madnn::kNumCU);
   MADNN_DISPATCH_DT(grad_dt, GDT, MADNN_DISPATCH_MODEL(model_dt, MDT, {
     hipLaunchKernelGGL((madnn::adam_kernel<GDT, MDT>), dim3(grid), dim3(madnn::kOptThreads), 0, stream, master, grad,
                        m1, m2, model, n, h, dscale);
