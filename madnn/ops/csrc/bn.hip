@@ -25,7 +25,6 @@ namespace madnn {
 
 constexpr int kBnThreads = 256;
 constexpr int kFinSlices = 32;   // finalize: 32 channels x 32 partial-row slices per 1024-lane block
-constexpr int kBnMaxPartials = 2 * kNumCU;
 
 struct BnGeom {
   int tpr, rpi;
@@ -53,6 +52,8 @@ struct BnTune {
   int wg_per_cu = 3;
   int hoist = 1;
   int unroll = 0;  // 1: apply walks handle two chunks per trip (more loads in flight)
+  int partials_per_cu = 2;  // reduction passes (statistics, backward sums): workgroups = partial rows per CU
+  //                            (ResNet-50 b512, profiles/r4_ab_bn_partials_*: 1 -1.8 %, 4 -0.5 % against 2)
 };
 inline BnTune& bn_tune() {
   static BnTune t;
@@ -583,8 +584,9 @@ inline const float* prereduce(const float* part, int& G, int C, int& pstride, in
 
 static int bn_grid_rows(int64_t M, int C) {
   const BnGeom g = bn_geom(C);
+  const int64_t cap = (int64_t)bn_tune().partials_per_cu * kNumCU;
   int64_t iters = (M + g.rpi - 1) / g.rpi;
-  return (int)(iters < kBnMaxPartials ? (iters < 1 ? 1 : iters) : kBnMaxPartials);
+  return (int)(iters < cap ? (iters < 1 ? 1 : iters) : cap);
 }
 
 }  // namespace madnn
@@ -598,17 +600,20 @@ static int bn_grid_rows(int64_t M, int C) {
 extern "C" {
 
 // key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU, 2: coefficient hoisting
-// (0/1); value < 0 only reads.
+// (0/1), 3: apply unroll (0/1), 4: reduction workgroups (partial rows) per CU; value < 0 only reads.
+// Key 4 sizes the partial slabs: change it only between steps (every call sizes its own workspace).
 // Returns the old value (-1 for an unknown key).
 int madnn_bn_tune(int key, int value) {
   int* f = key == 0   ? &madnn::bn_tune().reverse
            : key == 1 ? &madnn::bn_tune().wg_per_cu
            : key == 2 ? &madnn::bn_tune().hoist
            : key == 3 ? &madnn::bn_tune().unroll
+           : key == 4 ? &madnn::bn_tune().partials_per_cu
                       : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value >= 0) *f = key == 1 ? (value < 1 ? 1 : value) : (value != 0);
+  if (value >= 0) *f = key == 1 ? (value < 1 ? 1 : value) : key == 4 ? (value < 1 ? 1 : value > 8 ? 8 : value)
+                                                                     : (value != 0);
   return old;
 }
 
