@@ -236,6 +236,10 @@ def _comm_fields(engine, plan) -> dict:
         out["bubble_fraction"] = round(m["bubble_fraction"], 4)
     if "p2p_bytes" in m:
         out["p2p_bytes"] = m["p2p_bytes"]
+    if "plan_lags" in m:
+        # the pipeline's issue plans (transfer lag in forward-chunk units), the measured step of
+        # each during the warm-up and the one kept (parallel.pp.PipelineEngine._init_plans)
+        out["pp_plan"] = {"lags": m["plan_lags"], "kept": m["plan_lag"], "step_ms": m["plan_step_ms"]}
     return out
 
 

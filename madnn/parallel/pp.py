@@ -30,6 +30,7 @@ configs 3 and 4 require it.  Design for one MI355X node:
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -240,23 +241,35 @@ def simulate_schedule(kind: str, nstages: int, nmicro: int, nchunks: int = 1, t_
 _TIMELINE_CACHE: Dict[tuple, dict] = {}
 
 
-def _timeline(kind: str, nstages: int, nmicro: int, nchunks: int) -> dict:
-    key = (kind, nstages, nmicro, nchunks)
+def _timeline(kind: str, nstages: int, nmicro: int, nchunks: int, lag: float = 0.0) -> dict:
+    key = (kind, nstages, nmicro, nchunks, lag)
     if key not in _TIMELINE_CACHE:
-        _TIMELINE_CACHE[key] = simulate_schedule(kind, nstages, nmicro, nchunks)["times"]
+        _TIMELINE_CACHE[key] = simulate_schedule(kind, nstages, nmicro, nchunks, t_p2p=lag)["times"]
     return _TIMELINE_CACHE[key]
 
 
-def issue_plan(kind: str, stage: int, nstages: int, nmicro: int, nchunks: int = 1) -> List[tuple]:
+# transfer time in forward-chunk units the engine's second issue plan assumes when the plan
+# carries none (a hand-written placement): GPT-2 medium's 8-GPU plan prices 0.27-0.8
+_DEFAULT_LAG = 0.3
+
+
+def plan_lag(lag: float) -> float:
+    """A transfer time in forward-chunk units, rounded to 2 significant digits (the issue plans
+    and their caches are keyed on it)."""
+    return float(f"{lag:.2g}") if lag > 0 else 0.0
+
+
+def issue_plan(kind: str, stage: int, nstages: int, nmicro: int, nchunks: int = 1,
+               lag: float = 0.0) -> List[tuple]:
     """The program one pipeline rank issues per step: ``("C", op, c, m)`` compute items and
     ``("X", ops)`` point-to-point batches, ``ops`` = ``(("send"|"recv", "act"|"grad", c, m, peer
     stage), ...)``.  The engine issues each batch as ONE ``batch_isend_irecv`` on the replica's
     pipeline communicator (one ncclGroup: one kernel per batch) and orders the compute that
     consumes a received tensor after it.
 
-    Construction (any compute order: GPipe, 1F1B, interleaved): the compute-only schedule
-    (:func:`simulate_schedule`, forward 1 / backward 2) gives every compute a start and a finish
-    time on one global clock.  Each message is assigned to the BOUNDARY at its producer's
+    Construction (any compute order: GPipe, 1F1B, interleaved): a schedule of the computes
+    (:func:`simulate_schedule`, forward 1 / backward 2, each transfer ``lag`` forward-units long)
+    gives every compute a start and a finish time on one global clock.  Each message is assigned to the BOUNDARY at its producer's
     finish time T, on both ranks: the sender issues it right after the producer, the receiver
     in a batch placed before its first compute that starts at or after T (a compute that
     started earlier goes first).  Messages of one rank with the same boundary share a batch; in
@@ -277,11 +290,20 @@ def issue_plan(kind: str, stage: int, nstages: int, nmicro: int, nchunks: int = 
     so no stream-to-queue mapping can deadlock it (:func:`simulate_transport` checks
     ``queues="serial"``, round-robin queue pools and independent queues).  The round-3 engine
     pre-posted every receive of the step, which deadlocks as soon as one of those spinning
-    receive kernels shares a queue with the compute stream (``design="prepost"``)."""
+    receive kernels shares a queue with the compute stream (``design="prepost"``).
+
+    ``lag``: the argument holds for ANY consistent clock, so the transfer time can be part of
+    it.  With ``lag`` > 0 a receiver's batch lands before its first compute that starts after
+    the producer finished -- earlier relative to the consumer than with ``lag`` = 0, which lets
+    an interleaved schedule's slack hide the transfer (``simulate_transport`` with independent
+    queues: S = 4, M = 16, V = 2 at transfers of 0.27 forward: 108.9 vs 118.5, the round-3
+    pre-posting's 108.8) -- but a receive posted earlier also holds its hardware queue longer, so
+    when the gradient communicator shares the compute stream's queue ``lag`` = 0 is better
+    (123.4 vs 168.1).  The engine measures both on the job and keeps the faster."""
     S, V = nstages, nchunks
     SV = S * V
     order = native_runtime.pipeline_order(kind, stage, S, nmicro, V)
-    times = _timeline(kind, S, nmicro, V)
+    times = _timeline(kind, S, nmicro, V, plan_lag(lag))
     items: List[tuple] = []
     batches: Dict[float, list] = {}
     for op, c, m in order:
@@ -312,7 +334,7 @@ def _message(d: str, kind: str, c: int, m: int, stage: int, nstages: int) -> tup
     return (kind, vs + 1 if kind == "act" else vs - 1, m)
 
 
-def check_plan_fifo(kind: str, nstages: int, nmicro: int, nchunks: int = 1) -> int:
+def check_plan_fifo(kind: str, nstages: int, nmicro: int, nchunks: int = 1, lag: float = 0.0) -> int:
     """Every ordered rank pair's messages are received in the order they are sent (the
     communicator matches P2P operations of one pair FIFO).  Returns the message count; raises
     RuntimeError on a mismatch (which would deliver one microbatch's data to another)."""
@@ -320,7 +342,7 @@ def check_plan_fifo(kind: str, nstages: int, nmicro: int, nchunks: int = 1) -> i
     sent: Dict[tuple, list] = {}
     recvd: Dict[tuple, list] = {}
     for s in range(S):
-        for item in issue_plan(kind, s, S, nmicro, nchunks):
+        for item in issue_plan(kind, s, S, nmicro, nchunks, lag):
             if item[0] != "X":
                 continue
             for d, k, c, m, peer in item[1]:
@@ -380,7 +402,7 @@ def rank_streams(design: str, stage: int, nstages: int, dp: int = 1, tied: bool 
 def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, design: str = "split",
                        queues=None, dp: int = 1, tied: bool = False, first_step: bool = False,
                        queue_offset: int = 0, t_fwd: float = 1.0, t_bwd: float = 2.0, t_p2p: float = 0.0,
-                       t_coll: float = 0.0) -> dict:
+                       t_coll: float = 0.0, lag: float = 0.0) -> dict:
     """Replay one training step of every rank of a ``dp x nstages`` pipeline mesh against a model
     of the GPU's execution: every HIP stream of a rank feeds a hardware queue, and a queue runs
     its operations ONE AT A TIME in submission order (a compute kernel for ``t_fwd``/``t_bwd``, an
@@ -404,7 +426,7 @@ def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, d
     and last stage after the step); ``"batched"`` is the same plan on ONE communicator;
     ``"prepost"`` is the round-3 engine (one 2-rank communicator per channel, every receive of
     the step posted up front).  ``first_step`` adds the shape headers a new input signature
-    exchanges (host-blocking).
+    exchanges (host-blocking).  ``lag``: the issue plan's transfer time (:func:`issue_plan`).
 
     Raises RuntimeError on a deadlock (naming every stuck queue head) or a FIFO mismatch;
     returns ``{"makespan", "bubble", "ops", "queues"}``."""
@@ -442,7 +464,7 @@ def simulate_transport(kind: str, nstages: int, nmicro: int, nchunks: int = 1, d
             last_c = None
             need = None
             met_in, met_out = set(), set()
-            for item in issue_plan(kind, s, S, M, V):
+            for item in issue_plan(kind, s, S, M, V, lag):
                 if item[0] == "X":
                     batch = item[1]
                     if first_step:
@@ -823,7 +845,7 @@ class PipelineEngine:
     def __init__(self, stage_module: PipelineStage, *, stage: int, nstages: int, groups: rt.ProcessGroups,
                  microbatches: int, schedule: str, loss_fn: Callable, dp_engine: DataParallel,
                  cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=(),
-                 transport: Optional[P2PTransport] = None):
+                 transport: Optional[P2PTransport] = None, lag: float = 0.0):
         self.module = stage_module
         self.chunks = list(stage_module.chunks)
         self.V = len(self.chunks)
@@ -841,7 +863,7 @@ class PipelineEngine:
         self.buffer_refs = list(buffer_refs)   # (original name, owner module, local name)
         self.transport = transport
         self.order = native_runtime.pipeline_order(schedule, stage, nstages, microbatches, self.V)
-        self.plan_items = issue_plan(schedule, stage, nstages, microbatches, self.V)
+        self._init_plans(lag)
         S, SV = nstages, nstages * self.V
         self._vs = [virtual_stage(c, stage, S) for c in range(self.V)]
         self.holds_first = 0 in self._vs
@@ -869,6 +891,63 @@ class PipelineEngine:
         self._needs_tied = False
         self.last_loss = None
         self.stats = {"steps": 0, "p2p_batches": 0}
+
+    def _init_plans(self, lag: float) -> None:
+        """The issue plans this rank can run (:func:`issue_plan` at ``lag`` 0 and at the planned
+        transfer time) and how the engine picks one: ``MADNN_PP_PLAN`` = ``auto`` (default: time
+        both on the job -- the hardware-queue mapping decides which is faster -- and keep the
+        faster), ``0`` (lag 0 only) or ``lag`` (the lagged plan only).  Every plan is deadlock-free
+        fully serialised, and every rank switches at the same step, so any mix is safe."""
+        import os
+
+        S, M, V = self.nstages, self.M, self.V
+        mode = os.environ.get("MADNN_PP_PLAN", "auto")
+        lag = plan_lag(lag)
+        lags = [0.0]
+        if mode != "0" and lag > 0 and any(issue_plan(self.schedule, s, S, M, V) !=
+                                           issue_plan(self.schedule, s, S, M, V, lag) for s in range(S)):
+            lags = [lag] if mode == "lag" else [0.0, lag]
+        self._lags = lags
+        self._plans = [issue_plan(self.schedule, self.stage, S, M, V, g) for g in lags]
+        self.plan_items = self._plans[0]
+        self.plan_lag = lags[0]
+        # steps 1 .. 2L run the L plans alternately (step 0 exchanges the shape headers); the plan
+        # of a step is a function of the step count alone, so every rank runs the same one
+        self._tune = {"t": [0.0] * len(lags), "n": [0] * len(lags), "chosen": 0 if len(lags) == 1 else None}
+
+    def _tune_begin(self, new_sig: bool):
+        L, n = len(self._plans), self.stats["steps"]
+        if L == 1 or not 1 <= n <= 2 * L:
+            return None
+        i = (n - 1) % L
+        self.plan_items, self.plan_lag = self._plans[i], self._lags[i]
+        if torch.cuda.is_available() and rt.device().type == "cuda":
+            torch.cuda.synchronize()
+        return i, time.perf_counter(), new_sig
+
+    def _tune_end(self, tok) -> None:
+        if tok is None:
+            return
+        i, t0, new_sig = tok
+        if torch.cuda.is_available() and rt.device().type == "cuda":
+            torch.cuda.synchronize()
+        tn = self._tune
+        if not new_sig:                      # a step that also exchanged headers is not timed
+            tn["t"][i] += time.perf_counter() - t0
+            tn["n"][i] += 1
+        if self.stats["steps"] != 2 * len(self._plans):
+            return
+        t = torch.tensor([tt / max(nn_, 1) for tt, nn_ in zip(tn["t"], tn["n"])], dtype=torch.float64)
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            # the job's time per plan is its slowest rank's; every rank takes the same decision
+            dev = rt.device() if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = t.to(dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t = t.cpu()
+        best = int(torch.argmin(t))
+        tn["chosen"] = best
+        tn["ms"] = [round(float(x) * 1e3, 3) for x in t]
+        self.plan_items, self.plan_lag = self._plans[best], self._lags[best]
 
     @property
     def is_first(self):
@@ -911,6 +990,7 @@ class PipelineEngine:
                 torch.cuda.current_stream().wait_stream(self.dp.comm_stream)
         if self._needs_tied:
             self._wait_tied()
+        tune = self._tune_begin(new_sig)
         inbox: Dict[tuple, torch.Tensor] = {}     # ("act"|"grad", c, m) -> received tensor
         outbox: Dict[tuple, torch.Tensor] = {}    # ("act"|"grad", c, m) -> tensor to send
         acts_in: Dict[tuple, torch.Tensor] = {}
@@ -983,6 +1063,7 @@ class PipelineEngine:
         if tp is not None:
             tp.drain()
             self.stats["p2p_batches"] = tp.batches
+        self._tune_end(tune)
         self.stats["steps"] += 1
         self.last_loss = total
         return total
@@ -1059,6 +1140,9 @@ class PipelineEngine:
         tp = self.transport
         out["p2p_bytes"] = tp.bytes if tp is not None else 0
         out["p2p_batches_per_step"] = (tp.batches / max(self.stats["steps"], 1)) if tp is not None else 0
+        out["plan_lags"] = list(self._lags)
+        out["plan_lag"] = self.plan_lag
+        out["plan_step_ms"] = self._tune.get("ms")
         return out
 
     # ------------------------------------------------------------ inference
@@ -1115,15 +1199,18 @@ def transport_time(schedule: str, nstages: int, nmicro: int, nchunks: int, chunk
     """Seconds of one pipelined step of ``nmicro`` microbatches when one chunk's forward +
     backward of one microbatch takes ``chunk_s`` (split 1 : 2) and one activation / gradient
     transfer ``p2p_s``: the makespan of :func:`simulate_transport` on the engine's transport
-    (independent queues), so the planner prices exactly the communication this engine exposes.
-    Cached on the transfer / compute ratio (2 significant digits)."""
+    (independent queues), so the planner prices exactly the communication this engine exposes --
+    the better of its two issue plans (``lag`` 0 and the transfer time), as the engine keeps the
+    one that measured faster.  Cached on the transfer / compute ratio (2 significant digits)."""
     if nstages <= 1 or chunk_s <= 0:
         return nmicro * nchunks * max(chunk_s, 0.0)
     ratio = float(f"{p2p_s / chunk_s:.2g}") if p2p_s > 0 else 0.0
     key = (schedule, nstages, nmicro, nchunks, ratio)
     if key not in _TRANSPORT_CACHE:
-        _TRANSPORT_CACHE[key] = simulate_transport(schedule, nstages, nmicro, nchunks, "split", None,
-                                                   t_fwd=1.0, t_bwd=2.0, t_p2p=3.0 * ratio)["makespan"] / 3.0
+        t = [simulate_transport(schedule, nstages, nmicro, nchunks, "split", None, t_fwd=1.0, t_bwd=2.0,
+                                t_p2p=3.0 * ratio, lag=lag)["makespan"] / 3.0
+             for lag in sorted({0.0, plan_lag(3.0 * ratio)})]
+        _TRANSPORT_CACHE[key] = min(t)
     return _TRANSPORT_CACHE[key] * chunk_s
 
 
@@ -1250,7 +1337,8 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                              rebuild_buckets=cfg.rebuild_buckets and optimizer is not None)
     engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
                             schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
-                            tied=tied_local, param_names=names, buffer_refs=buffer_refs, transport=transport)
+                            tied=tied_local, param_names=names, buffer_refs=buffer_refs, transport=transport,
+                            lag=getattr(plan, "p2p_lag", None) or _DEFAULT_LAG)
     engine.plan = plan
     if optimizer is not None:
         if not _is_fused(optimizer):

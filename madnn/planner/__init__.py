@@ -227,6 +227,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
                 best["mem_list"], spine, costs, cands, B, schedule=best.get("schedule", "1f1b"),
                 virtual=best.get("V", 1), tp=best.get("tp", 1), measured=measured)
     plan.calibration = calib
+    plan.p2p_lag = best.get("lag", 0.0)   # the pipeline engine's second issue plan (pp.issue_plan)
     plan.comm_probe = comm_probe
     plan.machine = hw
     plan.plan_s = time.perf_counter() - t_start
@@ -476,6 +477,7 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
     bucket_bytes = _bucket_bytes(cfg, costs, rb)
     rank_params = [sum(chunk_est[v].params for v in vs) for vs in ranks]
     opt_s = max(optimizer_s(p, opt, hw) for p in rank_params)
+    lag = 0.0
     if pp == 1:
         compute = rank_t[0]
         bubble = 0.0
@@ -487,7 +489,9 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
         p2p = max((costs[bounds[v + 1] - 1].out_bytes * mb for v in range(nst - 1)), default=0.0)
         # the engine's transport simulated with this node's (measured) P2P time: bubble AND the
         # transfers the schedule leaves on the critical path
-        pipe = transport_time(schedule, pp, M, V, max(rank_t) / V, hw.p2p_s(p2p))
+        chunk_s, p2p_s = max(rank_t) / V, hw.p2p_s(p2p)
+        pipe = transport_time(schedule, pp, M, V, chunk_s, p2p_s)
+        lag = 3.0 * p2p_s / chunk_s if chunk_s > 0 else 0.0   # one transfer in forward-chunk units
         bubble = pipeline_bubble(schedule, pp, M, V)
         comm_s = max(pipe - compute / max(1.0 - bubble, 1e-3), 0.0)   # transfers left on the critical path
         dp_s = 0.0
@@ -502,7 +506,8 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
     strategy = "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp")
     return {"strategy": strategy, "dp": dp, "pp": pp, "tp": 1, "M": M, "V": V, "schedule": schedule,
             "ckpt": ckpt, "bounds": bounds, "step_s": step, "compute_s": compute, "comm_s": comm_s,
-            "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits, "opt_s": opt_s}
+            "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits, "opt_s": opt_s,
+            "lag": lag}
 
 
 def _tp_linears(layer: nn.Module, tp: int, min_params: int, in_shape, in_dtype):

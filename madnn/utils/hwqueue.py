@@ -39,9 +39,10 @@ def _ranks(nstreams):
 
 
 def replay(kind: str, V: int, M: int, design: str, spin_us: int = 200, timeout_us: int = 300000,
-           streams: int = 7, epoch: int = 1) -> dict:
+           streams: int = 7, epoch: int = 1, lag: float = 0.0) -> dict:
     """Run one training step of both ranks' programs (``design``: ``engine`` = madnn's
-    ``issue_plan``, ``prepost`` = the round-3 engine) and count the messages that timed out."""
+    ``issue_plan`` at ``lag``, ``prepost`` = the round-3 engine) and count the messages that
+    timed out."""
     from ..ops import native_runtime
     from ..parallel.pp import issue_plan, recv_plan, virtual_stage
 
@@ -70,7 +71,7 @@ def replay(kind: str, V: int, M: int, design: str, spin_us: int = 200, timeout_u
         s = r.stage
         acts = []     # ("batch", stream_name, [(d, msg)], needs_last, is_recv) / ("compute", us)
         if design == "engine":
-            for item in issue_plan(kind, s, S, M, V):
+            for item in issue_plan(kind, s, S, M, V, lag):
                 if item[0] == "X":
                     for k in ("act", "grad"):
                         part = [(d, msg(d, kk, c, m, s)) for d, kk, c, m, _p in item[1] if kk == k]
@@ -143,5 +144,5 @@ def replay(kind: str, V: int, M: int, design: str, spin_us: int = 200, timeout_u
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     res = ok.cpu()
-    return {"schedule": kind, "V": V, "micro": M, "design": design, "messages": len(idx),
+    return {"schedule": kind, "V": V, "micro": M, "design": design, "lag": lag, "messages": len(idx),
             "timed_out": int((res == 0).sum()), "unset": int((res < 0).sum()), "wall_s": round(wall, 3)}

@@ -15,7 +15,8 @@ compute is a busy kernel (``hwq_spin``).  Every wait is bounded, so a program th
 on the queues shows up as timed-out messages.  Two programs per schedule:
 
 * ``engine``: madnn's ``issue_plan`` (boundary batches, activations / gradients on two
-  communicators, receive-only parts on a side stream);
+  communicators, receive-only parts on a side stream), at lag 0 and at lag 0.3 (boundaries on a
+  clock with transfers; the engine times both on a job and keeps the faster);
 * ``prepost``: the round-3 engine (every receive of the step posted up front on its channel's
   stream, sends after their producer).
 
@@ -37,6 +38,7 @@ def main():
     ap.add_argument("--spin-us", type=int, default=200)
     ap.add_argument("--timeout-us", type=int, default=300000)
     ap.add_argument("--streams", type=int, default=7, help="streams per rank (compute + comm)")
+    ap.add_argument("--reps", type=int, default=1, help="replays per (schedule, plan)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
@@ -49,11 +51,12 @@ def main():
     results = []
     epoch = 0
     for kind, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", 2)):
-        for design in ("engine", "prepost"):
-            epoch += 1
-            rec = replay(kind, V, args.micro, design, args.spin_us, args.timeout_us, args.streams, epoch)
-            results.append(rec)
-            print(json.dumps(rec), flush=True)
+        for design, lag in (("engine", 0.0), ("engine", 0.3), ("prepost", 0.0)):
+            for _rep in range(args.reps):
+                epoch += 1
+                rec = replay(kind, V, args.micro, design, args.spin_us, args.timeout_us, args.streams, epoch, lag)
+                results.append(rec)
+                print(json.dumps(rec), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"streams_per_rank": args.streams, "timeout_us": args.timeout_us, "spin_us": args.spin_us,

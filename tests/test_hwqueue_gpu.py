@@ -44,13 +44,16 @@ def test_probe_sees_a_setter_on_another_priority_queue(cuda):
     assert ok == 1 and ticks < 10_000_000
 
 
+@pytest.mark.parametrize("lag", [0.0, 0.3])
 @pytest.mark.parametrize("kind,V", [("gpipe", 1), ("1f1b", 1), ("interleaved", 2)])
-def test_engine_pipeline_program_completes_on_real_hw_queues(cuda, kind, V):
+def test_engine_pipeline_program_completes_on_real_hw_queues(cuda, kind, V, lag):
     """Both ranks of an S = 2 pipeline replayed on this GPU's hardware queues (one queue pool
-    per rank, seven streams each, rendezvous messages): madnn's issue plan never times out."""
+    per rank, seven streams each, rendezvous messages): both of madnn's issue plans complete
+    without a timed-out message."""
     import madnn.ops as ops
     from madnn.utils.hwqueue import replay
 
     assert ops.load_kernels()
-    rec = replay(kind, V, 8, "engine", spin_us=100, timeout_us=200000, epoch=100 + V + (kind == "gpipe"))
+    rec = replay(kind, V, 8, "engine", spin_us=100, timeout_us=200000,
+                 epoch=100 + V + (kind == "gpipe") + (10 if lag else 0), lag=lag)
     assert rec["timed_out"] == 0 and rec["unset"] == 0, rec

@@ -86,13 +86,23 @@ def _w_pp(rank, world, model_kind, schedule, dp, microbatches, steps, clip=None,
         ropt.step()
         ropt.zero_grad()
         if eng.holds_last and dp == 1:
-            torch.testing.assert_close(loss, rl.detach(), atol=1e-5, rtol=1e-5)
+            lt = 1e-5 if step < 3 else 2e-4      # Adam's drift over more steps (see below)
+            torch.testing.assert_close(loss, rl.detach(), atol=lt, rtol=lt)
+    if steps > 2 * len(eng._lags):
+        # both issue plans ran (steps 1 .. 2L) and every rank kept the same one
+        assert eng._tune["chosen"] is not None and eng.plan_lag == eng._lags[eng._tune["chosen"]]
+        import torch.distributed as dist
+
+        got = [None] * dist.get_world_size()
+        dist.all_gather_object(got, eng.plan_lag)
+        assert len(set(got)) == 1, got
     ref_params = dict(ref.named_parameters(remove_duplicate=False))
     mine = eng.state_dict()
     assert mine, "stage holds no parameters"
     # Adam (lr 1e-2) turns near-zero gradients into +-lr updates, so on the deeper model a few
-    # elements whose gradient rounds differently across the microbatch split move by ~1e-4
-    tol = 1e-3 if model_kind == "gpt8" else 5e-5
+    # elements whose gradient rounds differently across the microbatch split move by ~1e-4 (and
+    # so on any model after more than a few steps)
+    tol = 1e-3 if model_kind == "gpt8" or steps > 3 else 5e-5
     for name, p in mine.items():
         torch.testing.assert_close(p.detach(), ref_params[name].detach(), atol=tol, rtol=tol,
                                    msg=lambda m, name=name: f"{name}: {m}")
@@ -124,12 +134,12 @@ def test_pp_interleaved_parity(S, M, V):
 
 @pytest.mark.parametrize("schedule,dp,M,V", [("1f1b", 1, 8, None), ("interleaved", 1, 8, 2), ("gpipe", 1, 4, None)])
 def test_pp_4stages_parity_under_emulated_rccl(monkeypatch, schedule, dp, M, V):
-    """Same parity check with every channel group's P2P ops serialised in issue order, as
-    eagerly initialised RCCL communicators run them (3 steps: the 2nd and 3rd pre-post every
-    receive of the step)."""
+    """Same parity check with every P2P batch executed the way a fully serialised RCCL rank runs
+    it (rendezvous, complementary-batch check).  6 steps: the engine alternates its two issue
+    plans (lag 0 / lagged) in steps 1-4 and keeps the faster from step 5 on."""
     monkeypatch.setenv("MADNN_EMULATE_RCCL_P2P", "1")
     monkeypatch.setenv("MADNN_EMULATE_RCCL_P2P_TIMEOUT", "60")
-    run_dist(_w_pp, 4, "gpt8" if V else "gpt", schedule, dp, M, 3, None, V)
+    run_dist(_w_pp, 4, "gpt8" if V else "gpt", schedule, dp, M, 6, None, V)
 
 
 def test_pp_clip_grad_norm_is_global_and_tied_counted_once():

@@ -110,16 +110,19 @@ _PLANS = [(k, V, S, M) for S in (2, 4, 8) for k, V in (("gpipe", 1), ("1f1b", 1)
           for M in sorted({S, 8, 16, 32}) if k != "interleaved" or M % S == 0]
 
 
+@pytest.mark.parametrize("lag", [0.0, 0.3])
 @pytest.mark.parametrize("kind,V,S,M", _PLANS)
-def test_issue_plan_messages_pair_up_fifo(kind, V, S, M):
+def test_issue_plan_messages_pair_up_fifo(kind, V, S, M, lag):
     """Every message of every rank's issue plan is sent once and received once, in the same order
-    on both ends of each rank pair, and every compute's input comes from a batch before it."""
+    on both ends of each rank pair, and every compute's input comes from a batch before it --
+    for both plans the engine can run (boundaries on the compute-only clock, lag 0, and on a
+    clock with transfers 0.3 of a forward long)."""
     from madnn.parallel.pp import check_plan_fifo, issue_plan
 
-    assert check_plan_fifo(kind, S, M, V) == 2 * M * (S * V - 1)
+    assert check_plan_fifo(kind, S, M, V, lag) == 2 * M * (S * V - 1)
     for s in range(S):
         have = set()
-        for item in issue_plan(kind, s, S, M, V):
+        for item in issue_plan(kind, s, S, M, V, lag):
             if item[0] == "X":
                 assert 1 <= len(item[1]) <= 4
                 have |= {(k, c, m) for d, k, c, m, _p in item[1] if d == "recv"}
@@ -132,13 +135,14 @@ def test_issue_plan_messages_pair_up_fifo(kind, V, S, M):
                     assert ("grad", c, m) in have
 
 
+@pytest.mark.parametrize("lag", [0.0, 0.3])
 @pytest.mark.parametrize("kind,V,S,M", _PLANS)
-def test_pipeline_transport_safe_under_hw_queue_sharing(kind, V, S, M):
+def test_pipeline_transport_safe_under_hw_queue_sharing(kind, V, S, M, lag):
     """The engine's program (issue_plan on the act/grad communicators, DP all-reduce, tied sum)
     completes when every stream of a rank feeds ONE serialising hardware queue, on any rotation of
     a 4-queue (HIP's GPU_MAX_HW_QUEUES default) and a 2-queue round-robin pool, and with
     independent queues -- dp1 and dp2 meshes, steady state and the first step's host-blocking
-    shape headers."""
+    shape headers, for both issue plans the engine chooses between (lag 0 and 0.3)."""
     from madnn.parallel.pp import simulate_schedule, simulate_transport
 
     for dp in (1, 2):
@@ -146,9 +150,9 @@ def test_pipeline_transport_safe_under_hw_queue_sharing(kind, V, S, M):
             for q, offs in (("serial", [0]), (4, range(4)), (2, range(2)), (None, [0])):
                 for off in offs:
                     simulate_transport(kind, S, M, V, "split", q, dp=dp, tied=True, first_step=first,
-                                       queue_offset=off)
+                                       queue_offset=off, t_p2p=lag / 2, lag=lag)
     # with free transfers the transport adds no bubble over the compute-only schedule
-    r = simulate_transport(kind, S, M, V, "split", None)
+    r = simulate_transport(kind, S, M, V, "split", None, lag=lag)
     assert r["bubble"] == pytest.approx(simulate_schedule(kind, S, M, V)["bubble"], abs=1e-9)
 
 
@@ -727,9 +731,10 @@ def test_tuning_table_roundtrip(tmp_path):
 
 def test_planner_prices_pipelines_with_the_engine_transport():
     """transport_time = the simulated makespan of the engine's own transport: with free transfers
-    it is the compute-only schedule (M*chunk / (1 - bubble)); with transfers it grows, and the
-    1F1B exposure stays below GPipe's at the same transfer cost."""
-    from madnn.parallel.pp import pipeline_bubble, transport_time
+    it is the compute-only schedule (M*chunk / (1 - bubble)); with transfers it grows, and it is
+    the better of the engine's two issue plans: the one placed on a clock that includes the
+    transfer time hides most of GPipe's transfers, which the lag-0 plan leaves exposed."""
+    from madnn.parallel.pp import pipeline_bubble, simulate_transport, transport_time
 
     chunk = 3e-3
     for kind, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", 2)):
@@ -740,7 +745,9 @@ def test_planner_prices_pipelines_with_the_engine_transport():
     # a transfer of a quarter of a microbatch forward (chunk = forward + backward = 3 forwards)
     exp = {k: transport_time(k, 4, 16, 1, chunk, chunk / 12) / transport_time(k, 4, 16, 1, chunk, 0.0)
            for k in ("gpipe", "1f1b")}
-    assert 1.0 < exp["1f1b"] < exp["gpipe"]
+    lag0 = {k: simulate_transport(k, 4, 16, 1, "split", None, t_p2p=0.25)["makespan"]
+            / simulate_transport(k, 4, 16, 1, "split", None)["makespan"] for k in ("gpipe", "1f1b")}
+    assert 1.0 < exp["1f1b"] <= lag0["1f1b"] and 1.0 < exp["gpipe"] < lag0["gpipe"]
 
 
 def test_chain_calibration_rescales_activation_memory_at_a_batch_that_fits(monkeypatch):
