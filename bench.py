@@ -295,7 +295,12 @@ def bench_gpt2(args, world, rank):
 
     steps = args.gpt2_steps or args.steps
     warm = args.warmup if args.gpt2_warmup is None else args.gpt2_warmup
-    for _ in range(warm):
+    # a pipeline engine with two issue plans times them in its steps 1 .. 2L (PipelineEngine.
+    # _init_plans); those steps run before the warm-up proper, so the timed steps all use the
+    # plan it kept whatever --warmup is
+    tuning = 2 * len(getattr(engine, "_lags", [0.0])) if len(getattr(engine, "_lags", [0.0])) > 1 else 0
+    extra = max(0, tuning + 1 - warm)
+    for _ in range(extra + warm):
         step()
     _sync_all()
     t0 = time.perf_counter()
@@ -311,7 +316,8 @@ def bench_gpt2(args, world, rank):
             "planned_step_ms": round(engine.plan.est_step_s * 1e3, 2) if getattr(engine, "plan", None) else None,
             "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
             "virtual_stages": getattr(engine, "V", None) if stages > 1 else None,
-            "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "loss_last_stage": lv,
+            "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "plan_tuning_steps": extra,
+            "loss_last_stage": lv,
             "peak_mem_gib": _peak_gib(), "plan": _plan_info(plan), **_comm_fields(engine, plan)}
     return dt, steps, gbatch, info
 

@@ -106,6 +106,8 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     assert pp["plan"]["pp"] == 4 and pp["plan"]["strategy"] == "pp" and pp["plan"]["comm_measured"]
     assert 0 < pp["bubble_fraction"] < 1 and pp["p2p_gbps"] > 0 and pp["p2p_bytes"] > 0
     assert pp["pp_plan"]["lags"][0] == 0.0 and pp["pp_plan"]["kept"] in pp["pp_plan"]["lags"]
+    if len(pp["pp_plan"]["lags"]) > 1:   # both plans were timed before the warm-up
+        assert len(pp["pp_plan"]["step_ms"]) == 2 and pp["plan_tuning_steps"] == 4
 
 
 def _gpt2_8rank(extra_env=None, timeout=900, extra_args=()):
