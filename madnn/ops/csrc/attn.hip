@@ -27,6 +27,8 @@
 //    dispatched to one XCD work on the same heads, so K/V tiles hit in its L2.
 // Reference: the reference has no attention; this serves the
 // transformer configs of BASELINE.json (GPT-2 medium, BERT-large, Llama-3 8B).
+#include <type_traits>
+
 #include "attn.h"
 #include "common.h"
 
@@ -330,7 +332,11 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const MadnnAttnArgs
 }
 
 // ------------------------------------------------------------------ backward: dQ
-template <int D, bool CAUSAL, bool DELTA>
+struct RtIndex {  // a run-time LDS buffer index with the .value interface of std::integral_constant
+  int value;
+};
+
+template <int D, bool CAUSAL, bool DELTA, bool U2>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
@@ -387,8 +393,9 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
   stk.store(sK[0], tid);
   stv.store(sV[0], tid);
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+  int t = 0;
+  auto tile = [&](auto curc) {  // U2: as in the dK/dV kernel
+    const int cur = curc.value;
     const bool more = t + 1 < ntiles;
     if (more) {
       stk.load(kb_, a.k_ss, (t + 1) * kTile, a.S, tid);
@@ -444,6 +451,16 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       stv.store(sV[cur ^ 1], tid);
     }
     __syncthreads();
+    ++t;
+  };
+  if constexpr (U2) {
+    while (t + 1 < ntiles) {
+      tile(std::integral_constant<int, 0>{});
+      tile(std::integral_constant<int, 1>{});
+    }
+    if (t < ntiles) tile(std::integral_constant<int, 0>{});
+  } else {
+    while (t < ntiles) tile(RtIndex{t & 1});
   }
   if (qrow < a.S) {
     uint16_t* qp = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow * a.dq_ss;
@@ -487,7 +504,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
 }
 
 // --------------------------------------------------------------- backward: dK, dV
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, bool U2>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[2][kTile * D];
@@ -562,8 +579,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   }
   __syncthreads();
   int cur_t = 0, nxt_h = 0, nxt_t = 0;  // this tile's query-tile index; the next tile's (head, tile)
-  for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
+  // U2: two tiles per trip with the LDS buffer index a compile-time constant, so the buffer base
+  // folds into the ds_read immediate offsets instead of costing a VALU op per read address
+  int it = 0;
+  auto tile = [&](auto curc) {
+    const int cur = curc.value;
     const bool more = it + 1 < total;
     if (++nxt_t == nt) {
       nxt_t = 0;
@@ -633,6 +653,16 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
       put_stats(stat_next, cur ^ 1);
     }
     __syncthreads();
+    ++it;
+  };
+  if constexpr (U2) {
+    while (it + 1 < total) {
+      tile(std::integral_constant<int, 0>{});
+      tile(std::integral_constant<int, 1>{});
+    }
+    if (it < total) tile(std::integral_constant<int, 0>{});
+  } else {
+    while (it < total) tile(RtIndex{it & 1});
   }
   // lane holds dK/dV[key = k0w + acc_row(r, hh)][d = 32*db + l32]
   uint16_t* kp = a.dk + b * a.dk_sb + hk * a.dk_sh;
@@ -702,6 +732,8 @@ int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default),
 // (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
 // their loops are not VALU-issue-bound)
 int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
+int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
+int g_attn_dq_u2 = 1;     // madnn_attn_tune(3, v): the same for the dQ loop
 
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
@@ -718,15 +750,23 @@ template <int D, bool CAUSAL>
 hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nb = (a.S + kRowsWG - 1) / kRowsWG;
   if (g_attn_dq_delta) {
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+    if (g_attn_dq_u2) {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+    }
   } else {
     const int64_t lanes = (int64_t)a.B * a.S * a.H * (D / 8);
     hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((lanes + 255) / 256), dim3(256), 0, st, a);
     MADNN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
   }
   MADNN_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  if (g_attn_bwd_u2) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, false>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -740,10 +780,11 @@ extern "C" {
 
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 
-// A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0);
+// A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0),
+// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0);
 // returns the previous value
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : nullptr;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;
