@@ -3,6 +3,7 @@ flipped between interleaved timing windows on the same box, so both arms see the
 state and clocks):
 
     python bench/resnet_flag_ab.py --flag madnn.models.resnet:_DUAL_BN --batch 1536 --windows 6 --steps 5
+    python bench/resnet_flag_ab.py --flag bn_tune:multi --on 1=1,3=1 --off 1=3,3=0   # several native keys
 """
 import argparse
 import importlib
@@ -48,7 +49,12 @@ def main():
 
         class _Native:
             def __setattr__(self, k, v):
-                tune(int(k), int(v))
+                if k == "multi":   # --flag bn_tune:multi --on 3=1,1=2 --off 3=0,1=3: several keys per arm
+                    for kv in str(v).split(","):
+                        kk, vv = kv.split("=")
+                        tune(int(kk), int(vv))
+                else:
+                    tune(int(k), int(v))
 
         mod = _Native()
     else:
