@@ -11,16 +11,21 @@ configs 3 and 4 require it.  Design for one MI355X node:
   (``madnn_pipeline_order``): GPipe, 1F1B, or interleaved 1F1B where every rank
   holds V chunks (virtual stages c*S + rank), shrinking the bubble from
   (S-1)/(M+S-1) toward (S-1)/(V*M+S-1);
-* communication is derived from that order (``issue_plan``): between two
-  computes ONE batched exchange with the neighbours -- the previous compute's
-  output out, the next compute's input in -- issued as a single
-  ``batch_isend_irecv`` on the replica's pipeline communicator (one RCCL kernel
-  per batch, one RCCL stream per rank for all P2P traffic).  Each rank's
-  program completes even when every GPU operation of the rank runs one at a
-  time in issue order, which is what makes it safe on MI355X, where HIP
-  multiplexes the process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues
-  that may serialise dispatches of different streams (``simulate_transport``
-  models the queues; ``scripts/hwqueue_probe.py`` measures the sharing);
+* communication is derived from that order (``issue_plan``): every message
+  sits in the batch of its producer's finish time on a global schedule clock,
+  on both ranks; a batch is at most two ``batch_isend_irecv`` calls (one RCCL
+  kernel each): activations on the replica's pipeline communicator, gradients
+  on a second one over the same ranks (``P2PTransport``).  Each rank's program
+  completes even when every GPU operation of the rank runs one at a time in
+  issue order, which is what makes it safe on MI355X, where HIP multiplexes the
+  process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues that may
+  serialise dispatches of different streams (``simulate_transport`` models the
+  queues; ``scripts/hwqueue_probe.py`` measures the sharing).  Two plans --
+  boundaries on the compute-only clock and on one with transfer time -- are
+  timed in the first steps and the faster is kept.  Reference contrast: the
+  reference's collectives are blocking and one at a time
+  (datamodule.lua:214-222, nodemodule.lua:52,66,103,117), which cannot deadlock
+  but cannot overlap either;
 * gradients of each rank are reduced over its DP group by the bucketed
   ``DataParallel`` reducer during each chunk's LAST microbatch backward
   (``no_sync`` before) on links disjoint from the PP hops;
