@@ -88,6 +88,10 @@ def _w_pp(rank, world, model_kind, schedule, dp, microbatches, steps, clip=None,
         if eng.holds_last and dp == 1:
             lt = 1e-5 if step < 3 else 2e-4      # Adam's drift over more steps (see below)
             torch.testing.assert_close(loss, rl.detach(), atol=lt, rtol=lt)
+    from madnn.parallel.pp import _DEFAULT_LAG, plan_lag
+
+    # the second issue plan sits at the transfer time the planner priced (or the default)
+    assert eng._lags[0] == 0.0 and all(g == plan_lag(eng.plan.p2p_lag or _DEFAULT_LAG) for g in eng._lags[1:])
     if steps > 2 * len(eng._lags):
         # both issue plans ran (steps 1 .. 2L) and every rank kept the same one
         assert eng._tune["chosen"] is not None and eng.plan_lag == eng._lags[eng._tune["chosen"]]
