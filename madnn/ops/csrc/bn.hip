@@ -19,6 +19,8 @@
 // "Global float atomics") and produces the per-channel affine coefficients, the
 // running-stat update and the num_batches_tracked increment (so no extra host
 // launches per layer).
+#include <type_traits>
+
 #include "common.h"
 
 namespace madnn {
@@ -51,7 +53,7 @@ struct BnTune {
   int reverse = 1;
   int wg_per_cu = 3;
   int hoist = 1;
-  int unroll = 0;  // 1: apply walks handle two chunks per trip (more loads in flight)
+  int unroll = 0;  // 1 / 2: apply walks handle two / four chunks per trip (more loads in flight)
   int partials_per_cu = 2;  // reduction passes (statistics, backward sums): workgroups = partial rows per CU
   //                            (ResNet-50 b512, profiles/r4_ab_bn_partials_*: 1 -1.8 %, 4 -0.5 % against 2)
 };
@@ -59,9 +61,11 @@ inline BnTune& bn_tune() {
   static BnTune t;
   return t;
 }
-// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting, bit 2 unroll
+// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting, bit 2 two
+// chunks per trip, bit 3 four chunks per trip
 inline int bn_walk_flags() {
-  return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2) | (bn_tune().unroll ? 4 : 0);
+  const int u = bn_tune().unroll;
+  return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2) | (u == 1 ? 4 : u >= 2 ? 8 : 0);
 }
 
 // grid-stride walk of [0, total) in 8-element lane chunks, forward or back-to-front; c0 tracks
@@ -277,23 +281,29 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
       if (mask) mask[i >> 3] = (unsigned char)bits;
     }
   };
-  if (fixed && (reverse & 4)) {  // two chunks per trip: both chunks' loads issued before either store
-    while (w.n >= 2) {
-      const int64_t i0 = w.i;
-      w.next();
-      const int64_t i1 = w.i;
-      w.next();
-      float v0[8], v1[8], r0[8], r1[8];
-      load8<XDT>(x, i0, v0);
-      load8<XDT>(x, i1, v1);
-      if constexpr (RES) {
-        load8<XDT>(res, i0, r0);
-        load8<XDT>(res, i1, r1);
+  // U chunks per trip: every chunk's loads issued before the first store
+  auto trips = [&](auto uc) {
+    constexpr int U = decltype(uc)::value;
+    while (w.n >= U) {
+      int64_t ix[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ix[u] = w.i;
+        w.next();
       }
-      body(i0, v0, r0);
-      body(i1, v1, r1);
+      float v[U][8], r[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load8<XDT>(x, ix[u], v[u]);
+      if constexpr (RES) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8<XDT>(res, ix[u], r[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(ix[u], v[u], r[u]);
     }
-  }
+  };
+  if (fixed && (reverse & 8)) trips(std::integral_constant<int, 4>{});
+  if (fixed && (reverse & 4)) trips(std::integral_constant<int, 2>{});
   for (; w.n > 0; w.next()) {
     const int64_t i = w.i;
     if (!fixed) coef(w.c0);
@@ -506,25 +516,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       if (dres != nullptr) store8<XDT>(dres, i, dv);  // null: the consumer masks dy itself (resmask)
     }
   };
-  if (fixed && (reverse & 4)) {  // two chunks per trip (see bn_apply_kernel)
-    while (w.n >= 2) {
-      const int64_t i0 = w.i;
-      w.next();
-      const int64_t i1 = w.i;
-      w.next();
-      float d0[8], d1[8], x0[8], x1[8], q0[8], q1[8];
-      load8<XDT>(dy, i0, d0);
-      load8<XDT>(dy, i1, d1);
-      load8<XDT>(x, i0, x0);
-      load8<XDT>(x, i1, x1);
-      if constexpr (RAFF) {
-        load8<XDT>(rin, i0, q0);
-        load8<XDT>(rin, i1, q1);
+  auto trips = [&](auto uc) {  // U chunks per trip (see bn_apply_kernel)
+    constexpr int U = decltype(uc)::value;
+    while (w.n >= U) {
+      int64_t ix[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ix[u] = w.i;
+        w.next();
       }
-      body(i0, d0, x0, q0);
-      body(i1, d1, x1, q1);
+      float d[U][8], xv[U][8], q[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load8<XDT>(dy, ix[u], d[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) load8<XDT>(x, ix[u], xv[u]);
+      if constexpr (RAFF) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load8<XDT>(rin, ix[u], q[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(ix[u], d[u], xv[u], q[u]);
     }
-  }
+  };
+  if (fixed && (reverse & 8)) trips(std::integral_constant<int, 4>{});
+  if (fixed && (reverse & 4)) trips(std::integral_constant<int, 2>{});
   for (; w.n > 0; w.next()) {
     const int64_t i = w.i;
     if (!fixed) coef(w.c0);
@@ -600,7 +615,8 @@ static int bn_grid_rows(int64_t M, int C) {
 extern "C" {
 
 // key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU, 2: coefficient hoisting
-// (0/1), 3: apply unroll (0/1), 4: reduction workgroups (partial rows) per CU; value < 0 only reads.
+// (0/1), 3: apply chunks per trip (0: one, 1: two, 2: four), 4: reduction workgroups (partial rows) per
+// CU; value < 0 only reads.
 // Key 4 sizes the partial slabs: change it only between steps (every call sizes its own workspace).
 // Returns the old value (-1 for an unknown key).
 int madnn_bn_tune(int key, int value) {
@@ -612,8 +628,11 @@ int madnn_bn_tune(int key, int value) {
                       : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value >= 0) *f = key == 1 ? (value < 1 ? 1 : value) : key == 4 ? (value < 1 ? 1 : value > 8 ? 8 : value)
-                                                                     : (value != 0);
+  if (value >= 0)
+    *f = key == 1 ? (value < 1 ? 1 : value)
+         : key == 4 ? (value < 1 ? 1 : value > 8 ? 8 : value)
+         : key == 3 ? (value > 2 ? 2 : value)
+                    : (value != 0);
   return old;
 }
 

@@ -631,7 +631,7 @@ def test_bn_relu_maxpool_fused_matches_fp32(cuda, shape, with_stats):
 
 
 def test_batchnorm_apply_walk_variants_bitwise(cuda):
-    """The BN apply walks (coefficient hoisting on/off, one or two chunks per trip) are pure
+    """The BN apply walks (coefficient hoisting on/off, one, two or four chunks per trip) are pure
     scheduling changes: outputs and gradients must be bitwise identical across them."""
     import ctypes
 
@@ -647,7 +647,7 @@ def test_batchnorm_apply_walk_variants_bitwise(cuda):
     outs = []
     old = (tune(2, -1), tune(3, -1))
     try:
-        for hoist, unroll in ((0, 0), (1, 0), (1, 1)):
+        for hoist, unroll in ((0, 0), (1, 0), (1, 1), (1, 2)):
             tune(2, hoist)
             tune(3, unroll)
             res = []
@@ -661,12 +661,12 @@ def test_batchnorm_apply_walk_variants_bitwise(cuda):
     finally:
         tune(2, old[0])
         tune(3, old[1])
-    # hoisting is bitwise neutral; the two-chunk walk lets the compiler contract the backward's
-    # a*g + b*x + c differently, so its gradients may differ in the last bf16 place
+    # hoisting is bitwise neutral; the two- and four-chunk walks let the compiler contract the
+    # backward's a*g + b*x + c differently, so their gradients may differ in the last bf16 place
     bad = [(v, k, (a.float() - b.float()).abs().max().item())
            for v, other in enumerate(outs[1:], 1) for k, (a, b) in enumerate(zip(outs[0], other))
            if not torch.equal(a, b)]
-    assert all(v == 2 and k in (1, 2, 4, 5) for v, k, _ in bad), bad
+    assert all(v >= 2 and k in (1, 2, 4, 5) for v, k, _ in bad), bad
     for v, k, d in bad:
         ref = outs[0][k].float().abs().max().item()
         assert d <= 2 ** -7 * max(ref, 1.0), (v, k, d, ref)
