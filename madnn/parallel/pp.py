@@ -850,7 +850,7 @@ class PipelineEngine:
     def __init__(self, stage_module: PipelineStage, *, stage: int, nstages: int, groups: rt.ProcessGroups,
                  microbatches: int, schedule: str, loss_fn: Callable, dp_engine: DataParallel,
                  cast_dtype, tied: List[tuple], param_names: Dict[int, str], buffer_refs=(),
-                 transport: Optional[P2PTransport] = None, lag: float = 0.0):
+                 transport: Optional[P2PTransport] = None, lag: float = 0.0, sig_group=None):
         self.module = stage_module
         self.chunks = list(stage_module.chunks)
         self.V = len(self.chunks)
@@ -867,6 +867,7 @@ class PipelineEngine:
         self.param_names = param_names
         self.buffer_refs = list(buffer_refs)   # (original name, owner module, local name)
         self.transport = transport
+        self.sig_group = sig_group
         self.order = native_runtime.pipeline_order(schedule, stage, nstages, microbatches, self.V)
         self._init_plans(lag)
         S, SV = nstages, nstages * self.V
@@ -978,11 +979,16 @@ class PipelineEngine:
             ts = list(targets.chunk(M))
             if len(ts) != M:
                 raise ValueError(f"targets of {targets.shape[0]} do not split into {M} microbatches")
-        # every rank of a pipeline must see the same batch SHAPE each step (ranks without the
-        # first/last chunk may pass None): the header exchange is keyed on it
+        # the header exchange is keyed on the batch signature; ranks without the first / last
+        # chunk may pass None, so the pipeline agrees on "new signature" every step (a host-side
+        # MAX over the replica's ranks: no device synchronisation)
         ref = inputs if inputs is not None else targets
         sig = (tuple(ref.shape), ref.dtype) if ref is not None else "static"
         new_sig = sig != self._sig
+        if self.sig_group is not None and dist.get_world_size(self.sig_group) > 1:
+            flag = torch.tensor([1 if new_sig else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.sig_group)
+            new_sig = bool(flag.item())
         if self.dp._needs_finalize:
             # gradient accumulation across train_step calls (no optimizer step in between)
             if self.tied:
@@ -1268,10 +1274,16 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     groups = rt.ProcessGroups(mesh)
     # the gradient communicator of every pipeline replica (same ranks as its pipeline group)
     grad_groups = []
+    # a host-side (gloo) group per replica for the per-step input-signature agreement: ranks
+    # without the first / last chunk may pass None and cannot see a shape change themselves
+    sig_groups = []
     if S > 1:
+        gloo = dist.is_initialized() and dist.get_backend() == "gloo"
         for d in range(plan.dp):
             ranks = [mesh.rank_of(d, s, 0) for s in range(S)]
             grad_groups.append(dist.new_group(ranks) if dist.is_initialized() else None)
+            sig_groups.append(None if not dist.is_initialized() else
+                              grad_groups[-1] if gloo else dist.new_group(ranks, backend="gloo"))
     stage = groups.pp_idx
     ranges = _chunk_layer_ranges(plan, stage, S, V)
     all_layers = plan.spine.layers
@@ -1343,7 +1355,8 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
                             schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
                             tied=tied_local, param_names=names, buffer_refs=buffer_refs, transport=transport,
-                            lag=getattr(plan, "p2p_lag", None) or _DEFAULT_LAG)
+                            lag=getattr(plan, "p2p_lag", None) or _DEFAULT_LAG,
+                            sig_group=sig_groups[groups.dp_idx] if sig_groups else None)
     engine.plan = plan
     if optimizer is not None:
         if not _is_fused(optimizer):

@@ -255,3 +255,39 @@ def _w_emulated_transport_catches_unpaired_batches(rank, world):
 def test_emulated_serial_transport_detects_unpaired_batches():
     """Regression check of the CPU emulation itself (MADNN_EMULATE_RCCL_P2P)."""
     run_dist(_w_emulated_transport_catches_unpaired_batches, 2)
+
+
+def _w_plan_tuning_with_shape_change(rank, world):
+    """The issue plan of a step is a function of the step count alone: when the batch shape
+    changes in the middle of the plan tuning (steps 1-4), the first / last stage exchange new
+    shape headers while the interior stages do not, and every rank still runs the same plan
+    (under the serial emulation a mismatch would raise "transport deadlock")."""
+    import os
+
+    import torch.distributed as dist
+
+    import madnn
+    from madnn.optim import FusedAdam
+
+    os.environ["MADNN_EMULATE_RCCL_P2P"] = "1"
+    os.environ["MADNN_EMULATE_RCCL_P2P_TIMEOUT"] = "60"
+    model = _gpt_tiny(8)
+    opt = FusedAdam(model.parameters(), lr=1e-3)
+    eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=4, microbatches=4, schedule="interleaved",
+                                virtual_stages=2, example_input=torch.zeros(1, 32, dtype=torch.long),
+                                loss_fn=model.loss_fn, checkpointing="none", global_batch=8)
+    assert len(eng._lags) == 2
+    g = torch.Generator().manual_seed(7)
+    for step in range(7):
+        seq = 32 if step != 2 else 16          # a new input signature at a tuning step
+        ids = torch.randint(0, 512, (8, seq), generator=g)
+        # interior ranks pass nothing: their signature stays "static", only the ends see the change
+        eng.train_step(ids if eng.holds_first else None, ids if eng.holds_last else None)
+        opt.step()
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, (eng.plan_lag, eng._tune["chosen"]))
+    assert len(set(got)) == 1 and got[0][1] is not None, got
+
+
+def test_plan_tuning_survives_a_shape_change_mid_tuning():
+    run_dist(_w_plan_tuning_with_shape_change, 4)
