@@ -336,7 +336,7 @@ struct RtIndex {  // a run-time LDS buffer index with the .value interface of st
   int value;
 };
 
-template <int D, bool CAUSAL, bool DELTA, bool U2>
+template <int D, bool CAUSAL, bool DELTA, bool U2, bool LIM = false>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
@@ -417,13 +417,24 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       // masking as one wave-uniform block on the scores (exp2(-inf) = 0): interior tiles run
       // none of it (a per-element `if` costs an exec-mask branch per element)
       if ((k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w)) {
+        if constexpr (LIM) {
+          // LIM: key = k0 + off + 4 hh with off = kb*32 + acc_row(r, 0) a compile-time constant, so
+          // the mask is one compare of that constant against a per-lane limit
+          const int lim = (CAUSAL ? min(qrow, a.S - 1) : a.S - 1) - k0 - 4 * hh;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+          for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kb * 32 + acc_row(r, hh);
-            const bool ok = key < a.S && (!CAUSAL || key <= qrow);
-            sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
+            for (int r = 0; r < 16; ++r) sc[kb][r] = (kb * 32 + acc_row(r, 0) <= lim) ? sc[kb][r] : -__builtin_inff();
+          }
+        } else {
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + kb * 32 + acc_row(r, hh);
+              const bool ok = key < a.S && (!CAUSAL || key <= qrow);
+              sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
+            }
           }
         }
       }
@@ -504,7 +515,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
 }
 
 // --------------------------------------------------------------- backward: dK, dV
-template <int D, bool CAUSAL, bool U2>
+template <int D, bool CAUSAL, bool U2, bool LIM = false>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[2][kTile * D];
@@ -613,12 +624,21 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
         }
       }
       if (CAUSAL && q0 < k0w + 31) {  // diagonal tile: one wave-uniform masking block
+        if constexpr (LIM) {
+          const int lo = krow - q0 - 4 * hh;  // query offset qb*32 + acc_row(r, 0) must reach it
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
+          for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int qi = qb * 32 + acc_row(r, hh);
-            sc[qb][r] = (krow <= q0 + qi) ? sc[qb][r] : -__builtin_inff();
+            for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : -__builtin_inff();
+          }
+        } else {
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int qi = qb * 32 + acc_row(r, hh);
+              sc[qb][r] = (krow <= q0 + qi) ? sc[qb][r] : -__builtin_inff();
+            }
           }
         }
       }
@@ -734,6 +754,7 @@ int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default),
 int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
 int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
 int g_attn_dq_u2 = 1;     // madnn_attn_tune(3, v): the same for the dQ loop
+int g_attn_mask_lim = 1;  // madnn_attn_tune(5, v): backward masks as one compare against a per-lane limit (0: per element)
 
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
@@ -750,7 +771,10 @@ template <int D, bool CAUSAL>
 hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nb = (a.S + kRowsWG - 1) / kRowsWG;
   if (g_attn_dq_delta) {
-    if (g_attn_dq_u2) {
+    if (g_attn_dq_u2 && g_attn_mask_lim) {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st,
+                         a);
+    } else if (g_attn_dq_u2) {
       hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
     } else {
       hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
@@ -762,7 +786,9 @@ hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
   }
   MADNN_HIP_CHECK(hipGetLastError());
-  if (g_attn_bwd_u2) {
+  if (g_attn_bwd_u2 && g_attn_mask_lim) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  } else if (g_attn_bwd_u2) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, false>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
@@ -781,10 +807,10 @@ extern "C" {
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 
 // A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0),
-// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0);
+// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0), key 5 = backward masks against a per-lane limit;
 // returns the previous value
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : nullptr;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;
