@@ -39,7 +39,7 @@ KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "
 RUNTIME_SOURCES = ["runtime.cpp"]
 # per-source extra flags: MFMA kernels keep their accumulators in the (unified) VGPR file
 # instead of AGPRs, which removes a v_accvgpr_read/write around every softmax element
-EXTRA_FLAGS = {"attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+EXTRA_FLAGS = {"attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _hipcc() -> str:

@@ -113,20 +113,38 @@ __device__ __forceinline__ bf16x8 pack_acc(const f32x16& x, int s) {
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // [64][D] tile: global (row stride `ld` elements, rows >= nvalid read as zeros) -> regs -> LDS.
-template <int D>
+// BUF (the backward kernels): buffer loads through a per-tile descriptor (base at row0, range = the
+// nvalid - row0 rows left): rows past the end come back as zeros from the range check, so the load
+// needs no branch, no zero fill and no 64-bit address arithmetic -- the per-lane byte offset is
+// tile-invariant (cdna_hip_programming.md T8 / T20: the descriptor is built from wave-uniform values
+// only).  Measured: backward -8 % at D = 128, neutral at D = 64; the forward kernel keeps the global
+// loads (+23 % forward time at D = 128 with BUF, profiles/r4_ab_attn_valu_trees.log).
+template <int D, bool BUF = false>
 struct TileStage {
   static constexpr int CH = D / 8;
   static constexpr int PER = kTile * CH / kThreads;
   u32x4 r[PER];
   __device__ __forceinline__ void load(const uint16_t* base, int64_t ld, int row0, int nvalid, int tid) {
+    if constexpr (BUF) {
+      const int64_t left = (int64_t)max(nvalid - row0, 0) * ld * 2;
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint16_t*>(base + (int64_t)row0 * ld), 0, (int)min(left, (int64_t)0x7fffffff), 0x00020000);
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = tid + kThreads * i;
-      const int row = c / CH, ch = c % CH;
-      if (row0 + row < nvalid) {
-        r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * ld + ch * 8);
-      } else {
-        r[i] = u32x4{0u, 0u, 0u, 0u};
+      for (int i = 0; i < PER; ++i) {
+        const int c = tid + kThreads * i;
+        const int row = c / CH, ch = c % CH;
+        r[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(row * ld + ch * 8) * 2, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = tid + kThreads * i;
+        const int row = c / CH, ch = c % CH;
+        if (row0 + row < nvalid) {
+          r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * ld + ch * 8);
+        } else {
+          r[i] = u32x4{0u, 0u, 0u, 0u};
+        }
       }
     }
   }
@@ -197,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
   const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
   const int ntiles = (kv_end + kTile - 1) / kTile;
 
-  TileStage<D> stk, stv;
+  TileStage<D> stk, stv;  // global loads (see TileStage)
   stk.load(kb_, a.k_ss, 0, a.S, tid);
   stv.load(vb_, a.v_ss, 0, a.S, tid);
   stk.store(sK[0], tid);
@@ -336,7 +354,9 @@ struct RtIndex {  // a run-time LDS buffer index with the .value interface of st
   int value;
 };
 
-template <int D, bool CAUSAL, bool DELTA, bool U2, bool LIM = false>
+// ACCD: the dP^T accumulators start at -delta (a loop-invariant register tuple: delta belongs to the
+// lane's query row), so dS = P * acc costs no subtraction
+template <int D, bool CAUSAL, bool DELTA, bool U2, bool LIM = false, bool ACCD = false>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
@@ -385,9 +405,12 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
   f32x16 dq[DB];
 #pragma unroll
   for (int d = 0; d < DB; ++d) dq[d] = zero16();
+  f32x16 ndl;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ndl[r] = -dl;
   const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
   const int ntiles = (kv_end + kTile - 1) / kTile;
-  TileStage<D> stk, stv;
+  TileStage<D, true> stk, stv;
   stk.load(kb_, a.k_ss, 0, a.S, tid);
   stv.load(vb_, a.v_ss, 0, a.S, tid);
   stk.store(sK[0], tid);
@@ -407,7 +430,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         sc[kb] = zero16();
-        dp[kb] = zero16();
+        dp[kb] = ACCD ? ndl : zero16();
 #pragma unroll
         for (int s = 0; s < DS; ++s) {
           sc[kb] = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
@@ -443,7 +466,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -lse));
-          sc[kb][r] = p * (dp[kb][r] - dl);
+          sc[kb][r] = ACCD ? p * dp[kb][r] : p * (dp[kb][r] - dl);
         }
       }
       // dQ^T[d][q] += sum_key K[key][d] dS^T[key][q]
@@ -515,7 +538,9 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
 }
 
 // --------------------------------------------------------------- backward: dK, dV
-template <int D, bool CAUSAL, bool U2, bool LIM = false>
+// ACCD: the tile's -delta rows are read from LDS straight into the dP accumulator before its MFMAs
+// (dP - delta then costs no VALU: dS = P * acc)
+template <int D, bool CAUSAL, bool U2, bool LIM = false, bool ACCD = false>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[2][kTile * D];
@@ -560,13 +585,18 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   // the tile's LSE (threads 0..63) / delta (64..127) row statistics: fetched into a register
   // together with the tile's Q/dO loads and written to LDS with them, so their global-load
   // latency is covered by the tile's compute (a load stored right away exposes it every tile)
+  // (one buffer load per lane of waves 0 / 1 through a descriptor that ends at row S: a row past the
+  // end reads 0 for both -- harmless, since its Q and dO rows are zeros, so its P and dS terms
+  // multiply zero operands)
+  const int swave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform to the compiler
   auto fetch_stats = [&](int hq, int q0) -> float {
     float v = 0.f;
-    if (tid < 2 * kTile) {
-      const int q = q0 + (tid & (kTile - 1));
-      const int64_t sr = ((int64_t)b * a.H + hq) * a.S + min(q, a.S - 1);
-      v = tid < kTile ? a.lse[sr] : a.delta[sr];
-      if (q >= a.S) v = tid < kTile ? __builtin_inff() : 0.f;
+    if (swave < 2) {
+      const float* arr = (swave == 0 ? a.lse : a.delta) + ((int64_t)b * a.H + hq) * a.S + q0;
+      const __amdgpu_buffer_rsrc_t rsrc =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(arr), 0, max(a.S - q0, 0) * 4, 0x00020000);
+      v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, lane * 4, 0, 0));
+      if (ACCD && swave == 1) v = -v;
     }
     return v;
   };
@@ -577,7 +607,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
       sD[buf][tid - kTile] = v;
     }
   };
-  TileStage<D> stq, sto;
+  TileStage<D, true> stq, sto;
   if (total > 0) {
     const uint16_t *qp, *dp;
     int q0, hq;
@@ -616,7 +646,12 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         sc[qb] = zero16();
-        dp[qb] = zero16();
+        if constexpr (ACCD) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dp[qb][r] = sD[cur][qb * 32 + acc_row(r, hh)];
+        } else {
+          dp[qb] = zero16();
+        }
 #pragma unroll
         for (int s = 0; s < DS; ++s) {
           sc[qb] = mfma(lds_row<D>(sQ[cur], qb * 32 + l32, 2 * s + hh), kf[s], sc[qb]);
@@ -649,7 +684,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
           const int qi = qb * 32 + acc_row(r, hh);
           const float p = ex2(fmaf(sc[qb][r], a.scale_log2, -sL[cur][qi]));
           sc[qb][r] = p;
-          dp[qb][r] = p * (dp[qb][r] - sD[cur][qi]);
+          dp[qb][r] = ACCD ? p * dp[qb][r] : p * (dp[qb][r] - sD[cur][qi]);
         }
       }
       // dV[key][d] += sum_q P[q][key] dO[q][d];  dK[key][d] += sum_q dS[q][key] Q[q][d]
@@ -755,6 +790,9 @@ int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ
 int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
 int g_attn_dq_u2 = 1;     // madnn_attn_tune(3, v): the same for the dQ loop
 int g_attn_mask_lim = 1;  // madnn_attn_tune(5, v): backward masks as one compare against a per-lane limit (0: per element)
+// madnn_attn_tune(6, v): dQ and dK/dV kernels start the dP accumulators at -delta (with keys 2/3 and 5 on; D = 64
+// only: backward -1..-2 % at D = 64, +8 % at D = 128, profiles/r4_ab_attn_valu_trees.log)
+int g_attn_dkdv_accd = 1;
 
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
@@ -771,7 +809,10 @@ template <int D, bool CAUSAL>
 hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nb = (a.S + kRowsWG - 1) / kRowsWG;
   if (g_attn_dq_delta) {
-    if (g_attn_dq_u2 && g_attn_mask_lim) {
+    if (D == 64 && g_attn_dq_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true, true, D == 64>), dim3(nb * a.B * a.H), dim3(kThreads),
+                         0, st, a);
+    } else if (g_attn_dq_u2 && g_attn_mask_lim) {
       hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st,
                          a);
     } else if (g_attn_dq_u2) {
@@ -786,7 +827,10 @@ hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
   }
   MADNN_HIP_CHECK(hipGetLastError());
-  if (g_attn_bwd_u2 && g_attn_mask_lim) {
+  if (D == 64 && g_attn_bwd_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true, D == 64>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0,
+                       st, a);
+  } else if (g_attn_bwd_u2 && g_attn_mask_lim) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
   } else if (g_attn_bwd_u2) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
@@ -807,10 +851,11 @@ extern "C" {
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 
 // A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0),
-// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0), key 5 = backward masks against a per-lane limit;
+// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0), key 5 = backward masks against a per-lane limit,
+// key 6 = dP accumulators started at -delta;
 // returns the previous value
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : nullptr;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;

@@ -127,3 +127,36 @@ def test_qkv_bias_grad_from_attention_colsum(cuda, monkeypatch, H, HKV, D, S):
     q, k, v = qf.split([H, HKV, HKV], dim=2)
     (_ref(q, k, v, True, D ** -0.5) * g).sum().backward()
     assert _rel(b.grad, bf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2 and _rel(x.grad, xf.grad) < 2e-2
+
+
+# the A/B variants kept behind madnn_attn_tune (attn.hip): key -> the non-default value tested
+_VARIANTS = [(0, 0), (1, 0), (2, 0), (3, 0), (5, 0), (6, 1)]
+
+
+@pytest.mark.parametrize("key,value", _VARIANTS)
+@pytest.mark.parametrize("B,S,H,HKV,D,causal", [(1, 200, 4, 2, 64, True), (1, 130, 2, 2, 128, False),
+                                                (1, 384, 4, 1, 128, True)])
+def test_attention_tunable_variants_match_reference(cuda, key, value, B, S, H, HKV, D, causal):
+    import ctypes
+
+    assert ops.load_kernels()
+    knob = ctypes.CDLL(str(ops.kernels_path())).madnn_attn_tune
+    old = knob(key, value)
+    assert old >= 0
+    try:
+        torch.manual_seed(1)
+        q = torch.randn(B, S, H, D, device=cuda).bfloat16().requires_grad_(True)
+        k = torch.randn(B, S, HKV, D, device=cuda).bfloat16().requires_grad_(True)
+        v = torch.randn(B, S, HKV, D, device=cuda).bfloat16().requires_grad_(True)
+        o = ops.attention(q, k, v, causal=causal)
+        do = torch.randn_like(o)
+        o.backward(do)
+        torch.cuda.synchronize()
+    finally:
+        knob(key, old)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    orf = _ref(qr, kr, vr, causal, D ** -0.5)
+    orf.backward(do.float())
+    assert _rel(o, orf) < 1e-2
+    for g, gr, name in ((q.grad, qr.grad, "dq"), (k.grad, kr.grad, "dk"), (v.grad, vr.grad, "dv")):
+        assert _rel(g, gr) < 2e-2, name
