@@ -16,6 +16,8 @@
 //    chip-wide and non-deterministic).
 //  * The XCD swizzle is deliberately absent: there is no inter-block reuse on a
 //    row-wise op (cdna_hip_programming.md T1 "Transfer: 0% on LayerNorm").
+#include <type_traits>
+
 #include "common.h"
 
 namespace madnn {
@@ -77,7 +79,10 @@ struct Raw8 {
 // are loaded once before the loop (loading them after the row reductions exposed an L2 round trip
 // per row), and the next row's x (and residual) loads are issued before the current row's two
 // reductions, so every wave keeps a row of loads in flight while it reduces.
-template <int XDT, int WDT, int TPR, int NC>
+// DEPTH = 2: two rows of loads in flight per wave (slots alternate with a compile-time index, so no
+// register copy waits on an in-flight load): one 2-KB row per wave at 32 waves per CU is ~64 KB in
+// flight per CU, under the ~90 KB HBM latency x bandwidth needs (A/B: madnn_norm_tune key 3).
+template <int XDT, int WDT, int TPR, int NC, int DEPTH = 1>
 __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, const void* __restrict__ w, const void* __restrict__ b,
     void* __restrict__ y, void* __restrict__ sum_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -98,38 +103,45 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     }
   }
   const int64_t rstep = (int64_t)gridDim.x * RPB;
-  Raw8<XDT> nx[NC], nr[NC];
+  Raw8<XDT> nx[DEPTH][NC], nr[DEPTH][NC];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    nx[c].zero();
-    nr[c].zero();
+  for (int d = 0; d < DEPTH; ++d) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      nx[d][c].zero();
+      nr[d][c].zero();
+    }
   }
-  auto fetch = [&](int64_t row) {
+  auto fetch = [&](auto slotc, int64_t row) {
+    constexpr int SL = decltype(slotc)::value;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (row < rows && col < H) {
-        nx[c].load(x, row * H + col);
-        if (res) nr[c].load(res, row * H + col);
+        nx[SL][c].load(x, row * H + col);
+        if (res) nr[SL][c].load(res, row * H + col);
       }
     }
   };
-  fetch((int64_t)blockIdx.x * RPB + sub);
-  for (int64_t row0 = (int64_t)blockIdx.x * RPB; row0 < rows; row0 += rstep) {
+  int64_t row0 = (int64_t)blockIdx.x * RPB;
+  fetch(std::integral_constant<int, 0>{}, row0 + sub);
+  if constexpr (DEPTH == 2) fetch(std::integral_constant<int, 1>{}, row0 + rstep + sub);
+  auto step = [&](auto slotc) {
+    constexpr int SL = decltype(slotc)::value;
     const int64_t row = row0 + sub;
     const bool live = row < rows;  // uniform per row group; all lanes still join the LDS reduction
     float v[NC][8];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      nx[c].unpack(v[c]);
+      nx[SL][c].unpack(v[c]);
       if (res) {
         float r[8];
-        nr[c].unpack(r);
+        nr[SL][c].unpack(r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] += r[j];
       }
     }
-    fetch(row + rstep);  // the next row's loads fly under this row's reductions
+    fetch(slotc, row + DEPTH * rstep);  // this slot's next row flies under this row's reductions
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -173,6 +185,16 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
       if (mean_out) mean_out[row] = mean;
       rstd_out[row] = rstd;
     }
+    row0 += rstep;
+  };
+  if constexpr (DEPTH == 2) {
+    while (row0 < rows) {
+      step(std::integral_constant<int, 0>{});
+      if (row0 >= rows) break;
+      step(std::integral_constant<int, 1>{});
+    }
+  } else {
+    while (row0 < rows) step(std::integral_constant<int, 0>{});
   }
 }
 
@@ -453,15 +475,16 @@ static NormCfg pick_cfg(int H) {
 // backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
 // (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
 // +0.5 % over 16 (4: -0.1 %)
-static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1;
+static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1, g_norm_fwd_depth = 1;
 
 extern "C" {
 
 int madnn_norm_tune(int key, int value) {
-  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early : nullptr;
+  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early
+         : key == 3 ? &g_norm_fwd_depth : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value > 0 || key == 2) *f = value;
+  if (value > 0 || key == 2) *f = key == 3 ? (value >= 2 ? 2 : 1) : value;
   return old;
 }
 
@@ -478,8 +501,13 @@ hipError_t madnn_norm_fwd(const void* x, const void* res, const void* w, const v
       constexpr int RPB = kNormThreads / TPR;
       int64_t blocks = (rows + RPB - 1) / RPB;
       const int grid = blocks > g_norm_fwd_wg * kNumCU ? g_norm_fwd_wg * kNumCU : (int)blocks;
-      hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w, b,
-                         y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
+      if (g_norm_fwd_depth == 2 && TPR == kWave) {
+        hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC, TPR == kWave ? 2 : 1>), dim3(grid), dim3(kNormThreads), 0,
+                           stream, x, res, w, b, y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
+      } else {
+        hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w,
+                           b, y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
+      }
     });
   });
   return hipGetLastError();

@@ -772,3 +772,34 @@ def test_linear_bias_grad_with_two_consumers(cuda, second):
     fwd(xf, wf, bf, lwf, lbf, True).backward()
     assert _rel(b.grad, bf.grad) < 2e-2
     assert _rel(w.grad, wf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("rows,H,res", [(257, 1024, False), (20000, 1024, True), (3001, 64, False),
+                                        (100000, 768, True)])
+def test_norm_fwd_two_rows_in_flight_matches_default(cuda, rows, H, res):
+    # madnn_norm_tune key 3 = 2: the forward keeps two rows of loads in flight per wave (alternating
+    # compile-time slots); the same arithmetic, so outputs and statistics match the default bitwise
+    import ctypes
+
+    knob = ctypes.CDLL(str(ops.kernels_path())).madnn_norm_tune
+    torch.manual_seed(9)
+    x = torch.randn(rows, H, device=cuda, dtype=torch.bfloat16)
+    r = torch.randn(rows, H, device=cuda, dtype=torch.bfloat16) if res else None
+    w = torch.rand(H, device=cuda) + 0.5
+    b = torch.randn(H, device=cuda) * 0.1
+    outs = {}
+    for depth in (1, 2):
+        old = knob(3, depth)
+        try:
+            outs[depth] = ops.layer_norm(x, w, b, residual=r) if res else ops.layer_norm(x, w, b)
+            torch.cuda.synchronize()
+        finally:
+            knob(3, old)
+    a, c = outs[1], outs[2]
+    if res:
+        assert torch.equal(a[0], c[0]) and torch.equal(a[1], c[1])
+        a = a[0]
+    else:
+        assert torch.equal(a, c)
+    ref = torch.nn.functional.layer_norm((x.float() + r.float()) if res else x.float(), (H,), w, b, 1e-5)
+    torch.testing.assert_close(a.float(), ref, atol=3e-2, rtol=3e-2)
