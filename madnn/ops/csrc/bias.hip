@@ -98,7 +98,8 @@ __host__ __device__ inline BiasGeom bias_geom(int N) {
   return {tpr, kBiasLanes / tpr, (lanes + tpr - 1) / tpr};
 }
 
-template <int XDT, bool GELU, bool FAST = true, bool RCP = true>
+// U: rows per lane in flight in the main loop (A/B knob madnn_bias_tune2 key 0 for the GELU variant)
+template <int XDT, bool GELU, bool FAST = true, bool RCP = true, int U = 4>
 __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
                                                                const void* __restrict__ pre, void* __restrict__ dp,
                                                                int64_t M, int N, float* __restrict__ partial) {
@@ -114,23 +115,23 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
   if (active) {
     const int64_t step = (int64_t)gridDim.y * g.rpi;
     int64_t r = (int64_t)blockIdx.y * g.rpi + rs;
-    for (; r + 3 * step < M; r += 4 * step) {
-      float v[4][8];
+    for (; r + (U - 1) * step < M; r += U * step) {
+      float v[U][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load8<XDT>(dy, (r + u * step) * N + col, v[u]);
+      for (int u = 0; u < U; ++u) load8<XDT>(dy, (r + u * step) * N + col, v[u]);
       if constexpr (GELU) {
-        float p[4][8];
+        float p[U][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) load8<XDT>(pre, (r + u * step) * N + col, p[u]);
+        for (int u = 0; u < U; ++u) load8<XDT>(pre, (r + u * step) * N + col, p[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad<FAST, RCP>(p[u][j]);
           store8<XDT>(dp, (r + u * step) * N + col, v[u]);
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) s[j] += v[u][j];
     }
@@ -199,12 +200,20 @@ using namespace madnn;
 static int g_bias_wg_per_cu[2] = {2, 4};
 static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
 static int g_gelu_rcp = 1;        // A/B knob: v_rcp (1) or the IEEE division (0) in the exp2-based tanh
+static int g_bias_gelu_unroll = 4;  // A/B knob (madnn_bias_tune2 key 0): GELU-variant rows in flight, 4 or 8
 
 extern "C" {
 
 int madnn_bias_tune(int gelu, int wg_per_cu) {
   const int old = g_bias_wg_per_cu[gelu ? 1 : 0];
   if (wg_per_cu > 0) g_bias_wg_per_cu[gelu ? 1 : 0] = wg_per_cu;
+  return old;
+}
+
+int madnn_bias_tune2(int key, int value) {
+  if (key != 0) return -1;
+  const int old = g_bias_gelu_unroll;
+  if (value > 0) g_bias_gelu_unroll = value >= 8 ? 8 : 4;
   return old;
 }
 
@@ -279,7 +288,10 @@ hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M,
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre && g_bias_fast_tanh && g_gelu_rcp) {
+    if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 8) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true, 8>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
+                         M, N, partial);
+    } else if (pre && g_bias_fast_tanh && g_gelu_rcp) {
       hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
                          N, partial);
     } else if (pre && g_bias_fast_tanh) {

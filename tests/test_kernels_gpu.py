@@ -803,3 +803,26 @@ def test_norm_fwd_two_rows_in_flight_matches_default(cuda, rows, H, res):
         assert torch.equal(a, c)
     ref = torch.nn.functional.layer_norm((x.float() + r.float()) if res else x.float(), (H,), w, b, 1e-5)
     torch.testing.assert_close(a.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("shape", [(16, 1024, 4096), (3, 77, 4096), (1000, 264)])
+def test_bias_grad_gelu_eight_rows_in_flight(cuda, shape):
+    """madnn_bias_tune2 key 0 = 8: the GELU bias-gradient kernel's main loop keeps 8 rows per lane in flight;
+    the GELU backward output is elementwise-identical to the 4-row default, the column sum within rounding."""
+    import ctypes
+
+    knob = ctypes.CDLL(str(ops.kernels_path())).madnn_bias_tune2
+    torch.manual_seed(7)
+    dy = torch.randn(*shape, device=cuda).bfloat16()
+    pre = torch.randn(*shape, device=cuda).bfloat16() * 2
+    res = {}
+    for u in (4, 8):
+        old = knob(0, u)
+        try:
+            res[u] = ops.bias_grad(dy, pre, torch.float32)
+            torch.cuda.synchronize()
+        finally:
+            knob(0, old)
+    assert torch.equal(res[4][1], res[8][1])
+    ref = res[4][0]
+    torch.testing.assert_close(res[8][0], ref, atol=1e-4 * ref.abs().max().item() + 1e-4, rtol=1e-4)
