@@ -200,7 +200,7 @@ using namespace madnn;
 static int g_bias_wg_per_cu[2] = {2, 4};
 static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
 static int g_gelu_rcp = 1;        // A/B knob: v_rcp (1) or the IEEE division (0) in the exp2-based tanh
-static int g_bias_gelu_unroll = 4;  // A/B knob (madnn_bias_tune2 key 0): GELU-variant rows in flight, 4 or 8
+static int g_bias_gelu_unroll = 4;  // A/B knob (madnn_bias_tune2 key 0): GELU-variant rows in flight, 2, 4 or 8
 
 extern "C" {
 
@@ -213,7 +213,7 @@ int madnn_bias_tune(int gelu, int wg_per_cu) {
 int madnn_bias_tune2(int key, int value) {
   if (key != 0) return -1;
   const int old = g_bias_gelu_unroll;
-  if (value > 0) g_bias_gelu_unroll = value >= 8 ? 8 : 4;
+  if (value > 0) g_bias_gelu_unroll = value >= 8 ? 8 : value <= 2 ? 2 : 4;
   return old;
 }
 
@@ -288,7 +288,10 @@ hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M,
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 8) {
+    if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 2) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true, 2>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
+                         M, N, partial);
+    } else if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 8) {
       hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true, 8>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
                          M, N, partial);
     } else if (pre && g_bias_fast_tanh && g_gelu_rcp) {
