@@ -827,3 +827,33 @@ def test_bias_grad_gelu_rows_in_flight_variants(cuda, shape):
     for u in (2, 8):
         assert torch.equal(res[4][1], res[u][1])
         torch.testing.assert_close(res[u][0], ref, atol=1e-4 * ref.abs().max().item() + 1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("V,ld", [(50257, 50304), (130, 136), (1000, 1000)])
+def test_one_pass_cross_entropy_fast_exp_variant(cuda, V, ld, monkeypatch):
+    """madnn_xent_tune key 0 = 1 (v_exp_f32 directly, vocabulary-end test per chunk) vs fp32 F.cross_entropy."""
+    import ctypes
+
+    knob = ctypes.CDLL(str(ops.kernels_path())).madnn_xent_tune
+    monkeypatch.setattr(ops, "XENT_FUSED", True)
+    torch.manual_seed(8)
+    B, S = 2, 9
+    base = (torch.randn(B, S, ld, device=cuda) * 3).bfloat16()
+    tg = torch.randint(0, V, (B, S), device=cuda)
+    tg[0, 2] = -100
+    old = knob(0, 1)
+    try:
+        lg = base.clone().requires_grad_(True)
+        loss = ops.cross_entropy(lg, tg, shift=True, vocab=V)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        knob(0, old)
+    lr = base.float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr[:, :-1, :V].reshape(-1, V), tg[:, 1:].reshape(-1), ignore_index=-100)
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref, atol=2e-3, rtol=2e-3)
+    g = lg.grad.float()
+    torch.testing.assert_close(g, lr.grad, atol=2e-2 * lr.grad.abs().max().item() + 1e-7, rtol=2e-2)
+    if ld > V:
+        assert lg.grad[..., V:].abs().max() == 0
