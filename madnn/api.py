@@ -241,8 +241,14 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
     fused = optimizer is None or _is_fused(optimizer)
     space = build_space(model, optimizer, cfg, device, dtype_of, cl)
     world = rt.get_world_size(group)
-    sync_every = cfg.sync_every or 1
-    engine = DataParallel(model, space, group=group, src_rank=src_rank, sync=cfg.sync, sync_every=sync_every,
+    sync, sync_every, sync_samples = cfg.sync, cfg.sync_every, None
+    if sync == "params" and sync_every == -1:
+        sync = "manual"  # the reference's batchSize = -1 (datamodule.lua:45)
+    if sync == "params" and sync_every is None:
+        sync_samples = _heuristic_period(cfg)
+    engine = DataParallel(model, space, group=group, src_rank=src_rank, sync=sync,
+                          sync_every=sync_every if sync_every not in (None, -1) else 1,
+                          sync_samples=sync_samples, sync_budget=cfg.sync_budget,
                           overlap=cfg.overlap, cast_dtype=dtype, channels_last=cl, unpack_grads=not fused,
                           broadcast_buffers=cfg.broadcast_buffers, find_unused=cfg.find_unused,
                           sync_comm=cfg.sync_comm, rebuild_buckets=cfg.rebuild_buckets and fused)
@@ -261,6 +267,21 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
     get_logger().info("madnn dp: world=%d buckets=%d params=%.1fM dtype=%s channels_last=%s", world,
                       len(space.buckets), space.numel() / 1e6, dtype, cl)
     return engine, optimizer
+
+
+def _heuristic_period(cfg: Config) -> int:
+    """The reference's default period (R6, datamodule.lua:68-78) for ``sync="params"`` without
+    ``sync_every``: 1/10/50/100 SAMPLES by the size of this rank's shard -- ``cfg.local_size``,
+    else the shard ``madnn.data`` last cut on this rank.  With neither, the shard is taken to be
+    large (the heuristic's top tier, 100 samples)."""
+    from .data import last_local_size
+
+    local = cfg.local_size if cfg.local_size is not None else last_local_size()
+    if local is None:
+        get_logger().warning("madnn dp: sync='params' without sync_every and no known shard size "
+                             "(pass local_size=): using the heuristic's top tier, 100 samples")
+        return default_sync_period(10 ** 9)
+    return default_sync_period(int(local))
 
 
 def _after_plain_step(engine: DataParallel):

@@ -283,6 +283,7 @@ def _plan_meta(engine) -> dict:
                 "schedule": engine.schedule}
     if isinstance(engine, DataParallel):
         return {"strategy": "dp", "dp": engine.world, "pp": 1, "sync": engine.sync, "sync_every": engine.sync_every,
+                "sync_samples": engine.sync_samples, "sync_calibration": engine.sync_calibration,
                 "steps": engine._steps}
     return {"strategy": "none"}
 
@@ -414,13 +415,16 @@ def _load_resume_state(path: str, engine, meta: dict) -> Optional[dict]:
         rng = torch.load(legacy, weights_only=True)
         return {"rng_cpu": rng["cpu"], **({"rng_cuda": rng["cuda"]} if "cuda" in rng else {})}
     st = torch.load(f, weights_only=True)
-    if mapped is not None and mapped != c:
+    if mapped is not None and (mapped["dp"], mapped["pp"]) != (c["dp"], c["pp"]):
         # a rank with no saved state of its own (resumed on a larger mesh) borrows another
-        # coordinate's state: fold ITS coordinates into the RNG streams, or it would draw the
-        # same dropout masks as the rank it borrowed from
-        st["rng_cpu"] = _fold_rng(st["rng_cpu"], c)
+        # coordinate's state: fold its dp / pp coordinates into the RNG streams, or it would draw
+        # the same dropout masks as the replica it borrowed from.  The tp coordinate is NOT folded:
+        # a tensor-parallel group's ranks must keep one shared stream (dropout on replicated
+        # activations), and they borrow from one saved TP group, whose states are equal
+        fold = {"dp": c["dp"], "pp": c["pp"]}
+        st["rng_cpu"] = _fold_rng(st["rng_cpu"], fold)
         if "rng_cuda" in st:
-            st["rng_cuda"] = _fold_rng(st["rng_cuda"], c)
+            st["rng_cuda"] = _fold_rng(st["rng_cuda"], fold)
     return st
 
 

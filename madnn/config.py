@@ -18,7 +18,7 @@ from __future__ import annotations
 import dataclasses
 import os
 from dataclasses import dataclass, field
-from typing import Optional
+from typing import Optional, Union
 
 
 def _env(name: str, default, cast):
@@ -36,7 +36,12 @@ class Config:
     strategy: str = "auto"
     # data parallel
     sync: str = "grads"                  # grads | params | manual
-    sync_every: Optional[int] = None     # period K for sync="params" (None => reference heuristic)
+    # period K for sync="params": an int = optimizer steps; None = the reference heuristic on the
+    # local shard size (R6: 1/10/50/100 SAMPLES); "auto" = measured (smallest K whose parameter
+    # average costs <= sync_budget of K steps: the reference's comm_speed -> optimize_sync intent)
+    sync_every: Optional[Union[int, str]] = None
+    local_size: Optional[int] = None     # samples in this rank's shard (None: the last madnn.data shard)
+    sync_budget: float = 0.05            # sync_every="auto": allowed sync time / compute time
     bucket_mb: float = 0.0               # gradient bucket cap (MB of reduce dtype); 0 = auto (see auto_bucket_mb)
     overlap: bool = True                 # overlap bucket all-reduce with backward on a comm stream
     reduce_dtype: str = "auto"           # gradient all-reduce dtype: auto = each bucket's own (bf16 / fp32 norms)
@@ -81,7 +86,9 @@ class Config:
                 continue
             cur = getattr(cfg, f.name)
             if cur is None:
-                cast = int if f.name in ("sync_every", "pp_stages", "microbatches", "virtual_stages") else str
+                cast = int if f.name in ("pp_stages", "microbatches", "virtual_stages", "local_size") else str
+                if f.name == "sync_every":
+                    cast = _int_or_auto
                 if f.name == "channels_last":
                     cast = bool
             else:
@@ -110,8 +117,19 @@ class Config:
             raise ValueError(f"unknown checkpointing policy {self.checkpointing!r}")
         if self.nonfinite not in ("ignore", "skip", "raise"):
             raise ValueError(f"unknown nonfinite policy {self.nonfinite!r}")
+        if self.sync_every is not None and self.sync_every != "auto":
+            if isinstance(self.sync_every, str):
+                self.sync_every = _int_or_auto(self.sync_every)
+            if int(self.sync_every) < 1 and int(self.sync_every) != -1:
+                raise ValueError(f"sync_every must be >= 1, -1 (manual), None or 'auto', not {self.sync_every!r}")
+        if not 0.0 < self.sync_budget:
+            raise ValueError("sync_budget must be > 0")
         if self.bucket_mb < 0:
             raise ValueError("bucket_mb must be >= 0 (0 = auto)")
+
+
+def _int_or_auto(v):
+    return "auto" if str(v).lower() == "auto" else int(v)
 
 
 def auto_bucket_mb(grad_bytes: float, lo: float = 4.0, hi: float = 64.0, target: int = 8) -> float:

@@ -13,12 +13,24 @@ documented intent) or ``pad`` (wrap-around so every sample is seen).
 from __future__ import annotations
 
 import math
+from collections.abc import Mapping
 from typing import Iterator, Optional, Sequence, Tuple
 
 import torch
 
 from .. import runtime as rt
 from ..utils.logging import get_logger
+
+
+_last_local = {"size": None}
+
+
+def last_local_size() -> Optional[int]:
+    """Samples in the shard this rank was last given by :func:`shard` or a
+    :class:`DistributedSampler` (None if neither ran).  The reference sizes its sync period from
+    the shard ``parallelize`` just cut (datamodule.lua:37-47); ``distribute(sync="params")`` reads
+    it here when ``Config.local_size`` is not given."""
+    return _last_local["size"]
 
 
 def shard_bounds(n: int, rank: int, world: int, remainder: str = "drop") -> Tuple[int, int]:
@@ -47,17 +59,20 @@ def shard(data, rank: Optional[int] = None, world: Optional[int] = None, remaind
         out = data[idx] if isinstance(data, torch.Tensor) else [data[i] for i in idx.tolist()]
         if verbose:
             get_logger().info("rank %d: strided shard stripe=%d", rank, stripe)
+        _last_local["size"] = len(out)
         return out
     start, end = shard_bounds(n, rank, world, remainder)
     if remainder == "pad":
         per = math.ceil(n / world)
         idx = [(rank * per + i) % n for i in range(per)]
+        _last_local["size"] = per
         if isinstance(data, torch.Tensor):
             return data[torch.tensor(idx)]
         return [data[i] for i in idx]
     if verbose:
         get_logger().info("rank %d: shard [%d, %d) stripe=%d remainder=%d", rank, start, end, n // world,
                           n - (n // world) * world)
+    _last_local["size"] = end - start
     return data[start:end]
 
 
@@ -127,6 +142,7 @@ class DistributedSampler(torch.utils.data.Sampler):
         self.cursor = 0          # indices of this epoch already yielded (may run ahead of training)
         self.consumed = 0        # samples of this epoch the training loop has taken (track / advance)
         self._tracked = False
+        _last_local["size"] = len(self)
 
     def set_epoch(self, e: int):
         if e != self.epoch:
@@ -142,15 +158,14 @@ class DistributedSampler(torch.utils.data.Sampler):
     def track(self, batches, batch_size: Optional[int] = None):
         """Yield from ``batches`` (a DataLoader / DevicePrefetcher over this sampler), counting
         each batch as consumed when it reaches the caller: a checkpoint taken in the loop body
-        after the step resumes at the next unseen batch, however far the loader prefetched."""
+        after the step resumes at the next unseen batch, however far the loader prefetched.
+
+        A batch's size is read from its first tensor: element 0 of a list / tuple, the first value
+        of a dict (HF-style collators), or the batch itself; any other batch type needs
+        ``batch_size``."""
         self._tracked = True
         for b in batches:
-            if batch_size is not None:
-                n = batch_size
-            else:
-                first = b[0] if isinstance(b, (list, tuple)) else b
-                n = len(first)
-            self.consumed += n
+            self.consumed += batch_size if batch_size is not None else _batch_len(b)
             yield b
 
     def position(self) -> int:
@@ -192,6 +207,24 @@ class DistributedSampler(torch.utils.data.Sampler):
 
     def __len__(self):
         return len(self._indices())
+
+
+def _batch_len(b) -> int:
+    if isinstance(b, Mapping):
+        if not b:
+            raise ValueError("DistributedSampler.track: empty dict batch; pass batch_size=")
+        b = next(iter(b.values()))
+    elif isinstance(b, (list, tuple)):
+        if not b:
+            raise ValueError("DistributedSampler.track: empty batch; pass batch_size=")
+        b = b[0]
+    if isinstance(b, torch.Tensor):
+        if b.dim() == 0:
+            raise ValueError("DistributedSampler.track: 0-d batch tensor; pass batch_size=")
+        return int(b.shape[0])
+    if isinstance(b, (list, tuple)):
+        return len(b)
+    raise TypeError(f"DistributedSampler.track cannot size a {type(b).__name__} batch; pass batch_size=")
 
 
 class DevicePrefetcher:

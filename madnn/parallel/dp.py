@@ -22,7 +22,9 @@ MI355X-native redesign:
 from __future__ import annotations
 
 import contextlib
-from typing import Optional
+import math
+import time
+from typing import Optional, Union
 
 import torch
 from torch import nn
@@ -42,6 +44,13 @@ def default_sync_period(local_size: int) -> int:
     if local_size < 5000:
         return 50
     return 100
+
+
+def auto_sync_period(step_s: float, sync_s: float, budget: float = 0.05, k_max: int = 10000) -> int:
+    """Smallest K with ``sync_s <= budget * K * step_s`` (1 <= K <= k_max)."""
+    if step_s <= 0:
+        return k_max if sync_s > 0 else 1
+    return int(min(max(math.ceil(sync_s / (budget * step_s) - 1e-9), 1), k_max))
 
 
 def robustness_tick(step: int, group=None) -> None:
@@ -80,14 +89,29 @@ def _cast_inputs(obj, dtype, channels_last):
     return obj
 
 
+def _leading_dim(args, kwargs) -> int:
+    """Samples in one forward's input: the leading dim of its first tensor (0 if none)."""
+    for a in list(args) + list(kwargs.values()):
+        if isinstance(a, torch.Tensor):
+            return int(a.shape[0]) if a.dim() > 0 else 1
+        if isinstance(a, (list, tuple)) and a and isinstance(a[0], torch.Tensor):
+            return int(a[0].shape[0]) if a[0].dim() > 0 else 1
+        if isinstance(a, dict):
+            n = _leading_dim((), a)
+            if n:
+                return n
+    return 0
+
+
 class DataParallel(nn.Module):
     """Wraps a module whose parameters live in a :class:`FlatParamSpace`."""
 
     def __init__(self, module: nn.Module, space: FlatParamSpace, *, group=None, src_rank: int = 0,
-                 sync: str = "grads", sync_every: int = 1, overlap: bool = True,
+                 sync: str = "grads", sync_every: Union[int, str] = 1, overlap: bool = True,
                  cast_dtype: Optional[torch.dtype] = None, channels_last: bool = False,
                  unpack_grads: bool = False, broadcast_buffers: bool = True, find_unused: bool = True,
-                 sync_comm: bool = False, grad_sinks: bool = True, rebuild_buckets: bool = True):
+                 sync_comm: bool = False, grad_sinks: bool = True, rebuild_buckets: bool = True,
+                 sync_samples: Optional[int] = None, sync_budget: float = 0.05):
         super().__init__()
         self.module = module
         self.space = space
@@ -95,7 +119,17 @@ class DataParallel(nn.Module):
         self.src_rank = src_rank
         self.world = rt.get_world_size(group)
         self.sync = sync
-        self.sync_every = max(int(sync_every), 1)
+        # sync="params" period: every ``sync_every`` optimizer steps, or "auto" (measured, see
+        # _auto_period), or -- ``sync_samples`` -- whenever the count of trained SAMPLES crosses a
+        # multiple of it (the reference's unit, datamodule.lua:102,151)
+        self.sync_every = "auto" if sync_every == "auto" else max(int(sync_every), 1)
+        self.sync_samples = int(sync_samples) if sync_samples else None
+        self.sync_budget = float(sync_budget)
+        self.sync_calibration = None          # sync_every="auto": the measurement and the chosen K
+        self._samples = 0
+        self._fwd_samples = 0
+        self._calib = None
+        self._period_origin = 0
         self.cast_dtype = cast_dtype
         self.channels_last = channels_last
         self.unpack_grads = unpack_grads
@@ -337,9 +371,71 @@ class DataParallel(nn.Module):
             ops.sync_choices(self.group, src=self.src_rank)
         if self._observe is not None:
             self._maybe_relayout()
-        if self.sync == "params" and self._steps % self.sync_every == 0:
-            self.average_parameters()
+        if self.sync == "params":
+            self._params_tick()
         robustness_tick(self._steps, self.group)
+
+    # -------------------------------------------------------- sync period
+    def _params_tick(self):
+        n, self._fwd_samples = self._fwd_samples, 0
+        if self.sync_samples is not None:
+            before = self._samples
+            self._samples += max(n, 1)
+            if self._samples // self.sync_samples > before // self.sync_samples:
+                self.average_parameters()
+        elif self.sync_every == "auto":
+            self._auto_period()
+        elif (self._steps - self._period_origin) % self.sync_every == 0:
+            self.average_parameters()
+
+    AUTO_WARMUP = 1   # steps averaged every step before timing starts (allocator, kernel choices)
+    AUTO_MEASURE = 3  # steps timed: compute since the previous average ended, then the average
+
+    def _clock(self) -> float:
+        if self.is_cuda:
+            torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def _auto_period(self):
+        """sync_every="auto": the reference's intended period from measured communication speed
+        (``comm_speed`` -> ``optimize_sync``, datamodule.lua:40-47,65-78,280-303), done on the job.
+        The first AUTO_WARMUP + AUTO_MEASURE steps average every step (K = 1 is always correct);
+        the measured ones time the compute since the previous average and the average itself.
+        Every rank then takes the MAX of both over the group and picks the smallest K with
+        ``sync <= sync_budget * K * step``, so all replicas agree on K.  The device synchronises
+        only during these few steps."""
+        c = self._calib
+        if c is None:
+            c = self._calib = {"step": [], "sync": [], "t_end": None}
+        k = self._steps
+        now = self._clock()
+        if c["t_end"] is not None and k > self.AUTO_WARMUP:
+            c["step"].append(now - c["t_end"])
+            t0 = now
+            self.average_parameters()
+            now = self._clock()
+            c["sync"].append(now - t0)
+        else:
+            self.average_parameters()
+            now = self._clock()
+        c["t_end"] = now
+        if len(c["sync"]) < self.AUTO_MEASURE:
+            return
+        step_s = sum(c["step"]) / len(c["step"])
+        sync_s = sum(c["sync"]) / len(c["sync"])
+        t = torch.tensor([step_s, sync_s], dtype=torch.float64,
+                         device=self.space.buckets[0].master.device if self.space.buckets else "cpu")
+        if not comm._local(self.group):
+            comm.all_reduce(t, "max", group=self.group)
+        step_s, sync_s = float(t[0]), float(t[1])
+        kk = auto_sync_period(step_s, sync_s, self.sync_budget)
+        self.sync_every = kk
+        self._period_origin = k
+        self._calib = None
+        self.sync_calibration = {"step_ms": step_s * 1e3, "sync_ms": sync_s * 1e3, "budget": self.sync_budget,
+                                 "K": kk, "decided_at_step": k}
+        get_logger().info("madnn dp: sync period auto -> K=%d steps (step %.2f ms, parameter average %.2f ms, "
+                          "budget %.0f%%)", kk, step_s * 1e3, sync_s * 1e3, 100 * self.sync_budget)
 
     def _maybe_relayout(self):
         """After the first step: if the buckets did not fill in the order backward produced
@@ -415,6 +511,8 @@ class DataParallel(nn.Module):
             # gradients are about to be accumulated again before the optimizer ran: the next
             # backward's in-place adds into p.grad must follow the packs still reading it
             torch.cuda.current_stream().wait_stream(self.comm_stream)
+        if self.sync == "params" and torch.is_grad_enabled():
+            self._fwd_samples += _leading_dim(args, kwargs)
         if self.cast_dtype is not None or self.channels_last:
             args = _cast_inputs(args, self.cast_dtype, self.channels_last)
             kwargs = _cast_inputs(kwargs, self.cast_dtype, self.channels_last)
@@ -461,7 +559,8 @@ class DataParallel(nn.Module):
         self._hooks.clear()
 
     def extra_repr(self) -> str:
-        return (f"world={self.world}, sync={self.sync}, period={self.sync_every}, "
+        period = f"{self.sync_samples} samples" if self.sync_samples else self.sync_every
+        return (f"world={self.world}, sync={self.sync}, period={period}, "
                 f"buckets={len(self.space.buckets)}, overlap={self.comm_stream is not None}")
 
 

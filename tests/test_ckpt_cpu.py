@@ -273,3 +273,32 @@ def test_sampler_resume_counts_consumed_not_prefetched():
         next(it)                  # 8 handed out (a prefetching loop) ...
     a.advance(4)                  # ... 4 trained
     assert a.state_dict()["cursor"] == 4
+
+
+def test_resume_on_larger_tp_mesh_keeps_tp_groups_on_one_rng_stream(tmp_path, monkeypatch):
+    """a rank resumed on a larger mesh borrows a saved coordinate's RNG state; the
+    dp / pp coordinates are folded in (replicas draw different masks), the tp coordinate is not
+    (a tensor-parallel group keeps one shared stream)."""
+    import types
+
+    from madnn import ckpt
+
+    g = torch.Generator()
+    g.manual_seed(7)
+    shared = g.get_state()          # saved at dp=1 x tp=2: both tp ranks on one stream
+    for tp in range(2):
+        torch.save({"rng_cpu": shared.clone()}, str(tmp_path / f"state-dp0-pp0-tp{tp}.pt"))
+    meta = {"mesh": {"dp": 1, "pp": 1, "tp": 2}}
+
+    def state_at(dp, tp):
+        eng = types.SimpleNamespace(groups=types.SimpleNamespace(dp_idx=dp, pp_idx=0, tp_idx=tp))
+        return ckpt._load_resume_state(str(tmp_path), eng, meta)["rng_cpu"]
+
+    # resumed at dp=2 x tp=4: every rank of one TP group shares a stream ...
+    for dp in range(2):
+        states = [state_at(dp, tp) for tp in range(4)]
+        for s in states[1:]:
+            assert torch.equal(s, states[0])
+    # ... the saved replica keeps its own, the new replica gets a different one
+    assert torch.equal(state_at(0, 3), shared)
+    assert not torch.equal(state_at(1, 0), shared)

@@ -110,6 +110,58 @@ def test_params_mode_equals_grads_mode_k1():
     run_dist(_w_params_mode, 2)
 
 
+def _w_params_period(rank, world, mode):
+    """``distribute(sync="params")`` period: None -> the reference heuristic in SAMPLES on the
+    local shard (R6, datamodule.lua:68-78); "auto" -> K measured on the job, agreed by all ranks."""
+    import madnn
+    from madnn.data import shard
+    from madnn.optim import FusedSGD
+    from madnn.parallel.dp import auto_sync_period
+
+    x, y = _data(3, n=2400)
+    xs, ys = shard(x), shard(y)                       # 1200 local samples -> heuristic 10 samples
+    assert len(xs) == 1200
+    model = _ref_model()
+    opt = FusedSGD(model.parameters(), lr=0.05)
+    kw = {"sync_every": "auto", "sync_budget": 1e6 if mode == "auto_k1" else 1e-6} if mode != "none" else {}
+    dm, opt = madnn.distribute(model, opt, strategy="dp", sync="params", **kw)
+    synced = []
+    real = dm.average_parameters
+
+    def counting():
+        synced.append(dm._steps)
+        real()
+
+    dm.average_parameters = counting
+    for step in range(8):
+        F.cross_entropy(dm(xs[step * 4:step * 4 + 4]), ys[step * 4:step * 4 + 4]).backward()
+        opt.step()
+        opt.zero_grad()
+        if step + 1 in synced:
+            for p in model.parameters():
+                _check_same_across_ranks(p.detach())
+    if mode == "none":
+        assert dm.sync_samples == 10
+        assert synced == [3, 5, 8]                   # 4 samples per step: crossing 10, 20, 30
+        return
+    cal = dm.sync_calibration
+    assert cal is not None and cal["decided_at_step"] == 4
+    k = torch.tensor([float(cal["K"]), cal["step_ms"], cal["sync_ms"]], dtype=torch.float64)
+    _check_same_across_ranks(k)                      # every rank chose the same K from the same MAXes
+    assert cal["K"] == auto_sync_period(cal["step_ms"], cal["sync_ms"], cal["budget"])
+    assert synced[:4] == [1, 2, 3, 4]                # K = 1 while measuring
+    if mode == "auto_k1":
+        assert cal["K"] == 1 and synced == list(range(1, 9))
+    else:
+        assert cal["K"] == 10000 and synced == [1, 2, 3, 4]
+    assert dm.sync_every == cal["K"]
+
+
+@pytest.mark.parametrize("mode", ["none", "auto_k1", "auto_kmax"])
+def test_distribute_params_sync_period(mode):
+    run_dist(_w_params_period, 2, mode)
+
+
 def _w_no_sync(rank, world):
     import madnn
     from madnn.optim import FusedSGD

@@ -784,3 +784,28 @@ def test_chain_calibration_rescales_activation_memory_at_a_batch_that_fits(monke
     layers = sum(c.call_s(8) for c in costs)
     cal = planner._calibrate_chain(None, None, costs, 8, torch.bfloat16, Config(), hw)
     assert seen["batch"] == 8 and cal["ratio"] == pytest.approx(1.0 / layers)
+
+
+def test_auto_sync_period_is_the_smallest_k_within_budget():
+    from madnn.parallel.dp import auto_sync_period
+
+    assert auto_sync_period(10.0, 0.4, 0.05) == 1          # 0.4 <= 0.05 * 1 * 10
+    assert auto_sync_period(10.0, 0.6, 0.05) == 2
+    assert auto_sync_period(10.0, 5.0, 0.05) == 10
+    assert auto_sync_period(1.0, 1e9, 0.05) == 10000       # clamped
+    for step, sync in [(3.0, 0.7), (1.0, 2.5), (0.2, 0.011)]:
+        k = auto_sync_period(step, sync, 0.05)
+        assert sync <= 0.05 * k * step * (1 + 1e-9) and (k == 1 or sync > 0.05 * (k - 1) * step)
+
+
+def test_sampler_track_sizes_dict_and_rejects_unsized_batches():
+    import pytest as _pt
+
+    from madnn.data import DistributedSampler
+
+    s = DistributedSampler(10, rank=0, world=1, shuffle=False)
+    batches = [{"input_ids": torch.zeros(3, 5), "labels": torch.zeros(3)}, (torch.zeros(2, 4), torch.zeros(2))]
+    assert len(list(s.track(batches))) == 2 and s.consumed == 5
+    with _pt.raises(TypeError):
+        list(s.track([object()]))
+    assert len(list(s.track([object()], batch_size=4))) == 1 and s.consumed == 9
