@@ -258,6 +258,13 @@ def _timeline(kind: str, nstages: int, nmicro: int, nchunks: int, lag: float = 0
 _DEFAULT_LAG = 0.3
 
 
+def _planned_lag(plan) -> float:
+    """The issue-plan lag the planner priced; the default only when the plan carries none (a
+    planned 0.0 -- transfers priced as negligible -- stays 0: no second plan to time)."""
+    lag = getattr(plan, "p2p_lag", None)
+    return _DEFAULT_LAG if lag is None else float(lag)
+
+
 def plan_lag(lag: float) -> float:
     """A transfer time in forward-chunk units, rounded to 2 significant digits (the issue plans
     and their caches are keyed on it)."""
@@ -1355,7 +1362,7 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
     engine = PipelineEngine(stage_mod, stage=stage, nstages=S, groups=groups, microbatches=plan.microbatches,
                             schedule=schedule, loss_fn=loss_fn, dp_engine=dp_engine, cast_dtype=dtype,
                             tied=tied_local, param_names=names, buffer_refs=buffer_refs, transport=transport,
-                            lag=getattr(plan, "p2p_lag", None) or _DEFAULT_LAG,
+                            lag=_planned_lag(plan),
                             sig_group=sig_groups[groups.dp_idx] if sig_groups else None)
     engine.plan = plan
     if optimizer is not None:

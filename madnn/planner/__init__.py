@@ -373,6 +373,17 @@ def optimizer_s(params: float, opt: str, hw: Machine) -> float:
     return params * per / (hw.hbm_tbps * 1e12)
 
 
+def _agreed_min(x: float) -> float:
+    """MIN of ``x`` over the job's ranks (``x`` itself without a multi-rank process group)."""
+    import torch.distributed as dist
+
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return float(x)
+    v = torch.tensor([float(x)], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    return float(v)
+
+
 def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw: Machine):
     """Scale the per-layer costs so their sum matches ONE timing of the whole spine at the
     measurement batch (isolated layer timings miss what neighbouring layers do to each other).
@@ -388,9 +399,15 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
         return None
     nparams = sum(c.params for c in costs)
     act = sum(c.act_bytes for c in costs)
+    import torch.distributed as dist
+
+    from .. import comm
+
     held = torch.cuda.memory_allocated() if torch.cuda.is_available() else 0
-    # weights + grads, then the saved activations, within 3/4 of what the device has left
-    budget = 0.75 * hw.hbm_gb * 1e9 - held - nparams * 6
+    # weights + grads, then the saved activations, within 3/4 of what the device has left; the
+    # ranks hold different amounts, so they agree on the tightest budget (MIN) before any branch:
+    # every rank then takes the same early return or times the chain at the same batch
+    budget = _agreed_min(0.75 * hw.hbm_gb * 1e9 - held - nparams * 6)
     if nparams * 6 > 0.25 * hw.hbm_gb * 1e9 or budget <= 0:
         return None
     # halve until it fits: batch / 2^k keeps to the shapes the shipped tuning records hold more
@@ -400,10 +417,6 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
         cb //= 2
     if act * cb > budget:
         return None
-    import torch.distributed as dist
-
-    from .. import comm
-
     saved = {}
     try:
         t = measure_chain(spine, example_input, costs, batch=cb, dtype=dtype, saved=saved)

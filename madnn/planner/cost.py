@@ -307,26 +307,28 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
         return costs
     import torch.distributed as dist
 
-    dev = device or torch.device("cuda", torch.cuda.current_device())
-    b = int(batch or max(example_input.shape[0], 1))
-    b2 = max(b // 4, 1) if two_point and b >= 4 else None
-    keys, first = [], {}
-    for i, layer in enumerate(spine.layers):
-        if i == 0:
-            in_key = ("input", tuple(example_input.shape[1:]), str(example_input.dtype))
-        else:
-            in_key = (tuple(costs[i - 1].out_shape), str(costs[i - 1].out_dtype))
-        key = (layer_signature(layer), in_key)
-        keys.append(key)
-        first.setdefault(key, i)
-    distinct = sorted(first, key=lambda k: first[k])
     from .. import runtime as rt
 
     multi = dist.is_available() and dist.is_initialized() and rt.get_world_size(group) > 1
     me, world = (rt.get_rank(group), rt.get_world_size(group)) if multi else (0, 1)
     mine = {}
     err = None
+    keys, first, distinct = [], {}, []
     try:
+        # setup, timing and (below) the fit all end in MeasurementFailed on every rank, never in
+        # an exception some ranks raise while their peers wait in a collective
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        b = int(batch or max(example_input.shape[0], 1))
+        b2 = max(b // 4, 1) if two_point and b >= 4 else None
+        for i, layer in enumerate(spine.layers):
+            if i == 0:
+                in_key = ("input", tuple(example_input.shape[1:]), str(example_input.dtype))
+            else:
+                in_key = (tuple(costs[i - 1].out_shape), str(costs[i - 1].out_dtype))
+            key = (layer_signature(layer), in_key)
+            keys.append(key)
+            first.setdefault(key, i)
+        distinct = sorted(first, key=lambda k: first[k])
         for j, key in enumerate(distinct):
             if j % world != me:
                 continue
@@ -364,6 +366,19 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
         dist.all_gather_object(gathered, mine, group=group)
         for g in gathered:
             mine.update(g)
+    try:
+        fitted = _fit_measurements(distinct, mine)
+    except Exception as e:  # noqa: BLE001 - every rank fits the same gathered numbers: same outcome
+        raise MeasurementFailed(f"fitting the layer timings failed ({e})") from e
+    for key, c in zip(keys, costs):
+        c.fwd_s, c.bwd_s, c.fixed_s = fitted[key]
+        c.measured = True
+    torch.cuda.empty_cache()
+    return costs
+
+
+def _fit_measurements(distinct, mine) -> dict:
+    """Per distinct layer: (fwd s/sample, bwd s/sample, fixed s/call) from its one or two timings."""
     fitted = {}
     for j, key in enumerate(distinct):
         res = mine[j]
@@ -379,11 +394,7 @@ def measure_layers(spine: Spine, example_input: torch.Tensor, costs: List[LayerC
                 fixed = max((f1 + k1) - n1 * (slope_f + slope_b), 0.0)
                 fwd_ps, bwd_ps = slope_f, slope_b
         fitted[key] = (fwd_ps / 1e3, bwd_ps / 1e3, fixed / 1e3)
-    for key, c in zip(keys, costs):
-        c.fwd_s, c.bwd_s, c.fixed_s = fitted[key]
-        c.measured = True
-    torch.cuda.empty_cache()
-    return costs
+    return fitted
 
 
 def measure_chain(spine: Spine, example_input: torch.Tensor, costs: List[LayerCost], *, batch: int,

@@ -356,3 +356,16 @@ def _w_local_groups(rank, world):
 
 def test_singleton_axes_create_no_process_group():
     run_dist(_w_local_groups, 2)
+
+
+def _w_agreed_budget(rank, world):
+    from madnn.planner import _agreed_min
+
+    # ranks holding different amounts of memory: every rank sees the tightest budget, so the
+    # chain calibration takes the same early return / the same chain batch on all of them
+    assert _agreed_min(1e9 if rank == 0 else -5.0) == -5.0
+    assert _agreed_min(float(10 + rank)) == 10.0
+
+
+def test_chain_calibration_budget_is_agreed_across_ranks():
+    run_dist(_w_agreed_budget, 2)

@@ -809,3 +809,13 @@ def test_sampler_track_sizes_dict_and_rejects_unsized_batches():
     with _pt.raises(TypeError):
         list(s.track([object()]))
     assert len(list(s.track([object()], batch_size=4))) == 1 and s.consumed == 9
+
+
+def test_planned_zero_lag_is_kept():
+    import types
+
+    from madnn.parallel.pp import _DEFAULT_LAG, _planned_lag
+
+    assert _planned_lag(types.SimpleNamespace(p2p_lag=0.0)) == 0.0
+    assert _planned_lag(types.SimpleNamespace(p2p_lag=0.27)) == 0.27
+    assert _planned_lag(types.SimpleNamespace()) == _DEFAULT_LAG
