@@ -23,6 +23,7 @@ from madnn.optim import FusedAdam  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="bert-large")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--checkpointing", default="all")
@@ -30,14 +31,15 @@ def main():
     a = ap.parse_args()
     madnn.init()
     torch.manual_seed(0)
-    model = BertForPreTraining(bert_config("bert-large"))
+    cfg = bert_config(a.model)
+    model = BertForPreTraining(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
     eng, opt = madnn.distribute(model, opt, strategy="auto", checkpointing=a.checkpointing, global_batch=a.batch,
                                 example_input=torch.zeros(1, a.seq, dtype=torch.long))
     if madnn.get_rank() == 0:
         print(eng.plan.describe() if eng.plan is not None else "dp")
     dp = eng.plan.dp if eng.plan is not None else madnn.get_world_size()
-    ids = madnn.data.synthetic_batch("tokens", a.batch // dp, madnn.device(), seq_len=a.seq, vocab=30522)[0]
+    ids = madnn.data.synthetic_batch("tokens", a.batch // dp, madnn.device(), seq_len=a.seq, vocab=cfg.vocab_size)[0]
     for step in range(a.steps):
         loss = eng.train_step(ids, ids)
         opt.clip_grad_norm_(1.0)

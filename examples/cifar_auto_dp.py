@@ -36,6 +36,7 @@ def main():
     ap.add_argument("-iterations", type=int, default=1)
     ap.add_argument("-threads", type=int, default=1)
     ap.add_argument("-usegpu", action="store_true")
+    ap.add_argument("-size", type=int, default=0, help="train/test samples override (quick runs; 0 = reference sizes)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     madnn.init(device="cuda" if a.usegpu else "cpu")
@@ -43,6 +44,8 @@ def main():
     t_pre = time.time()
     model = CifarConvNet()
     trsize, tesize = (32000, 10000) if a.data else (4000, 2000)
+    if a.size:
+        trsize, tesize = a.size, max(a.size // 2, 10)
     g = torch.Generator().manual_seed(a.seed)
     centers = torch.randn(10, 3, 32, 32, generator=g)  # synthetic but learnable classes
     ytr = torch.randint(0, 10, (trsize,), generator=g)

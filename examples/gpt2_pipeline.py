@@ -34,7 +34,8 @@ def main():
     a = ap.parse_args()
     madnn.init()
     torch.manual_seed(0)
-    model = GPT2(gpt2_config(a.model))
+    cfg = gpt2_config(a.model)
+    model = GPT2(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
     eng, opt = madnn.distribute(model, opt, strategy="pp", pp_stages=a.stages or madnn.get_world_size(),
                                 microbatches=a.microbatches, schedule=a.schedule,
@@ -42,12 +43,13 @@ def main():
     if madnn.get_rank() == 0:
         print(eng.plan.describe())
         print(eng.plan.table())
-    ids = madnn.data.synthetic_batch("tokens", a.batch, madnn.device(), seq_len=a.seq, vocab=50257)[0]
+    ids = madnn.data.synthetic_batch("tokens", a.batch, madnn.device(), seq_len=a.seq, vocab=cfg.vocab_size)[0]
     for step in range(a.steps):
         t0 = time.time()
         loss = eng.train_step(ids, ids)
         opt.step()
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         if eng.is_last:
             print(f"step {step} loss {float(loss):.4f} {a.batch / (time.time() - t0):.1f} samples/s")
     madnn.shutdown()

@@ -30,8 +30,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     a = ap.parse_args()
     madnn.init()
+    cfg = llama_config(a.model)
     with torch.device("meta"):
-        model = Llama(llama_config(a.model))
+        model = Llama(cfg)
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.1)
     eng, opt = madnn.distribute(model, opt, strategy=a.strategy, global_batch=a.batch,
                                 example_input=torch.zeros(1, a.seq, dtype=torch.long))
@@ -40,7 +41,7 @@ def main():
         print(plan.describe())
         print(plan.table())
     per_replica = a.batch // plan.dp
-    ids = madnn.data.synthetic_batch("tokens", per_replica, madnn.device(), seq_len=a.seq, vocab=128256)[0]
+    ids = madnn.data.synthetic_batch("tokens", per_replica, madnn.device(), seq_len=a.seq, vocab=cfg.vocab_size)[0]
     for step in range(a.steps):
         loss = eng.train_step(ids, ids)
         opt.step()
