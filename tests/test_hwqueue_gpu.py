@@ -57,3 +57,42 @@ def test_engine_pipeline_program_completes_on_real_hw_queues(cuda, kind, V, lag)
     rec = replay(kind, V, 8, "engine", spin_us=100, timeout_us=200000,
                  epoch=100 + V + (kind == "gpipe") + (10 if lag else 0), lag=lag)
     assert rec["timed_out"] == 0 and rec["unset"] == 0, rec
+
+
+_CHILD = r"""
+import json, sys
+sys.path.insert(0, {root!r})
+import torch
+import madnn.ops as ops
+from madnn.utils.hwqueue import replay
+assert ops.load_kernels()
+out = []
+for design, lag in (("engine", 0.0), ("engine", 0.3), ("prepost", 0.0)):
+    out.append(replay("1f1b", 1, 8, design, spin_us=100, timeout_us=100000, epoch=1 + len(out), lag=lag))
+print("RESULT " + json.dumps(out), flush=True)
+"""
+
+
+@pytest.mark.parametrize("queues", [1, 2])
+def test_replay_negative_control_at_few_hw_queues(queues):
+    """The replay can fail for the reason it guards against: with GPU_MAX_HW_QUEUES = 1 (set
+    before the child process touches the GPU) every stream of a replayed rank shares one hardware
+    queue -- the fully serialised setting of the transport's safety argument (pp.issue_plan) --
+    and the round-3 design that posts every receive up front deadlocks (its messages time out),
+    while both of the engine's issue plans complete.  At 2 queues the engine plans complete too."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(queues))
+    res = subprocess.run([sys.executable, "-c", _CHILD.format(root=root)], env=env, capture_output=True, text=True,
+                         timeout=100)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [ln for ln in res.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    eng0, eng_lag, prepost = json.loads(line[len("RESULT "):])
+    for rec in (eng0, eng_lag):
+        assert rec["timed_out"] == 0 and rec["unset"] == 0, rec
+    if queues == 1:
+        assert prepost["timed_out"] > 0, prepost
