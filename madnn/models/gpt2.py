@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import ops
 from ..nn.norm import FusedLayerNorm
 from .common import init_module_, SelfAttention, causal_lm_loss, init_normal_, linear, scale_residual_proj_
 
@@ -71,8 +72,14 @@ class GPT2MLP(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, x, residual=None):
-        """MLP(x) (+ ``residual``, added in c_proj's GEMM epilogue when dropout is off)."""
-        if residual is not None and (self.drop.p == 0.0 or not self.training):
+        """MLP(x) (+ ``residual``, added in c_proj's GEMM epilogue when dropout is off).  Plain
+        ``nn.Linear`` layers run as ONE fused autograd node (``ops.gelu_mlp``): the GELU and its
+        backward live in the two GEMMs' epilogues."""
+        no_drop = self.drop.p == 0.0 or not self.training
+        if no_drop and ops.FUSED_LINEAR and type(self.c_fc) is nn.Linear and type(self.c_proj) is nn.Linear:
+            return ops.gelu_mlp(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias,
+                                residual)
+        if residual is not None and no_drop:
             return linear(self.c_proj, linear(self.c_fc, x, gelu=True), residual=residual)
         y = self.drop(linear(self.c_proj, linear(self.c_fc, x, gelu=True)))
         return y + residual if residual is not None else y

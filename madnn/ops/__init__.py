@@ -1209,6 +1209,7 @@ def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
 WGRAD = os.environ.get("MADNN_WGRAD", "auto")  # weight-gradient GEMM: auto (timed per shape) | lt | k12
 _WGRAD_CHOICE: dict = {}
 _GELU_FWD_CHOICE: dict = {}
+_DGELU_CHOICE: dict = {}
 _TUNE = {"timed": 0, "table": None}   # run-time timings taken; the shipped table that was loaded
 
 # Per-shape implementation choices measured on MI355X and shipped in-tree, so a job starts
@@ -1234,7 +1235,7 @@ def load_tuning_table(path: Optional[str] = None) -> int:
     except (OSError, ValueError):
         return 0
     n = 0
-    for name, dst in (("wgrad", _WGRAD_CHOICE), ("gelu_fwd", _GELU_FWD_CHOICE)):
+    for name, dst in (("wgrad", _WGRAD_CHOICE), ("gelu_fwd", _GELU_FWD_CHOICE), ("dgelu", _DGELU_CHOICE)):
         for k, v in data.get(name, {}).items():
             dst.setdefault(ast.literal_eval(k), v)
             n += 1
@@ -1247,7 +1248,8 @@ def export_choices(path: str) -> None:
     import json
 
     data = {"arch": "gfx950", "wgrad": {repr(k): v for k, v in sorted(_WGRAD_CHOICE.items(), key=repr)},
-            "gelu_fwd": {repr(k): v for k, v in sorted(_GELU_FWD_CHOICE.items(), key=repr)}}
+            "gelu_fwd": {repr(k): v for k, v in sorted(_GELU_FWD_CHOICE.items(), key=repr)},
+            "dgelu": {repr(k): v for k, v in sorted(_DGELU_CHOICE.items(), key=repr)}}
     with open(path, "w") as f:
         json.dump(data, f, indent=1)
         f.write("\n")
@@ -1260,10 +1262,11 @@ def sync_choices(group=None, src: int = 0) -> None:
 
     if not dist.is_initialized() or dist.get_world_size(group) <= 1:
         return
-    obj = [(dict(_WGRAD_CHOICE), dict(_GELU_FWD_CHOICE))]
+    obj = [(dict(_WGRAD_CHOICE), dict(_GELU_FWD_CHOICE), dict(_DGELU_CHOICE))]
     dist.broadcast_object_list(obj, src=src, group=group)
     _WGRAD_CHOICE.update(obj[0][0])
     _GELU_FWD_CHOICE.update(obj[0][1])
+    _DGELU_CHOICE.update(obj[0][2])
 
 
 def tuning_timings() -> int:
@@ -1381,16 +1384,43 @@ def _k12_fwd_ok(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Ten
             and load_kernels())
 
 
+def _k12p_ok(rows: torch.Tensor, weight: torch.Tensor, out_features: int, tokens: int, red: int,
+             has_bias: bool) -> bool:
+    """K12P (the persistent GEMM with fused epilogues, gemmp.hip) takes the shape: 256-multiples
+    of tokens and output features (no edge tiles), a 64-multiple reduction, contiguous 16-B aligned
+    bf16 operands."""
+    return (_is_dev(rows) and rows.dtype == weight.dtype == torch.bfloat16 and rows.is_contiguous()
+            and weight.is_contiguous() and rows.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0
+            and load_kernels() and bool(torch.ops.madnn.gemmp_supported(out_features, tokens, red, has_bias)))
+
+
+def _timed_choice(table: dict, key, cands: dict, default: str) -> str:
+    """The implementation in ``cands`` that was faster for ``key`` (shipped table, else timed
+    once on first use outside graph capture, like :func:`tuned_wgrad`)."""
+    choice = table.get(key)
+    if choice in cands:
+        return choice
+    if torch.cuda.is_current_stream_capturing():
+        return default
+    _TUNE["timed"] += 1
+    times = {k: _time_wgrad(f) for k, f in cands.items()}
+    choice = table[key] = min(times, key=times.get)
+    return choice
+
+
 def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
-    """``(gelu_tanh(pre), pre)`` with ``pre = x W^T + b``, from whichever of two implementations was
+    """``(gelu_tanh(pre), pre)`` with ``pre = x W^T + b``, from whichever implementation was
     faster for the shape (timed once on first use, like :func:`tuned_wgrad`):
 
     * ``lt``: hipBLASLt GEMM (bias epilogue), then the K11 streaming GELU pass (hipBLASLt has no
       GELU+AUX algorithm at GPT-2's 65536-row shapes on gfx950);
-    * ``k12``: one K12 GEMM whose epilogue adds the bias, stores the pre-activation (the backward's
-      AUX) and the GELU output from the same LDS-staged rows -- no separate HBM pass.
+    * ``k12p``: K12P, the persistent GEMM whose epilogue adds the bias, stores the pre-activation
+      (the backward's AUX) and the GELU output from the accumulators while the next tile's
+      operands stream in (on shapes without edge tiles);
+    * ``k12``: the one-tile-per-workgroup K12 with the same epilogue staged through LDS (other
+      shapes).
 
-    ``MADNN_GELU_FWD=lt`` / ``k12`` pin one."""
+    ``MADNN_GELU_FWD=lt`` / ``k12`` / ``k12p`` pin one."""
     x2 = x.reshape(-1, x.shape[-1])
     out_shape = (*x.shape[:-1], weight.shape[0])
 
@@ -1401,23 +1431,59 @@ def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
     def k12():
         return torch.ops.madnn.linear_fwd(x2, weight, bias, None, 1, True)
 
+    def k12p():
+        return torch.ops.madnn.linear_fwd_p(x2, weight, bias, 1)
+
+    ok12 = _k12_fwd_ok(x2, weight, bias)
+    okp = ok12 and _k12p_ok(x2, weight, weight.shape[0], x2.shape[0], x2.shape[1], bias is not None)
     choice = GELU_FWD
-    if choice not in ("lt", "k12"):
+    if choice == "k12p" and not okp or choice == "k12" and not ok12:
         choice = "lt"
-        if _k12_fwd_ok(x2, weight, bias):
+    if choice not in ("lt", "k12", "k12p"):
+        choice = "lt"
+        if okp:
+            key = ("p", tuple(x2.shape), tuple(weight.shape), bias is not None)
+            choice = _timed_choice(_GELU_FWD_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")
+        elif ok12:
             key = (tuple(x2.shape), tuple(weight.shape), bias is not None)
-            choice = _GELU_FWD_CHOICE.get(key)
-            if choice is None:
-                if torch.cuda.is_current_stream_capturing():
-                    choice = "lt"
-                else:
-                    _TUNE["timed"] += 1
-                    t_lt, t_k12 = _time_wgrad(lt), _time_wgrad(k12)
-                    choice = _GELU_FWD_CHOICE[key] = "k12" if t_k12 < t_lt else "lt"
-    elif choice == "k12" and not _k12_fwd_ok(x2, weight, bias):
-        choice = "lt"
-    y, pre = k12() if choice == "k12" else lt()
+            choice = _timed_choice(_GELU_FWD_CHOICE, key, {"lt": lt, "k12": k12}, "lt")
+    y, pre = {"lt": lt, "k12": k12, "k12p": k12p}[choice]()
     return y.view(out_shape), pre.view(out_shape)
+
+
+DGELU = os.environ.get("MADNN_DGELU", "auto")  # c_proj dgrad + GELU backward: auto | lt | k12p
+
+
+def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dtype: torch.dtype):
+    """``(dh, db)``: the data gradient of the Linear after a tanh-GELU (``da = g2 @ w2``) pushed
+    through that GELU (``dh = da * gelu'(pre)``) plus the GELU Linear's bias gradient
+    (``db = sum(dh)``), from whichever was faster for the shape:
+
+    * ``lt``: hipBLASLt GEMM, then the K11 dGELU + column-sum pass (reads ``da`` and ``pre``,
+      writes ``dh``);
+    * ``k12p``: K12P with the dGELU epilogue -- ``da`` never reaches HBM, the column sums come from
+      the accumulators (per-wave partial rows + one finalize).
+
+    ``MADNN_DGELU=lt`` / ``k12p`` pin one."""
+    def lt():
+        db, dh = bias_grad(g2 @ w2, pre2, bias_dtype)
+        return dh, db
+
+    def k12p():
+        return tuple(torch.ops.madnn.linear_dgrad_p(g2, w2, pre2, bias_dtype))
+
+    ok = (bias_dtype in (torch.float32, torch.bfloat16) and _is_dev(pre2) and pre2.dtype == g2.dtype
+          and pre2.is_contiguous() and pre2.data_ptr() % 16 == 0
+          and _k12p_ok(g2, w2, w2.shape[1], g2.shape[0], g2.shape[1], False))
+    choice = DGELU if DGELU in ("lt", "k12p") else "auto"
+    if choice == "k12p" and not ok:
+        choice = "lt"
+    if choice == "auto":
+        choice = "lt"
+        if ok:
+            key = (tuple(g2.shape), tuple(w2.shape), str(bias_dtype))
+            choice = _timed_choice(_DGELU_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")
+    return lt() if choice == "lt" else k12p()
 
 
 class _LinearFn(torch.autograd.Function):
@@ -1498,6 +1564,95 @@ class _LinearFn(torch.autograd.Function):
                 dw = (g2.t() @ x2).to(weight.dtype)
         ctx.param = None
         return dx, dw, db, None, (g if ctx.has_res else None)
+
+
+def _linear_residual_fwd(a: torch.Tensor, weight, bias, residual):
+    """``a W^T + b (+ residual)``: one hipBLASLt call with the bias / residual epilogue when it
+    takes it, else ``F.linear`` + add."""
+    if residual is not None and _lt_ok(a, weight, False, True):
+        a2 = a.reshape(-1, a.shape[-1])
+        if not a2.is_contiguous():
+            a2 = a2.contiguous()
+        r2 = residual.reshape(-1, weight.shape[0]).contiguous()
+        out = _lt_linear(a2, weight, bias if bias is None or bias.is_contiguous() else bias.contiguous(), r2, False)
+        if out is not None:
+            return out[0].view(*a.shape[:-1], weight.shape[0])
+    y = F.linear(a, weight, bias)
+    return y + residual if residual is not None else y
+
+
+def _weight_grad(g2: torch.Tensor, x2: torch.Tensor, param: torch.Tensor) -> torch.Tensor:
+    """A Linear's weight gradient, written into the reducer's bucket slot when it has one."""
+    sink = grad_sink(param)
+    if sink is not None and sink.dtype == g2.dtype == x2.dtype and sink.is_contiguous():
+        return wgrad_into(g2, x2, sink)
+    if param.dtype == g2.dtype == x2.dtype and _is_dev(g2):
+        return wgrad_into(g2, x2, torch.empty(param.shape, dtype=param.dtype, device=param.device))
+    return (g2.t() @ x2).to(param.dtype)
+
+
+class _GeluMLPFn(torch.autograd.Function):
+    """``c_proj(gelu_tanh(c_fc(x))) (+ residual)`` as ONE autograd node, so that the GELU's
+    activation has no other consumer and its backward can live inside c_proj's data-gradient GEMM.
+
+    Forward: c_fc + bias + GELU in one GEMM epilogue (:func:`_gelu_linear_fwd`: K12P stores the
+    pre-activation and the activation from the accumulators), c_proj + bias + residual in
+    hipBLASLt's epilogue.  Backward: c_proj's bias gradient (the consumer's column sum when
+    attached), c_proj's weight gradient, then :func:`dgrad_dgelu` -- c_proj's data gradient with
+    c_fc's GELU backward and c_fc's bias gradient in its epilogue (no ``da`` in HBM, no K11
+    pass) -- and c_fc's weight and data gradients.  Weight gradients go straight into the
+    data-parallel buckets (:func:`grad_sink`).  Reference: the MP layer pair's activation
+    (nodemodule.lua:133-159)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, residual):
+        a, pre = _gelu_linear_fwd(x, w1, b1)
+        y = _linear_residual_fwd(a, w2, b2, residual)
+        ctx.save_for_backward(x, w1, pre, a, w2)
+        ctx.b1_dtype = b1.dtype if b1 is not None else None
+        ctx.b2_dtype = b2.dtype if b2 is not None else None
+        ctx.params = (w1, w2)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w1, pre, a, w2 = ctx.saved_tensors
+        p1, p2 = ctx.params
+        ctx.params = None
+        need = ctx.needs_input_grad
+        db2 = None
+        if ctx.b2_dtype is not None and need[4]:
+            cs = _attached(g, "_madnn_colsum")
+            if cs is not None and cs.numel() == g.shape[-1]:
+                db2 = cs.to(ctx.b2_dtype)
+            else:
+                db2, _ = bias_grad(g, None, ctx.b2_dtype)
+        g2 = g.reshape(-1, g.shape[-1])
+        if not g2.is_contiguous():
+            g2 = g2.contiguous()
+        a2 = a.reshape(-1, a.shape[-1])
+        dw2 = _weight_grad(g2, a2, p2) if need[3] else None
+        dh, db1 = dgrad_dgelu(g2, w2, pre.reshape(-1, pre.shape[-1]), ctx.b1_dtype or g2.dtype)
+        if ctx.b1_dtype is None or not need[2]:
+            db1 = None
+        x2 = x.reshape(-1, x.shape[-1])
+        dw1 = _weight_grad(dh, x2, p1) if need[1] else None
+        dx = (dh @ w1).view(*x.shape[:-1], w1.shape[1]) if need[0] else None
+        return dx, dw1, db1, dw2, db2, (g if ctx.has_res else None)
+
+
+def gelu_mlp(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2: torch.Tensor,
+             b2: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``linear(gelu_tanh(linear(x, w1, b1)), w2, b2) (+ residual)``: the transformer MLP as one
+    fused autograd node on HIP tensors (:class:`_GeluMLPFn`), eager ops elsewhere."""
+    if residual is not None and residual.shape[:-1] != x.shape[:-1]:
+        raise ValueError("gelu_mlp: residual must have the output's shape")
+    if not _is_dev(x) or not torch.is_grad_enabled() or w1.shape[0] % 8 or w2.shape[0] % 8:
+        h = F.gelu(F.linear(x, w1, b1), approximate="tanh")
+        y = F.linear(h, w2, b2)
+        return y + residual if residual is not None else y
+    return _GeluMLPFn.apply(x, w1, b1, w2, b2, residual)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,

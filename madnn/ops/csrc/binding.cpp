@@ -110,6 +110,12 @@ int madnn_wgrad_splits(int64_t, int64_t, int64_t);
 int madnn_gemm_tune(int, int);
 hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
                               hipStream_t);
+int madnn_gemmp_supported(int64_t, int64_t, int64_t, int);
+hipError_t madnn_linear_fwd_p(const void*, const void*, const void*, int, void*, void*, int, int64_t, int64_t,
+                              int64_t, hipStream_t);
+hipError_t madnn_linear_dgrad_p(const void*, const void*, const void*, void*, float*, int64_t, int64_t, int64_t,
+                                hipStream_t);
+hipError_t madnn_colsum_finalize(const float*, int, int64_t, void*, int, hipStream_t);
 hipError_t madnn_hwq_wait(const int*, int, int64_t, int*, hipStream_t);
 hipError_t madnn_hwq_set(int*, int, hipStream_t);
 hipError_t madnn_hwq_batch(const int*, const int*, int, int*, int*, int, int64_t, int*, const int*, hipStream_t);
@@ -824,6 +830,71 @@ at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::op
 
 int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) { return madnn_wgrad_splits(M, N, K); }
 
+// ---- K12P persistent GEMMs with overlapped epilogues (gemmp.hip) ------------------------------
+bool gemmp_supported(int64_t I, int64_t J, int64_t K, bool has_bias) {
+  return madnn_gemmp_supported(I, J, K, has_bias ? 1 : 0) != 0;
+}
+
+// y = x w^T (+ bias); act 1: (gelu(pre), pre) with pre = x w^T + bias
+std::tuple<at::Tensor, at::Tensor> linear_fwd_p(const at::Tensor& x, const at::Tensor& w,
+                                                const c10::optional<at::Tensor>& bias, int64_t act) {
+  gemm_check(x, "x");
+  gemm_check(w, "w");
+  const int64_t K = x.size(-1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K, "linear_p: weight must be [N, K]");
+  const bool hb = bias.has_value() && bias->defined();
+  TORCH_CHECK(madnn_gemmp_supported(N, M, K, hb ? 1 : 0), "linear_p: unsupported shape M=", M, " N=", N, " K=", K);
+  if (hb) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() &&
+                    (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16),
+                "linear_p: bias must be a contiguous fp32/bf16 [N]");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
+  shape.back() = N;
+  at::Tensor y = at::empty(shape, x.options());
+  at::Tensor aux = act == 1 ? at::empty(shape, x.options()) : at::empty({0}, x.options());
+  check(madnn_linear_fwd_p(x.data_ptr(), w.data_ptr(), hb ? bias->data_ptr() : nullptr,
+                           hb && bias->scalar_type() == at::kFloat ? 1 : 0, y.data_ptr(),
+                           act == 1 ? aux.data_ptr() : nullptr, (int)act, M, N, K, cur_stream(x)),
+        "linear_fwd_p");
+  return {y, aux};
+}
+
+// dx = dy w; with pre: (dx * gelu'(pre), column sums of that in bias_dtype) -- the GELU backward
+// and c_fc's bias gradient fused into the data-gradient GEMM
+std::tuple<at::Tensor, at::Tensor> linear_dgrad_p(const at::Tensor& dy, const at::Tensor& w,
+                                                  const c10::optional<at::Tensor>& pre, at::ScalarType bias_dtype) {
+  gemm_check(dy, "dy");
+  gemm_check(w, "w");
+  const int64_t N = dy.size(-1), K = w.size(1), M = dy.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == N, "linear_dgrad_p: weight must be [N, K]");
+  TORCH_CHECK(madnn_gemmp_supported(K, M, N, 0), "linear_dgrad_p: unsupported shape M=", M, " N=", N, " K=", K);
+  const bool hp = pre.has_value() && pre->defined();
+  if (hp) {
+    gemm_check(*pre, "pre");
+    TORCH_CHECK(pre->numel() == M * K && pre->size(-1) == K, "linear_dgrad_p: pre must be [M, K]");
+    TORCH_CHECK(bias_dtype == at::kFloat || bias_dtype == at::kBFloat16, "linear_dgrad_p: fp32/bf16 bias grad");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  std::vector<int64_t> shape(dy.sizes().begin(), dy.sizes().end());
+  shape.back() = K;
+  at::Tensor dx = at::empty(shape, dy.options());
+  at::Tensor db = hp ? at::empty({K}, dy.options().dtype(bias_dtype)) : at::empty({0}, dy.options());
+  at::Tensor part;
+  const int rows = (int)(M / 256 * 4);
+  if (hp) part = at::empty({rows, K}, dy.options().dtype(at::kFloat));
+  check(madnn_linear_dgrad_p(dy.data_ptr(), w.data_ptr(), hp ? pre->data_ptr() : nullptr, dx.data_ptr(),
+                             hp ? part.data_ptr<float>() : nullptr, M, N, K, cur_stream(dy)),
+        "linear_dgrad_p");
+  if (hp)
+    check(madnn_colsum_finalize(part.data_ptr<float>(), rows, K, db.data_ptr(), bias_dtype == at::kFloat ? 1 : 0,
+                                cur_stream(dy)),
+          "colsum_finalize");
+  return {dx, db};
+}
+
 // ---- K13 NHWC 3x3 / stride 1 / pad 1 convolution on MFMA --------------------------------------
 // x: [N, Ci, H, W] channels_last bf16; w: [Co, Ci, 3, 3] channels_last ([Co][3][3][Ci] in memory).
 std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
@@ -1399,6 +1470,9 @@ TORCH_LIBRARY(madnn, m) {
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
   m.def("wgrad_splits(int M, int N, int K) -> int", &wgrad_splits);
+  m.def("gemmp_supported(int I, int J, int K, bool has_bias) -> bool", &gemmp_supported);
+  m.def("linear_fwd_p(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
+  m.def("linear_dgrad_p(Tensor dy, Tensor w, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, bool out_bf16) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
@@ -1466,6 +1540,8 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_fwd", linear_fwd);
   m.impl("linear_dgrad", linear_dgrad);
   m.impl("linear_wgrad", linear_wgrad);
+  m.impl("linear_fwd_p", linear_fwd_p);
+  m.impl("linear_dgrad_p", linear_dgrad_p);
   m.impl("conv3x3_fwd", conv3x3_fwd);
   m.impl("conv3x3_wgrad", conv3x3_wgrad);
   m.impl("hwq_wait", hwq_wait);

@@ -819,3 +819,26 @@ def test_planned_zero_lag_is_kept():
     assert _planned_lag(types.SimpleNamespace(p2p_lag=0.0)) == 0.0
     assert _planned_lag(types.SimpleNamespace(p2p_lag=0.27)) == 0.27
     assert _planned_lag(types.SimpleNamespace()) == _DEFAULT_LAG
+
+
+def test_gelu_mlp_autograd_node_matches_eager():
+    """The fused MLP node (c_fc + GELU + c_proj + residual as one autograd Function) against
+    eager autograd; on CPU it runs the same Function through its unfused implementations."""
+    from madnn.ops import _GeluMLPFn
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, dtype=torch.float64, requires_grad=True)
+    w1 = torch.randn(64, 16, dtype=torch.float64, requires_grad=True)
+    b1 = torch.randn(64, dtype=torch.float64, requires_grad=True)
+    w2 = torch.randn(16, 64, dtype=torch.float64, requires_grad=True)
+    b2 = torch.randn(16, dtype=torch.float64, requires_grad=True)
+    r = torch.randn(3, 5, 16, dtype=torch.float64, requires_grad=True)
+    y = _GeluMLPFn.apply(x, w1, b1, w2, b2, r)
+    gy = torch.randn_like(y)
+    got = torch.autograd.grad(y, (x, w1, b1, w2, b2, r), gy)
+    ref_y = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(x, w1, b1),
+                                                                approximate="tanh"), w2, b2) + r
+    ref = torch.autograd.grad(ref_y, (x, w1, b1, w2, b2, r), gy)
+    torch.testing.assert_close(y, ref_y)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b)
