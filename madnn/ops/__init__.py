@@ -214,7 +214,7 @@ def _linear_bias_dtype(x: torch.Tensor):
     gf = x.grad_fn
     if gf is not None and type(gf).__name__ in _VIEW_NODES and len(gf.next_functions) == 1:
         gf = gf.next_functions[0][0]
-    if gf is None or type(gf).__name__ != "_LinearFnBackward":
+    if gf is None or type(gf).__name__ not in ("_LinearFnBackward", "_GeluMLPFnBackward"):
         return None
     return getattr(gf, "bias_dtype", None)
 
@@ -1611,6 +1611,7 @@ class _GeluMLPFn(torch.autograd.Function):
         ctx.save_for_backward(x, w1, pre, a, w2)
         ctx.b1_dtype = b1.dtype if b1 is not None else None
         ctx.b2_dtype = b2.dtype if b2 is not None else None
+        ctx.bias_dtype = ctx.b2_dtype   # the output's bias: consumers attach its column sum (_linear_bias_dtype)
         ctx.params = (w1, w2)
         ctx.has_res = residual is not None
         return y
