@@ -54,7 +54,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--model", default="all", choices=["all", "resnet50", "gpt2-medium"])
+    ap.add_argument("--model", default="all", choices=["all", "resnet50", "gpt2-medium", "bert-large", "llama3-8b"],
+                    help="all (the driver's contract: ResNet-50 + GPT-2), one half of it, or one of BASELINE's other "
+                         "configs: bert-large (config 5) / llama3-8b (config 4), planned by madnn.distribute "
+                         "(strategy and activation checkpointing are the planner's)")
+    ap.add_argument("--tf-config", default=None,
+                    help="bert / llama size for --model bert-large|llama3-8b (default: that model; bert-tiny / "
+                         "llama3-tiny for CPU harness tests)")
+    ap.add_argument("--tf-batch-per-gpu", type=int, default=None,
+                    help="sequences per GPU for --model bert-large (default 128 at --seq-len 512) / llama3-8b "
+                         "(default 4 at --seq-len 4096)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
     ap.add_argument("--gpt2-batch-per-gpu", type=int, default=128,
                     help="GPT-2 sequences per GPU (global = this x N); 128: 369k tok/s vs 360k at 64 on one "
@@ -78,7 +87,7 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--channels-last", type=int, default=1)
-    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--seq-len", type=int, default=None, help="default 1024 (GPT-2), 512 (BERT), 4096 (Llama)")
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--device", default="cuda", help="cuda (MI355X) or cpu (gloo; for testing the harness)")
@@ -322,6 +331,79 @@ def bench_gpt2(args, world, rank):
     return dt, steps, gbatch, info
 
 
+TF_METRIC = {"bert-large": "tokens/s BERT-large auto-partition + activation checkpointing + fused Adam (BASELINE "
+                           "config 5)",
+             "llama3-8b": "tokens/s Llama-3 8B auto hybrid DP x PP, 288 GB per-GPU sizing (BASELINE config 4)"}
+
+
+def bench_transformer(args, world, rank):
+    """BASELINE configs 4 and 5 on the same timing contract as the headline: the planner
+    (``strategy="auto"``, ``checkpointing="auto"``) places the model on this job's GPUs -- DP, PP
+    or DP x PP, and per block whether to recompute activations, priced against 288 GB -- and the
+    K steps are bracketed by a barrier + device synchronize, MAX over ranks.  Llama-3 8B is built
+    on the meta device and materialised per rank (its stage only under a pipeline plan)."""
+    import madnn
+    from madnn.optim import FusedAdam
+
+    name = args.model
+    seq = args.seq_len
+    torch.manual_seed(0)
+    if name == "bert-large":
+        from madnn.models.bert import BertForPreTraining, bert_config
+
+        cfg = bert_config(args.tf_config or "bert-large")
+        model = BertForPreTraining(cfg)
+        per_gpu = args.tf_batch_per_gpu or 128
+    else:
+        from madnn.models.llama import Llama, llama_config
+
+        cfg = llama_config(args.tf_config or "llama3-8b")
+        with torch.device("meta"):
+            model = Llama(cfg)
+        per_gpu = args.tf_batch_per_gpu or 4
+    gbatch = per_gpu * world
+    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
+    engine, opt = madnn.distribute(model, opt, strategy=args.strategy, checkpointing="auto", global_batch=gbatch,
+                                   example_input=torch.zeros(1, seq, dtype=torch.long))
+    plan = getattr(engine, "plan", None)
+    dp = plan.dp if plan is not None else world
+    stages = plan.pp if plan is not None else 1
+    replica = rank // stages if stages > 1 else rank
+    g = torch.Generator(device="cpu").manual_seed(4321 + replica)
+    ids = torch.randint(0, cfg.vocab_size, (gbatch // dp, seq), generator=g).to(madnn.device())
+
+    def step():
+        loss = engine.train_step(ids, ids)
+        opt.step()
+        return loss
+
+    tw = time.perf_counter()
+    tuning = 2 * len(getattr(engine, "_lags", [0.0])) if len(getattr(engine, "_lags", [0.0])) > 1 else 0
+    for _ in range(max(args.warmup, tuning + 1)):
+        step()
+    _sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    _sync_all()
+    dt = _max_over_ranks(time.perf_counter() - t0)
+    lv = float(loss.detach()) if loss is not None else None
+    ck = sum(bool(c) for c in plan.checkpoint) if plan is not None and plan.checkpoint else 0
+    nl = len(plan.checkpoint) if plan is not None and plan.checkpoint else None
+    tok = gbatch * seq * args.steps / dt
+    return {"metric": TF_METRIC[name], "value": round(tok, 1), "unit": "tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1000.0, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if madnn.device().type == "cuda" else "fp32",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {"model": args.tf_config or name, "global_batch": gbatch, "per_gpu_batch": per_gpu,
+                       "seq_len": seq, "parallelism": _parallelism(plan, world), "optimizer": "FusedAdam",
+                       "checkpointed_layers": ck, "layers": nl, "peak_mem_gib": _peak_gib(),
+                       "warmup_s": round(t0 - tw, 1), "loss": lv, "plan": _plan_info(plan),
+                       "plan_table": plan.table() if plan is not None else None,
+                       "samples_per_s": round(gbatch * args.steps / dt, 2)}}
+
+
 def _peak_gib():
     """This rank's peak allocated device memory (GiB) since the last reset; None on CPU."""
     if not torch.cuda.is_available():
@@ -367,6 +449,15 @@ def main():
     madnn.init(device=args.device, backend=args.backend)
     rank = madnn.get_rank()
     on_gpu = madnn.device().type == "cuda"
+    if args.seq_len is None:
+        args.seq_len = {"bert-large": 512, "llama3-8b": 4096}.get(args.model, 1024)
+    if args.model in TF_METRIC:
+        res = bench_transformer(args, world, rank)
+        if rank == 0:
+            print(res["config"].pop("plan_table") or "", file=sys.stderr)
+        _emit(res, rank, args)
+        madnn.shutdown()
+        return
     res = None
     if args.model in ("all", "resnet50"):
         dt, samples_per_step, config = bench_resnet(args, world, rank)

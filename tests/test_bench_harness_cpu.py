@@ -167,3 +167,24 @@ def test_bench_py_reports_resnet_when_gpt2_phase_fails():
         assert res["value"] > 0 and res["config"]["parallelism"] == "dp2"
         assert res["config"]["std_batch"]["per_gpu_batch"] == 2 and res["config"]["std_batch"]["value"] > 0
         assert "error" in res["gpt2_pp"] and res["gpt2_pp"]["parallelism"] == "pp2", fault
+
+
+@pytest.mark.parametrize("model,size", [("bert-large", "bert-tiny"), ("llama3-8b", "llama3-tiny")])
+def test_bench_py_transformer_configs_two_ranks_cpu(model, size):
+    """BASELINE configs 4 / 5 on the same timing contract: planner-chosen placement and
+    checkpointing, the checkpointed-layer count and the plan in the record."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--device", "cpu", "--model", model, "--tf-config", size, "--seq-len", "32", "--tf-batch-per-gpu", "2"]
+    env = dict(os.environ, OMP_NUM_THREADS="2", MADNN_LOG_LEVEL="WARNING")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    c = res["config"]
+    assert res["unit"] == "tokens/s" and res["n_gpus"] == 2 and c["global_batch"] == 4 and c["seq_len"] == 32
+    assert res["value"] == pytest.approx(4 * 32 * 2 / (res["ms_per_step"] * 2 / 1000), rel=1e-2)
+    assert c["plan"]["dp"] * c["plan"]["pp"] * c["plan"]["tp"] == 2
+    assert 0 <= c["checkpointed_layers"] <= c["layers"]
