@@ -508,7 +508,7 @@ class _XentFn(torch.autograd.Function):
         return grad, None, None, None, None
 
 
-XENT_FUSED = os.environ.get("MADNN_XENT_FUSED", "1") != "0"  # A/B switch (bench/gpt2_ab.py)
+XENT_FUSED = os.environ.get("MADNN_XENT_FUSED", "1") != "0"  # A/B switch
 
 
 def _xent_fused_ok(lg: torch.Tensor) -> bool:
@@ -626,7 +626,7 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 def conv1x1_route(cin: int, cout: int) -> tuple:
     """Which implementation runs each pass of a stride-1 1x1 conv, from the per-shape A/B of
-    ResNet-50's convolutions on MI355X (bench/conv1x1_vs_gemm.py + bench/k9_tune.py,
+    ResNet-50's convolutions on MI355X (round-1 A/B drivers, now in git history;
     profiles/r1_k9_conv1x1_ab.json):
 
     * forward: K9 (+ the BatchNorm statistics in its epilogue) where it is at least as fast as

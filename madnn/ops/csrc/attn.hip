@@ -537,6 +537,237 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
   }
 }
 
+// ----------------------------------------------------------- LDS-DMA tile staging (D = 64)
+
+__device__ __forceinline__ int swzf64(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+
+// A [64][64] bf16 tile -> the swz<64> LDS image by LDS-DMA (global_load_lds_dwordx4).  Wave w of 4
+// issues pieces 2w and 2w+1 (1 KiB = 8 rows each).  The image is lane-linear, so the XOR swizzle sits
+// on the SOURCE address (cdna_hip_programming.md rule 21): lane L of piece i fetches row 8i + L/8,
+// 16-B chunk (L % 8) ^ f(row).  Whole tiles only (S % 64 == 0: the launcher falls back to the
+// register-staged kernels otherwise).  No staging registers and no ds_write pass: the tile lands in
+// LDS while the wave computes, which is what lets the ring run two tiles ahead (the register-staged
+// loop waited for each tile's global latency at its end: 48 % of the dK/dV kernel's wave time in
+// s_waitcnt / barriers, profiles/r5_attn_pmc.md).  (buffer_load ... lds would range-check the tail,
+// but hipcc then drains vmcnt before every later ds_read: LDS-DMA through the global path it does not.)
+struct DmaTile64 {
+  int o0, o1;  // this lane's source element offsets within the tile (pieces 2w, 2w+1)
+  __device__ __forceinline__ void init(int wave, int lane, int64_t ld) {
+    const int r0 = 16 * wave + (lane >> 3), r1 = r0 + 8;
+    o0 = (int)((int64_t)r0 * ld + 8 * ((lane & 7) ^ swzf64(r0)));
+    o1 = (int)((int64_t)r1 * ld + 8 * ((lane & 7) ^ swzf64(r1)));
+  }
+  __device__ __forceinline__ void issue(const uint16_t* base, int64_t ld, int row0, uint16_t* tile, int wave) const {
+    const uint16_t* src = base + (int64_t)row0 * ld;
+    char* t = reinterpret_cast<char*>(tile) + 2 * wave * 1024;
+    glds16((const void*)(src + o0), (lds_void*)t);
+    glds16((const void*)(src + o1), (lds_void*)(t + 1024));
+  }
+};
+
+// 64 fp32 row statistics (LSE / delta of a query tile) -> LDS by one wave: one dword per lane
+__device__ __forceinline__ void dma_stats(const float* arr, float* dst) {
+  glds4((const void*)(arr + (threadIdx.x & 63)), (lds_void*)dst);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  // an LDS-DMA is a pending LDS write on the VM counter: __syncthreads() would drain it (vmcnt(0))
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// dK / dV with D = 64 on a 3-stage LDS-DMA ring (Q, dO, LSE and delta of query tile it + 2 are in
+// flight while tile it is computed).  Numerics as attn_bwd_dkdv_kernel<64, CAUSAL, U2, LIM, ACCD>:
+// the dP accumulators start at +delta against a NEGATED V^T operand (a sign flip of the 8 loop-
+// invariant V fragments in the prologue), so acc = delta - dP and dS = (-P) * acc, the negation a free
+// source modifier -- the raw delta from LDS needs no VALU.
+template <bool CAUSAL>
+__global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const MadnnAttnArgs a) {
+  constexpr int D = 64, DS = D / 16, DB = D / 32;
+  constexpr int kTileEl = kTile * D;
+  // ONE LDS array (a second __shared__ object can make hipcc drain vmcnt before LDS reads:
+  // cdna_hip_programming.md §5 'Projection GEMM' item 4a): Q[3] dO[3] tiles, LSE[3] delta[3], red
+  __shared__ __attribute__((aligned(16))) uint16_t smem[6 * kTileEl + 6 * 2 * kTile + 8 * D * 2];
+  uint16_t* const sQ = smem;
+  uint16_t* const sO = smem + 3 * kTileEl;
+  float* const sL = reinterpret_cast<float*>(smem + 6 * kTileEl);
+  float* const sD = sL + 3 * kTile;
+  float* const red = sD + 3 * kTile;  // [4][2 D]
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nkb = (a.S + kRowsWG - 1) / kRowsWG;
+  int kblk, b, hk;
+  map_block(nkb, a.Hkv, false, kblk, b, hk);
+  const int G = a.H / a.Hkv;
+  const int k0w = kblk * kRowsWG + wave * 32;
+  const int krow = k0w + l32;
+  const int kc = min(krow, a.S - 1);
+  bf16x8 kf[DS], vf[DS];
+  {
+    const uint16_t* kp = a.k + b * a.k_sb + hk * a.k_sh + (int64_t)kc * a.k_ss;
+    const uint16_t* vp = a.v + b * a.v_sb + hk * a.v_sh + (int64_t)kc * a.v_ss;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * hh);
+      u32x4 v = *reinterpret_cast<const u32x4*>(vp + 16 * s + 8 * hh);
+      v ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};  // -V (bf16 sign bits)
+      vf[s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  f32x16 dk[DB], dv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) {
+    dk[d] = zero16();
+    dv[d] = zero16();
+  }
+  const int t0 = CAUSAL ? (kblk * kRowsWG) / kTile : 0;
+  const int nt = (a.S + kTile - 1) / kTile - t0;
+  const int total = G * nt;
+  DmaTile64 gq, go;
+  gq.init(wave, lane, a.q_ss);
+  go.init(wave, lane, a.o_ss);
+  // the issue cursor (query head offset, query tile) runs two tiles ahead of the compute cursor
+  int iss_h = 0, iss_t = 0;
+  auto issue = [&](int buf) {
+    const int hq = hk * G + iss_h, q0 = (t0 + iss_t) * kTile;
+    gq.issue(a.q + b * a.q_sb + hq * a.q_sh, a.q_ss, q0, sQ + buf * kTileEl, wave);
+    go.issue(a.dout + b * a.o_sb + hq * a.o_sh, a.o_ss, q0, sO + buf * kTileEl, wave);
+    if (wave < 2) {
+      const int64_t so = ((int64_t)b * a.H + hq) * a.S + q0;
+      dma_stats((wave == 0 ? a.lse : a.delta) + so, (wave == 0 ? sL : sD) + buf * kTile);
+    }
+    if (++iss_t == nt) {
+      iss_t = 0;
+      ++iss_h;
+    }
+  };
+  // per-wave DMA instructions per tile (Q 2 + dO 2, + 1 statistics row on waves 0 / 1)
+  auto wait_all_but_one_tile = [&]() {
+    if (wave < 2) {
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+  };
+  if (total > 0) issue(0);
+  if (total > 1) {
+    issue(1);
+    wait_all_but_one_tile();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  int it = 0, cur_t = 0;
+  auto tile = [&](auto curc) {
+    constexpr int cur = decltype(curc)::value;
+    if (it + 2 < total) issue((cur + 2) % 3);
+    const int q0 = (t0 + cur_t) * kTile;
+    if (++cur_t == nt) cur_t = 0;
+    const uint16_t* tq = sQ + cur * kTileEl;
+    const uint16_t* to = sO + cur * kTileEl;
+    const float* tl = sL + cur * kTile;
+    const float* td = sD + cur * kTile;
+    if (!CAUSAL || q0 + kTile - 1 >= k0w) {
+      f32x16 sc[2], dp[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        sc[qb] = zero16();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[qb][r] = td[qb * 32 + acc_row(r, hh)];
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+          sc[qb] = mfma(lds_row<D>(tq, qb * 32 + l32, 2 * s + hh), kf[s], sc[qb]);
+          dp[qb] = mfma(lds_row<D>(to, qb * 32 + l32, 2 * s + hh), vf[s], dp[qb]);
+        }
+      }
+      if (CAUSAL && q0 < k0w + 31) {  // diagonal tile: one compare per element against a per-lane limit
+        const int lo = krow - q0 - 4 * hh;
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : -__builtin_inff();
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = ex2(fmaf(sc[qb][r], a.scale_log2, -tl[qb * 32 + acc_row(r, hh)]));
+          sc[qb][r] = p;
+          dp[qb][r] = (-p) * dp[qb][r];
+        }
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = pack_acc(sc[qb], s);
+          const bf16x8 sf = pack_acc(dp[qb], s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) {
+            dv[d] = mfma(pf, lds_tr<D>(to, qb * 32 + 16 * s, d * 32, lane), dv[d]);
+            dk[d] = mfma(sf, lds_tr<D>(tq, qb * 32 + 16 * s, d * 32, lane), dk[d]);
+          }
+        }
+      }
+    }
+    // tile it + 1 has landed (tile it + 2 may stay in flight); every wave's reads of this tile
+    // retire before the barrier, after which tile it + 3 may be issued into its stage
+    if (it + 2 < total) {
+      wait_all_but_one_tile();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    ++it;
+  };
+  while (it < total) {
+    tile(std::integral_constant<int, 0>{});
+    if (it < total) tile(std::integral_constant<int, 1>{});
+    if (it < total) tile(std::integral_constant<int, 2>{});
+  }
+  // lane holds dK/dV[key = k0w + acc_row(r, hh)][d = 32*db + l32]
+  uint16_t* kp = a.dk + b * a.dk_sb + hk * a.dk_sh;
+  uint16_t* vp = a.dv + b * a.dv_sb + hk * a.dv_sh;
+  float ck[DB], cv[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) ck[d] = cv[d] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = k0w + acc_row(r, hh);
+    if (key < a.S) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        const unsigned short kb16 = f32_to_bf16(dk[d][r] * a.scale), vb16 = f32_to_bf16(dv[d][r]);
+        kp[(int64_t)key * a.dk_ss + d * 32 + l32] = kb16;
+        vp[(int64_t)key * a.dv_ss + d * 32 + l32] = vb16;
+        ck[d] += bf16_to_f32(kb16);
+        cv[d] += bf16_to_f32(vb16);
+      }
+    }
+  }
+  if (a.cpart != nullptr) {
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+      ck[d] += __shfl_xor(ck[d], 32);
+      cv[d] += __shfl_xor(cv[d], 32);
+      if (hh == 0) {
+        red[wave * 2 * D + d * 32 + l32] = ck[d];
+        red[wave * 2 * D + D + d * 32 + l32] = cv[d];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * D) {
+      const float s = red[tid] + red[2 * D + tid] + red[4 * D + tid] + red[6 * D + tid];
+      const int64_t C = (int64_t)(a.H + 2 * a.Hkv) * D;
+      const int64_t col = (int64_t)a.H * D + (tid < D ? (int64_t)hk * D + tid : (int64_t)(a.Hkv + hk) * D + tid - D);
+      a.cpart[((int64_t)b * nkb + kblk) * C + col] = s;
+    }
+  }
+}
+
 // --------------------------------------------------------------- backward: dK, dV
 // ACCD: the tile's -delta rows are read from LDS straight into the dP accumulator before its MFMAs
 // (dP - delta then costs no VALU: dS = P * acc)
@@ -786,6 +1017,7 @@ __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float*
 int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default), 0 = V1
 // (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
 // their loops are not VALU-issue-bound)
+int g_attn_dkdv_dma = 1;  // madnn_attn_tune(7, v): D = 64 dK/dV on the 3-stage LDS-DMA ring (0: register staging)
 int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
 int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
 int g_attn_dq_u2 = 1;     // madnn_attn_tune(3, v): the same for the dQ loop
@@ -827,7 +1059,9 @@ hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
   }
   MADNN_HIP_CHECK(hipGetLastError());
-  if (D == 64 && g_attn_bwd_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
+  if (D == 64 && g_attn_dkdv_dma && a.S % kTile == 0) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+  } else if (D == 64 && g_attn_bwd_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true, D == 64>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0,
                        st, a);
   } else if (g_attn_bwd_u2 && g_attn_mask_lim) {
@@ -855,7 +1089,7 @@ int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 // key 6 = dP accumulators started at -delta;
 // returns the previous value
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : nullptr;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : key == 7 ? &g_attn_dkdv_dma : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;

@@ -22,7 +22,7 @@ constexpr int kBiasLanes = 256;
 
 // 8 elements per lane per access (16-byte loads/stores), U accesses in flight per lane,
 // grid-stride over the flat tensor.  HBM-bound: reads x, writes y, nothing else.
-template <int DT, bool RCP = true, int U = 4>
+template <int DT, int U = 4>
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                        int64_t n8) {
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh<RCP>(v[u][j]);
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh(v[u][j]);
       store8<DT>(y, (i + u * stride) * 8, v[u]);
     }
   }
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
     float v[8];
     load8<DT>(x, i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh<RCP>(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
     store8<DT>(y, i * 8, v);
   }
 }
@@ -58,8 +58,9 @@ __host__ __device__ inline BiasGeom bias_geom(int N) {
   return {tpr, kBiasLanes / tpr, (lanes + tpr - 1) / tpr};
 }
 
-// U: rows per lane in flight in the main loop (A/B knob madnn_bias_tune2 key 0 for the GELU variant)
-template <int XDT, bool GELU, bool FAST = true, bool RCP = true, int U = 4>
+// U: rows per lane in flight in the main loop (the GELU variant at 2 / 8 measured -0.08 % / -0.54 % on
+// the GPT-2 medium step against 4, round 4)
+template <int XDT, bool GELU, int U = 4>
 __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
                                                                const void* __restrict__ pre, void* __restrict__ dp,
                                                                int64_t M, int N, float* __restrict__ partial) {
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad<FAST, RCP>(p[u][j]);
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad(p[u][j]);
           store8<XDT>(dp, (r + u * step) * N + col, v[u]);
         }
       }
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
         float p[8];
         load8<XDT>(pre, r * N + col, p);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad<FAST, RCP>(p[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad(p[j]);
         store8<XDT>(dp, r * N + col, v);
       }
 #pragma unroll
@@ -158,34 +159,12 @@ using namespace madnn;
 // Round 2, GPT-2 medium at 64 x 1024 (M = 65536; profiles/r2_ab_madnn_bias_tune_*.json): the plain sum at
 // 2 per CU is 1.0 % faster per step than at 1 (4: +0.8 %); the GELU variant stays at 4 (2: +0.1 %, 8: -0.4 %).
 static int g_bias_wg_per_cu[2] = {2, 4};
-static int g_bias_fast_tanh = 1;  // A/B knob: exp2-based tanh in the GELU backward (1) or libm tanhf (0)
-static int g_gelu_rcp = 1;        // A/B knob: v_rcp (1) or the IEEE division (0) in the exp2-based tanh
-static int g_bias_gelu_unroll = 4;  // A/B knob (madnn_bias_tune2 key 0): GELU-variant rows in flight, 2, 4 or 8
 
 extern "C" {
 
 int madnn_bias_tune(int gelu, int wg_per_cu) {
   const int old = g_bias_wg_per_cu[gelu ? 1 : 0];
   if (wg_per_cu > 0) g_bias_wg_per_cu[gelu ? 1 : 0] = wg_per_cu;
-  return old;
-}
-
-int madnn_bias_tune2(int key, int value) {
-  if (key != 0) return -1;
-  const int old = g_bias_gelu_unroll;
-  if (value > 0) g_bias_gelu_unroll = value >= 8 ? 8 : value <= 2 ? 2 : 4;
-  return old;
-}
-
-int madnn_gelu_rcp(int on) {
-  const int old = g_gelu_rcp;
-  if (on >= 0) g_gelu_rcp = on != 0;
-  return old;
-}
-
-int madnn_bias_fast_tanh(int on) {
-  const int old = g_bias_fast_tanh;
-  if (on >= 0) g_bias_fast_tanh = on != 0;
   return old;
 }
 
@@ -227,13 +206,11 @@ hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t
   if (grid < 1) grid = 1;
   MADNN_DISPATCH_DT(dt, DT, {
     if (U == 16) {
-      hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 16>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 16>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
     } else if (U == 8) {
-      if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-      else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
     } else {
-      if (g_gelu_rcp) hipLaunchKernelGGL((gelu_fwd_kernel<DT, true, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-      else hipLaunchKernelGGL((gelu_fwd_kernel<DT, false, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
     }
   });
   return hipGetLastError();
@@ -248,21 +225,8 @@ hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M,
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 2) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true, 2>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
-                         M, N, partial);
-    } else if (pre && g_bias_fast_tanh && g_gelu_rcp && g_bias_gelu_unroll == 8) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true, 8>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
-                         M, N, partial);
-    } else if (pre && g_bias_fast_tanh && g_gelu_rcp) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
-                         N, partial);
-    } else if (pre && g_bias_fast_tanh) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, true, false>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp,
-                         M, N, partial);
-    } else if (pre) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true, false>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M,
-                         N, partial);
+    if (pre) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N, partial);
     } else {
       hipLaunchKernelGGL((bias_grad_kernel<XDT, false>), grid, dim3(kBiasLanes), 0, stream, dy, nullptr, nullptr,
                          M, N, partial);

@@ -32,7 +32,7 @@ struct BnGeom {
   int tpr, rpi;
 };
 
-// Run-time tunables of the two elementwise apply passes (bench/bn_order_ab.py sweeps them
+// Run-time tunables of the two elementwise apply passes (round-1 A/B sweeps
 // through madnn_bn_tune).
 //  reverse: walk the tensor from its far end.  The pass before an apply (statistics /
 //    backward reduction, or the conv that produced x) streams the same tensors front to back,

@@ -14,6 +14,33 @@ constexpr int kWave = 64;          // CDNA wavefront width (never 32)
 constexpr int kNumCU = 256;        // MI355X: 8 XCDs x 32 CUs
 constexpr int kNumXCD = 8;
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS-DMA (global_load_lds_dwordx4 / _dword: each lane's 16 / 4 bytes land at the wave-uniform LDS
+// address `dst` + size * lane), written as inline asm (cdna_hip_programming.md §5.7 recipe: M0 set and
+// restored inside the statement, s_nop 0 before the load).  Why not the builtin: hipcc treats every
+// later ds_read_b64_tr_b16 as aliasing each pending builtin LDS-DMA and drains vmcnt(0) before it,
+// which flushes the whole prefetch pipeline once per K step in every kernel that reads a transposed
+// operand (K12 data / weight gradients, K12P data gradient, the attention backward).  hipcc does not
+// count these loads: the kernels wait for them with their own counted s_waitcnt vmcnt(N) and barriers;
+// the compiler's own waits for its loads stay correct (they only ever see fewer younger operations).
+__device__ __forceinline__ void glds16(const void* src, lds_void* dst) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void glds4(const void* src, lds_void* dst) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
 // dtype codes shared with the Python side (madnn/ops/_native.py)
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 

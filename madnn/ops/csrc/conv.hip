@@ -52,7 +52,7 @@ constexpr int kThreads = 256;
 constexpr int kBK = 64;                // reduction depth of one pipeline step
 constexpr int kTargetWG = 2 * kNumCU;  // resident workgroups: 2 per CU
 
-// run-time tunables (bench/conv1x1_vs_gemm.py sweeps them through madnn_conv1x1_tune)
+// run-time tunables (swept through madnn_conv1x1_tune, profiles/r1_k9_tune.json)
 struct Tune {
   int fwd_wg = kTargetWG;  // forward / dgrad persistent grid target
   int wgrad_wg = 2 * kNumCU;  // weight-grad workgroups (tiles x m splits)
@@ -416,7 +416,7 @@ hipError_t launch(const GemmArgs& p, int grid, hipStream_t s) {
 // forward / dgrad: i tiles x j groups, each workgroup walking an equal share of the j tiles.
 // Shallow reductions (K < 512: one tile is a few k steps, HBM-bound) stay persistent so the next
 // tile's loads overlap this tile's epilogue; deep ones get one tile per workgroup (measured
-// faster: bench/k9_tune.py, profiles/r1_k9_tune.json).
+// faster: profiles/r1_k9_tune.json).
 inline void plan_persistent(GemmArgs& p, int64_t J, int BI, int64_t I, int64_t K) {
   p.i_tiles = (int)(I / BI);
   p.j_tiles = (int)((J + 127) / 128);

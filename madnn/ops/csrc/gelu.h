@@ -7,9 +7,9 @@
 
 namespace madnn {
 
-// FAST: on v_exp (libm tanhf is ~30 VALU per element with range branches: at 32 elements per lane
-// per row step the GELU backward pass was partly VALU-bound instead of HBM-bound); RCP: v_rcp_f32
-// (1 ulp) instead of the IEEE division sequence.
+// On v_exp_f32 and v_rcp_f32 (1 ulp): libm tanhf is ~30 VALU per element with range branches, and at
+// 32 elements per lane per row step the GELU backward pass was partly VALU-bound instead of HBM-bound
+// (the libm and IEEE-division variants were measured and dropped, rounds 2-3).
 // tanh-GELU through the logistic function: with u = k0 (x + k1 x^3),
 //   gelu(x)  = 0.5 x (1 + tanh u) = x s,      s = sigmoid(2u) = 1 / (1 + 2^(-2u log2 e))
 //   gelu'(x) = s + x s (1 - s) 2 u'(x),       2 u'(x) = 2 k0 (1 + 3 k1 x^2)
@@ -24,28 +24,21 @@ __device__ __forceinline__ float gelu_sig_arg(float x, float x2) {
   return x * fmaf(kB, x2, kA);
 }
 
-template <bool FAST = true, bool RCP = true>
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
-  if constexpr (FAST) {
-    const float e = __builtin_amdgcn_exp2f(gelu_sig_arg(x, x2));
-    const float s = RCP ? __builtin_amdgcn_rcpf(1.f + e) : 1.f / (1.f + e);
-    const float du = x * fmaf(2.f * k0 * 3.f * k1, x2, 2.f * k0);  // x 2u'(x)
-    return fmaf(du * s, 1.f - s, s);
-  } else {
-    const float t = tanhf(k0 * (x + k1 * x2 * x));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
-  }
+  const float e = __builtin_amdgcn_exp2f(gelu_sig_arg(x, x2));
+  const float s = __builtin_amdgcn_rcpf(1.f + e);
+  const float du = x * fmaf(2.f * k0 * 3.f * k1, x2, 2.f * k0);  // x 2u'(x)
+  return fmaf(du * s, 1.f - s, s);
 }
 
 // y = gelu_tanh(x) = x sigmoid(2u) on v_exp / v_rcp: the standalone GELU forward pass after c_fc
 // (hipBLASLt on gfx950 has no GELU epilogue that also returns the pre-activation the backward
 // needs, bench/lt_probe.py).
-template <bool RCP = true>
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float e = __builtin_amdgcn_exp2f(gelu_sig_arg(x, x * x));
-  return x * (RCP ? __builtin_amdgcn_rcpf(1.f + e) : 1.f / (1.f + e));
+  return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 
 }  // namespace madnn

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
       else if (part == 1) o = off[1][e];
       else if (part == 2) o = off[2][e];
       else o = off[3][e];
-      __builtin_amdgcn_global_load_lds((const void*)(base + o), (lds_void*)(dst + e * 512), 16, 0, 0);
+      glds16((const void*)(base + o), (lds_void*)(dst + e * 512));
     }
   };
 
@@ -399,8 +399,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
           float x0 = bf16_to_f32((unsigned short)(v[e] & 0xffffu));
           float x1 = bf16_to_f32((unsigned short)(v[e] >> 16));
           if (p.act == 1) {
-            x0 = round_bf16(gelu_tanh<true>(x0));
-            x1 = round_bf16(gelu_tanh<true>(x1));
+            x0 = round_bf16(gelu_tanh(x0));
+            x1 = round_bf16(gelu_tanh(x1));
           }
           if (p.res != nullptr) {
             x0 += bf16_to_f32((unsigned short)(rv[e] & 0xffffu));

@@ -153,8 +153,8 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
       oe1 = part == 2 ? o21 : o31;
     }
     uint16_t* dst = smem + ((cur_H >> 2) & 1) * kStage + part * kHalf + (2 * wave) * 512;
-    __builtin_amdgcn_global_load_lds((const void*)(base + oe0), (lds_void*)dst, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(base + oe1), (lds_void*)(dst + 512), 16, 0, 0);
+    glds16((const void*)(base + oe0), (lds_void*)dst);
+    glds16((const void*)(base + oe1), (lds_void*)(dst + 512));
     cur_H += 1;
     if ((cur_H & 3) == 0 && ++cur_t == nk) {
       cur_t = 0;
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
             const u32x4 d = swap_pairs(pack2(X[0], X[1]), pack2(X[2], X[3]), pack2(Y[0], Y[1]), pack2(Y[2], Y[3]));
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const float v0 = lo16(d[k]) * gelu_tanh_grad<true, true>(lo16(pv[mm][b][k]));
-              const float v1 = hi16(d[k]) * gelu_tanh_grad<true, true>(hi16(pv[mm][b][k]));
+              const float v0 = lo16(d[k]) * gelu_tanh_grad(lo16(pv[mm][b][k]));
+              const float v1 = hi16(d[k]) * gelu_tanh_grad(hi16(pv[mm][b][k]));
               cs[2 * k] += v0;
               cs[2 * k + 1] += v1;
               ov[mm][b][k] = pack2(v0, v1);
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
             *reinterpret_cast<u32x4*>(p.aux + (jb + 16 * b) * p.ldo + ib + 32 * m + io) = h;
             u32x4 o;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) o[k] = pack2(gelu_tanh<true>(lo16(h[k])), gelu_tanh<true>(hi16(h[k])));
+            for (int k = 0; k < 4; ++k) o[k] = pack2(gelu_tanh(lo16(h[k])), gelu_tanh(hi16(h[k])));
             *reinterpret_cast<u32x4*>(dst) = o;
           } else {
             *reinterpret_cast<u32x4*>(dst) = h;

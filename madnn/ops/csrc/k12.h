@@ -19,7 +19,6 @@ constexpr int kHalf = 128 * kBK;         // bf16 elements of one half-tile (16 K
 constexpr int kStage = 4 * kHalf;        // A0 A1 B0 B1
 constexpr int kLds = 2 * kStage;         // 128 KiB
 
-typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);

@@ -78,11 +78,9 @@ struct Raw8 {
 // Forward: the weight / bias columns of a lane never change across its grid-stride rows, so they
 // are loaded once before the loop (loading them after the row reductions exposed an L2 round trip
 // per row), and the next row's x (and residual) loads are issued before the current row's two
-// reductions, so every wave keeps a row of loads in flight while it reduces.
-// DEPTH = 2: two rows of loads in flight per wave (slots alternate with a compile-time index, so no
-// register copy waits on an in-flight load): one 2-KB row per wave at 32 waves per CU is ~64 KB in
-// flight per CU, under the ~90 KB HBM latency x bandwidth needs (A/B: madnn_norm_tune key 3).
-template <int XDT, int WDT, int TPR, int NC, int DEPTH = 1>
+// reductions, so every wave keeps a row of loads in flight while it reduces.  (Two rows in flight per
+// wave measured +0.05 % on the GPT-2 medium step, round 4: not kept.)
+template <int XDT, int WDT, int TPR, int NC>
 __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, const void* __restrict__ w, const void* __restrict__ b,
     void* __restrict__ y, void* __restrict__ sum_out, float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -103,45 +101,39 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
     }
   }
   const int64_t rstep = (int64_t)gridDim.x * RPB;
-  Raw8<XDT> nx[DEPTH][NC], nr[DEPTH][NC];
+  Raw8<XDT> nx[NC], nr[NC];
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      nx[d][c].zero();
-      nr[d][c].zero();
-    }
+  for (int c = 0; c < NC; ++c) {
+    nx[c].zero();
+    nr[c].zero();
   }
-  auto fetch = [&](auto slotc, int64_t row) {
-    constexpr int SL = decltype(slotc)::value;
+  auto fetch = [&](int64_t row) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (row < rows && col < H) {
-        nx[SL][c].load(x, row * H + col);
-        if (res) nr[SL][c].load(res, row * H + col);
+        nx[c].load(x, row * H + col);
+        if (res) nr[c].load(res, row * H + col);
       }
     }
   };
   int64_t row0 = (int64_t)blockIdx.x * RPB;
-  fetch(std::integral_constant<int, 0>{}, row0 + sub);
-  if constexpr (DEPTH == 2) fetch(std::integral_constant<int, 1>{}, row0 + rstep + sub);
-  auto step = [&](auto slotc) {
-    constexpr int SL = decltype(slotc)::value;
+  fetch(row0 + sub);
+  while (row0 < rows) {
     const int64_t row = row0 + sub;
     const bool live = row < rows;  // uniform per row group; all lanes still join the LDS reduction
     float v[NC][8];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      nx[SL][c].unpack(v[c]);
+      nx[c].unpack(v[c]);
       if (res) {
         float r[8];
-        nr[SL][c].unpack(r);
+        nr[c].unpack(r);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[c][j] += r[j];
       }
     }
-    fetch(slotc, row + DEPTH * rstep);  // this slot's next row flies under this row's reductions
+    fetch(row + rstep);  // the next row flies under this row's reductions
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -186,15 +178,6 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
       rstd_out[row] = rstd;
     }
     row0 += rstep;
-  };
-  if constexpr (DEPTH == 2) {
-    while (row0 < rows) {
-      step(std::integral_constant<int, 0>{});
-      if (row0 >= rows) break;
-      step(std::integral_constant<int, 1>{});
-    }
-  } else {
-    while (row0 < rows) step(std::integral_constant<int, 0>{});
   }
 }
 
@@ -475,16 +458,15 @@ static NormCfg pick_cfg(int H) {
 // backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
 // (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
 // +0.5 % over 16 (4: -0.1 %)
-static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1, g_norm_fwd_depth = 1;
+static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1;
 
 extern "C" {
 
 int madnn_norm_tune(int key, int value) {
-  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early
-         : key == 3 ? &g_norm_fwd_depth : nullptr;
+  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value > 0 || key == 2) *f = key == 3 ? (value >= 2 ? 2 : 1) : value;
+  if (value > 0 || key == 2) *f = value;
   return old;
 }
 
@@ -501,13 +483,8 @@ hipError_t madnn_norm_fwd(const void* x, const void* res, const void* w, const v
       constexpr int RPB = kNormThreads / TPR;
       int64_t blocks = (rows + RPB - 1) / RPB;
       const int grid = blocks > g_norm_fwd_wg * kNumCU ? g_norm_fwd_wg * kNumCU : (int)blocks;
-      if (g_norm_fwd_depth == 2 && TPR == kWave) {
-        hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC, TPR == kWave ? 2 : 1>), dim3(grid), dim3(kNormThreads), 0,
-                           stream, x, res, w, b, y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
-      } else {
-        hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w,
-                           b, y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
-      }
+      hipLaunchKernelGGL((norm_fwd_kernel<XDT, WDT, TPR, NC>), dim3(grid), dim3(kNormThreads), 0, stream, x, res, w,
+                         b, y, sum_out, mean_out, rstd_out, rows, H, eps, rms);
     });
   });
   return hipGetLastError();

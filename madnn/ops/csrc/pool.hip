@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_kernel(const void* __restrict
 
 using namespace madnn;
 
-// k=3/s=2 routing (A/B runs, bench/pool_ab.py, profiles/r1_pool_ab.json): 0 generic loops,
+// k=3/s=2 routing (A/B runs, profiles/r1_pool_ab.json): 0 generic loops,
 // 1 unrolled kernels (default), 2 unrolled kernels with the XCD-contiguous workgroup numbering.
 // At the stem shape (batch 512): fwd 389 / 379 / 408 us, bwd 434 / 398 / 398 us; the full
 // training step is unchanged within 0.1 % by either, so the pass is not latency- or L2-reuse-

@@ -3,7 +3,7 @@
 //
 // Why: with 3 input channels the NHWC stem is a poor fit for MIOpen's implicit-GEMM solvers
 // (0.9 ms forward at batch 512 on MI355X against a ~0.18 ms HBM bound; zero-padding the channels
-// to 4 or 8 is slower still: bench/stem_pad.py).
+// to 4 or 8 is slower still: round-1 A/B).
 //
 // Implicit GEMM, D[co][p] = sum_k W[co][k] X_patch[p][k], p = output pixel, with the reduction
 // ordered k = (kh, kw, c) and padded to 7 x 8 x 4 = 224 (kw = 7 and c = 3 carry zero weights):

@@ -805,29 +805,6 @@ def test_norm_fwd_two_rows_in_flight_matches_default(cuda, rows, H, res):
     torch.testing.assert_close(a.float(), ref, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("shape", [(16, 1024, 4096), (3, 77, 4096), (1000, 264)])
-def test_bias_grad_gelu_rows_in_flight_variants(cuda, shape):
-    """madnn_bias_tune2 key 0 = 2 / 8: the GELU bias-gradient kernel's main loop keeps 2 / 8 rows per lane in flight;
-    the GELU backward output is elementwise-identical to the 4-row default, the column sum within rounding."""
-    import ctypes
-
-    knob = ctypes.CDLL(str(ops.kernels_path())).madnn_bias_tune2
-    torch.manual_seed(7)
-    dy = torch.randn(*shape, device=cuda).bfloat16()
-    pre = torch.randn(*shape, device=cuda).bfloat16() * 2
-    res = {}
-    for u in (2, 4, 8):
-        old = knob(0, u)
-        try:
-            res[u] = ops.bias_grad(dy, pre, torch.float32)
-            torch.cuda.synchronize()
-        finally:
-            knob(0, old)
-    ref = res[4][0]
-    for u in (2, 8):
-        assert torch.equal(res[4][1], res[u][1])
-        torch.testing.assert_close(res[u][0], ref, atol=1e-4 * ref.abs().max().item() + 1e-4, rtol=1e-4)
-
 
 @pytest.mark.parametrize("V,ld", [(50257, 50304), (130, 136), (1000, 1000)])
 def test_one_pass_cross_entropy_fast_exp_variant(cuda, V, ld, monkeypatch):
