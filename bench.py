@@ -363,6 +363,12 @@ def bench_transformer(args, world, rank):
         per_gpu = args.tf_batch_per_gpu or 4
     gbatch = per_gpu * world
     opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
+    if world == 1 and any(p.is_meta for p in model.parameters()):
+        # one GPU holds the whole model whatever the plan: materialise it before planning, so the
+        # planner's chain calibration runs the real layers (N > 1: each rank builds its own stage)
+        from madnn.parallel.pp import materialize_
+
+        materialize_(model, madnn.device(), getattr(model, "init_weights", None), opt)
     engine, opt = madnn.distribute(model, opt, strategy=args.strategy, checkpointing="auto", global_batch=gbatch,
                                    example_input=torch.zeros(1, seq, dtype=torch.long))
     plan = getattr(engine, "plan", None)

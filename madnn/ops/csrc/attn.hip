@@ -768,6 +768,171 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const Madnn
   }
 }
 
+// The K / V key-tile ring of the D = 64 forward kernel (a dQ kernel on the same ring measured
+// bitwise-equal and no faster, profiles/r5_attn_ab_fwd_dq_dma.json, and was dropped): tile t + 2 is issued into
+// stage (t + 2) % 3 at the start of tile t (that stage last held tile t - 1, whose reads every wave
+// retired before the barrier that ended it); at the end of tile t each wave waits until at most its
+// own 4 DMA instructions of tile t + 2 are outstanding (tile t + 1 landed), then the barrier.
+struct KVRing64 {
+  static constexpr int kTileEl = kTile * 64;
+  DmaTile64 gk, gv;
+  const uint16_t *kb, *vb;
+  int64_t kld, vld;
+  uint16_t* sK;  // [3][kTileEl]
+  uint16_t* sV;  // [3][kTileEl]
+  int wave, ntiles;
+  __device__ __forceinline__ void init(const uint16_t* kb_, int64_t kld_, const uint16_t* vb_, int64_t vld_,
+                                       uint16_t* sK_, uint16_t* sV_, int wave_, int lane, int ntiles_) {
+    kb = kb_, vb = vb_, kld = kld_, vld = vld_, sK = sK_, sV = sV_, wave = wave_, ntiles = ntiles_;
+    gk.init(wave, lane, kld);
+    gv.init(wave, lane, vld);
+  }
+  __device__ __forceinline__ void issue(int t, int buf) const {
+    gk.issue(kb, kld, t * kTile, sK + buf * kTileEl, wave);
+    gv.issue(vb, vld, t * kTile, sV + buf * kTileEl, wave);
+  }
+  __device__ __forceinline__ void prologue() const {
+    if (ntiles > 0) issue(0, 0);
+    if (ntiles > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+  }
+  __device__ __forceinline__ void tile_start(int t, int cur) const {
+    if (t + 2 < ntiles) issue(t + 2, (cur + 2) % 3);
+  }
+  __device__ __forceinline__ void tile_end(int t) const {
+    if (t + 2 < ntiles) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+  }
+};
+
+// forward, D = 64, on the K / V LDS-DMA ring (numerics as attn_fwd_kernel<64, CAUSAL, true>)
+template <bool CAUSAL>
+__global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnArgs a) {
+  constexpr int D = 64, DS = D / 16, DB = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[6 * kTile * D];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
+  int qblk, b, h;
+  map_block(nqb, a.H, CAUSAL, qblk, b, h);
+  const int hk = h / (a.H / a.Hkv);
+  const int q0w = qblk * kRowsWG + wave * 32;
+  const int qrow = q0w + l32;
+  bf16x8 qf[DS];
+  {
+    const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)min(qrow, a.S - 1) * a.q_ss;
+#pragma unroll
+    for (int s = 0; s < DS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+  }
+  // retire the Q loads here: waited for lazily at first use, the compiler's counted wait would
+  // land inside the key loop and (DMA being invisible to it) drain the ring every tile
+#pragma unroll
+  for (int s = 0; s < DS; ++s) asm volatile("" ::"v"(qf[s]));
+  f32x16 o[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) o[d] = zero16();
+  float m = kNegBig, l = 0.f;
+  const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
+  KVRing64 ring;
+  ring.init(a.k + b * a.k_sb + hk * a.k_sh, a.k_ss, a.v + b * a.v_sb + hk * a.v_sh, a.v_ss, smem, smem + 3 * kTile * D,
+            wave, lane, kv_end / kTile);
+  ring.prologue();
+  int t = 0;
+  auto tile = [&](auto curc) {
+    constexpr int cur = decltype(curc)::value;
+    ring.tile_start(t, cur);
+    const uint16_t* tk = ring.sK + cur * KVRing64::kTileEl;
+    const uint16_t* tv = ring.sV + cur * KVRing64::kTileEl;
+    const int k0 = t * kTile;
+    if (!CAUSAL || k0 <= q0w + 31) {
+      f32x16 sc[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        sc[kb] = zero16();
+#pragma unroll
+        for (int s = 0; s < DS; ++s) sc[kb] = mfma(lds_row<D>(tk, kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
+      }
+      if (CAUSAL && k0 + kTile - 1 > q0w) {
+        const int lim = qrow - k0 - 4 * hh;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[kb][r] = kb * 32 + (r & 3) + 8 * (r >> 2) <= lim ? sc[kb][r] : -__builtin_inff();
+        }
+      }
+      float mx = sc[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float mtile = mx * a.scale_log2;
+      if (__any(mtile > m + kRescaleSlack)) {
+        const float mnew = fmaxf(m, mtile);
+        const float alpha = ex2(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        }
+        m = mnew;
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -m));
+          sc[kb][r] = p;
+          rs += p;
+        }
+      }
+      l += rs;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 pf = pack_acc(sc[kb], s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) o[d] = mfma(lds_tr<D>(tv, kb * 32 + 16 * s, d * 32, lane), pf, o[d]);
+        }
+      }
+    }
+    ring.tile_end(t);
+    ++t;
+  };
+  while (t < ring.ntiles) {
+    tile(std::integral_constant<int, 0>{});
+    if (t < ring.ntiles) tile(std::integral_constant<int, 1>{});
+    if (t < ring.ntiles) tile(std::integral_constant<int, 2>{});
+  }
+  const float lt = l + __shfl_xor(l, 32);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  if (qrow < a.S) {
+    uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qrow * a.o_ss;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        store4_bf16(op + d * 32 + 8 * g + 4 * hh, o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv,
+                    o[d][4 * g + 3] * inv);
+      }
+    }
+    if (hh == 0) a.lse[((int64_t)b * a.H + h) * a.S + qrow] = m + log2f(lt);
+  }
+}
+
 // --------------------------------------------------------------- backward: dK, dV
 // ACCD: the tile's -delta rows are read from LDS straight into the dP accumulator before its MFMAs
 // (dP - delta then costs no VALU: dS = P * acc)
@@ -1017,6 +1182,7 @@ __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float*
 int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default), 0 = V1
 // (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
 // their loops are not VALU-issue-bound)
+int g_attn_fwd_dma = 1;   // madnn_attn_tune(8, v): D = 64 forward on the K / V LDS-DMA ring
 int g_attn_dkdv_dma = 1;  // madnn_attn_tune(7, v): D = 64 dK/dV on the 3-stage LDS-DMA ring (0: register staging)
 int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
 int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
@@ -1029,7 +1195,9 @@ int g_attn_dkdv_accd = 1;
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
-  if (g_attn_v2) {
+  if (D == 64 && g_attn_fwd_dma && a.S % kTile == 0) {
+    hipLaunchKernelGGL((attn_fwd_dma_kernel<CAUSAL>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+  } else if (g_attn_v2) {
     hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, true>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
   } else {
     hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, false>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
@@ -1089,7 +1257,7 @@ int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 // key 6 = dP accumulators started at -delta;
 // returns the previous value
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : key == 7 ? &g_attn_dkdv_dma : nullptr;
+  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : key == 7 ? &g_attn_dkdv_dma : key == 8 ? &g_attn_fwd_dma : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;

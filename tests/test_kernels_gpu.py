@@ -459,7 +459,7 @@ def test_gelu_linear_forward_choices_match_fp32(cuda, monkeypatch, choice, bias_
     if b is not None:
         assert b.grad.dtype == bias_dt and _rel(b.grad, bf.grad) < 2e-2
     if choice == "auto":
-        assert set(madnn.ops._GELU_FWD_CHOICE.values()) <= {"k12", "lt"}
+        assert set(madnn.ops._GELU_FWD_CHOICE.values()) <= {"k12", "k12p", "lt"}
 
 
 @pytest.mark.parametrize("rms", [False, True])
