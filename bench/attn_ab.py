@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """K8 attention variants A/B in one process (interleaved rounds, same random operands): the
-``madnn_attn_tune`` keys given with --knob KEY:OFF:ON, at the GPT-2 medium and BERT-large shapes.
+``madnn_attn_tune`` keys given with --knob KEY:OFF:ON, at the GPT-2 medium, BERT-large and Llama-3 8B (B = 2, S = 4096, GQA, D = 128) shapes.
 Prints one JSON line per (shape, arm) with forward and backward times and TFLOP/s (forward
 4*B*H*S^2*D, halved when causal; backward 2.5x forward).
 
@@ -44,10 +44,12 @@ def main():
     tune = ctypes.CDLL(str(ops.kernels_path())).madnn_attn_tune
     key, off, on = (int(v) for v in a.knob.split(":"))
     rows = []
-    for name, S, H, D, causal in [("gpt2-medium", 1024, 16, 64, True), ("bert-large", 512, 16, 64, False)]:
-        B = a.batch
+    for name, S, H, HKV, D, causal, B in [("gpt2-medium", 1024, 16, 16, 64, True, a.batch),
+                                          ("bert-large", 512, 16, 16, 64, False, a.batch),
+                                          ("llama3-8b", 4096, 32, 8, 128, True, 2)]:
         g = torch.Generator(device="cuda").manual_seed(0)
-        q, k, v = (torch.randn(B, S, H, D, device="cuda", generator=g).bfloat16().requires_grad_(True) for _ in range(3))
+        q = torch.randn(B, S, H, D, device="cuda", generator=g).bfloat16().requires_grad_(True)
+        k, v = (torch.randn(B, S, HKV, D, device="cuda", generator=g).bfloat16().requires_grad_(True) for _ in range(2))
         do = torch.randn(B, S, H, D, device="cuda", generator=g).bfloat16()
         fl = 4.0 * B * H * S * S * D / (2 if causal else 1)
         o = ops.attention(q, k, v, causal=causal)

@@ -61,6 +61,8 @@ class BertEmbed(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, ids):
+        if ids.size(1) > self.position.num_embeddings:   # host-side: an out-of-range gather faults the GPU
+            raise ValueError(f"sequence length {ids.size(1)} exceeds max_position {self.position.num_embeddings}")
         pos = torch.arange(ids.size(1), device=ids.device)
         # single-segment synthetic input: token type 0 for every position
         x = self.word(ids) + (self.position(pos) + self.token_type.weight[0])

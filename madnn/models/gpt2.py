@@ -60,6 +60,8 @@ class GPT2Embed(nn.Module):
         self.drop = nn.Dropout(cfg.dropout)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        if ids.size(1) > self.wpe.num_embeddings:   # host-side: an out-of-range gather faults the GPU
+            raise ValueError(f"sequence length {ids.size(1)} exceeds n_positions {self.wpe.num_embeddings}")
         pos = torch.arange(ids.size(1), device=ids.device)
         return self.drop(self.wte(ids) + self.wpe(pos))
 

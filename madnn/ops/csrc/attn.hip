@@ -112,6 +112,26 @@ __device__ __forceinline__ bf16x8 pack_acc(const f32x16& x, int s) {
 // accumulator register r of lane half h -> row within the 32-row block
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// 8 bf16 scaled by k and rounded back to bf16: the exp2-domain operand prescale (row constants as
+// the initial accumulator, cdna_hip_programming.md 'Attention backward'): with Q (or K) prescaled by
+// -c, c = scale * log2(e), an S accumulator started at a row constant r ends as r - S' (S' = the
+// score in log2 units) and p = exp2(-acc) -- the negation a free source modifier -- so the per-element
+// scale-and-subtract (32 v_fma per tile per lane) is gone.  Cost: the operand is rounded to bf16 once
+// more (relative 2^-9 per element).
+__device__ __forceinline__ bf16x8 scale_bf16x8(const bf16x8& x, float k) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = static_cast<__bf16>(static_cast<float>(x[j]) * k);
+  return r;
+}
+
+__device__ __forceinline__ f32x16 splat16(float v) {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = v;
+  return z;
+}
+
 // [64][D] tile: global (row stride `ld` elements, rows >= nvalid read as zeros) -> regs -> LDS.
 // BUF (the backward kernels): buffer loads through a per-tile descriptor (base at row0, range = the
 // nvalid - row0 rows left): rows past the end come back as zeros from the range check, so the load
@@ -179,14 +199,61 @@ __device__ __forceinline__ void store4_bf16(uint16_t* p, float a, float b, float
 }
 
 // ------------------------------------------------------------------ forward
-// V2 (default; madnn_attn_tune(0, 0) selects V1 for A/B): the causal / sequence-end mask is one
-// compare of a compile-time key offset against a per-lane limit, and the running max is moved
-// only when a row's max grows by more than 2^8 (lazy rescale: the O / l rescale pass -- 32
-// multiplies and an exp per lane -- is skipped on most tiles; p <= 256 is exact in fp32 and
-// relative-exact in the bf16 P operand, and O / l and the LSE do not depend on which m is used).
+// The causal / sequence-end mask is one compare of a compile-time key offset against a per-lane
+// limit, and the running max is moved only when a row's max grows by more than 2^8 (lazy rescale:
+// the O / l rescale pass -- 32 multiplies and an exp per lane -- is skipped on most tiles; p <= 256 is
+// exact in fp32 and relative-exact in the bf16 P operand, and O / l and the LSE do not depend on
+// which m is used).
 constexpr float kRescaleSlack = 8.f;
 
-template <int D, bool CAUSAL, bool V2>
+// One key tile of the online softmax on the prescaled accumulators acc = mi - S' (masked: +inf; mi =
+// the rows' current reference, 0 before the first tile, m = kNegBig until then): the tile's row max
+// is mi - min(acc); when it passes m + slack (always on the first tile) O and l are rescaled, the
+// tile's acc shifted to the new reference and the splatted reference tuple (the next tiles' initial
+// accumulator) updated.  Then acc <- p = exp2(-acc) and l += the lane's part of the row sums.
+template <int DB>
+__device__ __forceinline__ void softmax_tile(f32x16 (&sc)[2], f32x16 (&o)[DB], float& m, float& mi, float& l,
+                                             f32x16& mref) {
+  float mn = sc[0][0];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mn = fminf(mn, sc[kb][r]);
+  }
+  mn = fminf(mn, __shfl_xor(mn, 32));
+  const float top = mi - mn;
+  if (__any(top > m + kRescaleSlack)) {
+    const float mnew = fmaxf(m, top);
+    const float alpha = ex2(m - mnew);
+    l *= alpha;
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    }
+    const float adj = mnew - mi;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[kb][r] += adj;
+    }
+    m = mi = mnew;
+    mref = splat16(mnew);
+  }
+  float rs = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = ex2(-sc[kb][r]);
+      sc[kb][r] = p;
+      rs += p;
+    }
+  }
+  l += rs;
+}
+
+template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
@@ -199,19 +266,20 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
   const int q0w = qblk * kRowsWG + wave * 32;
   const int qrow = q0w + l32;
 
-  // Q^T as the B operand of S^T = K.Q^T: lane holds Q[qrow][16s + 8hh + j]
+  // -c Q^T as the B operand of S^T = K.Q^T: lane holds -c Q[qrow][16s + 8hh + j]
   bf16x8 qf[DS];
   {
     const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)min(qrow, a.S - 1) * a.q_ss;
 #pragma unroll
-    for (int s = 0; s < DS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+    for (int s = 0; s < DS; ++s) qf[s] = scale_bf16x8(*reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh), -a.scale_log2);
   }
   const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
   f32x16 o[DB];
 #pragma unroll
   for (int d = 0; d < DB; ++d) o[d] = zero16();
-  float m = kNegBig, l = 0.f;
+  float m = kNegBig, mi = 0.f, l = 0.f;
+  f32x16 mref = zero16();
   const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
   const int ntiles = (kv_end + kTile - 1) / kTile;
 
@@ -233,63 +301,21 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
       f32x16 sc[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = zero16();
+        sc[kb] = mref;
 #pragma unroll
         for (int s = 0; s < DS; ++s) sc[kb] = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
       }
-      const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
-      if (edge) {
-        // V2: key k0 + kb*32 + acc_row(r, hh) is valid iff its compile-time offset
-        // kb*32 + (r&3) + 8*(r>>2) <= lim (one compare + select per element)
+      if ((k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w)) {
+        // key k0 + kb*32 + acc_row(r, hh) is valid iff its compile-time offset kb*32 + acc_row(r, 0)
+        // <= lim (one compare + select per element)
         const int lim = (CAUSAL ? min(a.S - 1, qrow) : a.S - 1) - k0 - 4 * hh;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            bool ok;
-            if constexpr (V2) {
-              ok = kb * 32 + (r & 3) + 8 * (r >> 2) <= lim;
-            } else {
-              const int key = k0 + kb * 32 + acc_row(r, hh);
-              ok = key < a.S && (!CAUSAL || key <= qrow);
-            }
-            sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
-          }
+          for (int r = 0; r < 16; ++r) sc[kb][r] = kb * 32 + acc_row(r, 0) <= lim ? sc[kb][r] : __builtin_inff();
         }
       }
-      // running max in log2 units of the scaled score: max(s) * c, c > 0
-      float mx = sc[0][0];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mtile = mx * a.scale_log2;
-      // rescale O only when some row's max moved (V2: by more than the slack); alpha == 1 exactly
-      // on the rows whose max did not move
-      if (__any(mtile > m + (V2 ? kRescaleSlack : 0.f))) {
-        const float mnew = fmaxf(m, mtile);
-        const float alpha = ex2(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int d = 0; d < DB; ++d) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-        }
-        m = mnew;
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -m));
-          sc[kb][r] = p;
-          rs += p;
-        }
-      }
-      l += rs;
+      softmax_tile<DB>(sc, o, m, mi, l, mref);
       // O^T[d][q] += sum_key V[key][d] P^T[key][q]
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -323,42 +349,16 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
   }
 }
 
-// ------------------------------------------------------- backward: delta = rowsum(dO * O)
-template <int D>
-__global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const MadnnAttnArgs a) {
-  constexpr int LPR = D / 8;  // lanes per (b, s, h) row
-  const int64_t rows = (int64_t)a.B * a.S * a.H;
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t row = gid / LPR;
-  const int part = (int)(gid % LPR);
-  float acc = 0.f;
-  int b = 0, s = 0, h = 0;
-  if (row < rows) {
-    h = (int)(row % a.H);
-    s = (int)((row / a.H) % a.S);
-    b = (int)(row / ((int64_t)a.H * a.S));
-    const int64_t off = b * a.o_sb + (int64_t)s * a.o_ss + h * a.o_sh + part * 8;
-    float x[8], y[8];
-    load8<kBF16>(a.dout, off, x);
-    load8<kBF16>(a.o, off, y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
-  }
-#pragma unroll
-  for (int w = LPR / 2; w > 0; w >>= 1) acc += __shfl_xor(acc, w, LPR);
-  if (row < rows && part == 0) a.delta[((int64_t)b * a.H + h) * a.S + s] = acc;
-}
-
 // ------------------------------------------------------------------ backward: dQ
-struct RtIndex {  // a run-time LDS buffer index with the .value interface of std::integral_constant
-  int value;
-};
-
-// ACCD: the dP^T accumulators start at -delta (a loop-invariant register tuple: delta belongs to the
-// lane's query row), so dS = P * acc costs no subtraction
-template <int D, bool CAUSAL, bool DELTA, bool U2, bool LIM = false, bool ACCD = false>
+// The S^T accumulators start at the lane's LSE (a loop-invariant register tuple) against the -c
+// prescaled Q, so p = exp2(-acc); ACCD (D = 64): the dP^T accumulators start at -delta the same way,
+// so dS = P * acc costs no subtraction (at D = 128 that tuple's 16 registers cost more than the
+// subtraction: -8 %, profiles/r4_ab_attn_valu_trees.log).  delta = rowsum(dO * O) is formed in the
+// prologue and written for the dK/dV kernel.  Two tiles per trip (compile-time LDS buffer index).
+template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
+  constexpr bool ACCD = D == 64;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
   // [128 rows][D] fp32 image (4 * 64 * D bf16 = 128 * D fp32)
   __shared__ __attribute__((aligned(16))) uint16_t sKV[4][kTile * D];
@@ -383,23 +383,17 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
     const uint16_t* op = a.o + b * a.o_sb + h * a.o_sh + (int64_t)qc * a.o_ss;
 #pragma unroll
     for (int s = 0; s < DS; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+      qf[s] = scale_bf16x8(*reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh), -a.scale_log2);
       df[s] = *reinterpret_cast<const bf16x8*>(dp + 16 * s + 8 * hh);
-      if constexpr (DELTA) {
-        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(op + 16 * s + 8 * hh);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(op + 16 * s + 8 * hh);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dl = fmaf(static_cast<float>(df[s][j]), static_cast<float>(ov[j]), dl);
-      }
+      for (int j = 0; j < 8; ++j) dl = fmaf(static_cast<float>(df[s][j]), static_cast<float>(ov[j]), dl);
     }
-    if constexpr (DELTA) dl += __shfl_xor(dl, 32, kWave);
+    dl += __shfl_xor(dl, 32, kWave);
   }
   const int64_t srow = ((int64_t)b * a.H + h) * a.S + qc;
-  const float lse = a.lse[srow];
-  if constexpr (DELTA) {
-    if (hh == 0 && qrow < a.S) a.delta[srow] = dl;
-  } else {
-    dl = a.delta[srow];
-  }
+  const f32x16 lse16 = splat16(a.lse[srow]);
+  if (hh == 0 && qrow < a.S) a.delta[srow] = dl;
   const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
   f32x16 dq[DB];
@@ -417,8 +411,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
   stv.store(sV[0], tid);
   __syncthreads();
   int t = 0;
-  auto tile = [&](auto curc) {  // U2: as in the dK/dV kernel
-    const int cur = curc.value;
+  auto tile = [&](auto curc) {
+    constexpr int cur = decltype(curc)::value;
     const bool more = t + 1 < ntiles;
     if (more) {
       stk.load(kb_, a.k_ss, (t + 1) * kTile, a.S, tid);
@@ -429,7 +423,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       f32x16 sc[2], dp[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = zero16();
+        sc[kb] = lse16;
         dp[kb] = ACCD ? ndl : zero16();
 #pragma unroll
         for (int s = 0; s < DS; ++s) {
@@ -440,32 +434,20 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       // masking as one wave-uniform block on the scores (exp2(-inf) = 0): interior tiles run
       // none of it (a per-element `if` costs an exec-mask branch per element)
       if ((k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w)) {
-        if constexpr (LIM) {
-          // LIM: key = k0 + off + 4 hh with off = kb*32 + acc_row(r, 0) a compile-time constant, so
-          // the mask is one compare of that constant against a per-lane limit
-          const int lim = (CAUSAL ? min(qrow, a.S - 1) : a.S - 1) - k0 - 4 * hh;
+        // key = k0 + off + 4 hh with off = kb*32 + acc_row(r, 0) a compile-time constant: the mask is
+        // one compare of that constant against a per-lane limit (acc = +inf: p = 0)
+        const int lim = (CAUSAL ? min(qrow, a.S - 1) : a.S - 1) - k0 - 4 * hh;
 #pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sc[kb][r] = (kb * 32 + acc_row(r, 0) <= lim) ? sc[kb][r] : -__builtin_inff();
-          }
-        } else {
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int key = k0 + kb * 32 + acc_row(r, hh);
-              const bool ok = key < a.S && (!CAUSAL || key <= qrow);
-              sc[kb][r] = ok ? sc[kb][r] : -__builtin_inff();
-            }
-          }
+          for (int r = 0; r < 16; ++r) sc[kb][r] = (kb * 32 + acc_row(r, 0) <= lim) ? sc[kb][r] : __builtin_inff();
         }
       }
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -lse));
+          const float p = ex2(-sc[kb][r]);
           sc[kb][r] = ACCD ? p * dp[kb][r] : p * (dp[kb][r] - dl);
         }
       }
@@ -487,15 +469,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
     __syncthreads();
     ++t;
   };
-  if constexpr (U2) {
-    while (t + 1 < ntiles) {
-      tile(std::integral_constant<int, 0>{});
-      tile(std::integral_constant<int, 1>{});
-    }
-    if (t < ntiles) tile(std::integral_constant<int, 0>{});
-  } else {
-    while (t < ntiles) tile(RtIndex{t & 1});
+  while (t + 1 < ntiles) {
+    tile(std::integral_constant<int, 0>{});
+    tile(std::integral_constant<int, 1>{});
   }
+  if (t < ntiles) tile(std::integral_constant<int, 0>{});
   if (qrow < a.S) {
     uint16_t* qp = a.dq + b * a.dq_sb + h * a.dq_sh + (int64_t)qrow * a.dq_ss;
     const float sc = a.scale;
@@ -579,10 +557,11 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 // dK / dV with D = 64 on a 3-stage LDS-DMA ring (Q, dO, LSE and delta of query tile it + 2 are in
-// flight while tile it is computed).  Numerics as attn_bwd_dkdv_kernel<64, CAUSAL, U2, LIM, ACCD>:
-// the dP accumulators start at +delta against a NEGATED V^T operand (a sign flip of the 8 loop-
-// invariant V fragments in the prologue), so acc = delta - dP and dS = (-P) * acc, the negation a free
-// source modifier -- the raw delta from LDS needs no VALU.
+// flight while tile it is computed).  Row constants as the initial accumulators, straight from LDS:
+// the S accumulators start at +LSE against the -c prescaled K (acc = LSE - S', p = exp2(-acc)), the
+// dP accumulators at +delta against a NEGATED V^T operand (a sign flip of the 8 loop-invariant V
+// fragments in the prologue), so acc = delta - dP and dS = (-P) * acc, the negations free source
+// modifiers -- neither row statistic costs VALU.
 template <bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const MadnnAttnArgs a) {
   constexpr int D = 64, DS = D / 16, DB = D / 32;
@@ -610,7 +589,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const Madnn
     const uint16_t* vp = a.v + b * a.v_sb + hk * a.v_sh + (int64_t)kc * a.v_ss;
 #pragma unroll
     for (int s = 0; s < DS; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * hh);
+      kf[s] = scale_bf16x8(*reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * hh), -a.scale_log2);
       u32x4 v = *reinterpret_cast<const u32x4*>(vp + 16 * s + 8 * hh);
       v ^= u32x4{0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u};  // -V (bf16 sign bits)
       vf[s] = __builtin_bit_cast(bf16x8, v);
@@ -673,9 +652,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const Madnn
       f32x16 sc[2], dp[2];
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
-        sc[qb] = zero16();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dp[qb][r] = td[qb * 32 + acc_row(r, hh)];
+        for (int r = 0; r < 16; ++r) {
+          sc[qb][r] = tl[qb * 32 + acc_row(r, hh)];
+          dp[qb][r] = td[qb * 32 + acc_row(r, hh)];
+        }
 #pragma unroll
         for (int s = 0; s < DS; ++s) {
           sc[qb] = mfma(lds_row<D>(tq, qb * 32 + l32, 2 * s + hh), kf[s], sc[qb]);
@@ -687,14 +668,14 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_dma_kernel(const Madnn
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : -__builtin_inff();
+          for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : __builtin_inff();
         }
       }
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = ex2(fmaf(sc[qb][r], a.scale_log2, -tl[qb * 32 + acc_row(r, hh)]));
+          const float p = ex2(-sc[qb][r]);
           sc[qb][r] = p;
           dp[qb][r] = (-p) * dp[qb][r];
         }
@@ -814,7 +795,7 @@ struct KVRing64 {
   }
 };
 
-// forward, D = 64, on the K / V LDS-DMA ring (numerics as attn_fwd_kernel<64, CAUSAL, true>)
+// forward, D = 64, on the K / V LDS-DMA ring (numerics as attn_fwd_kernel<64, CAUSAL>)
 template <bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnArgs a) {
   constexpr int D = 64, DS = D / 16, DB = D / 32;
@@ -831,7 +812,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnA
   {
     const uint16_t* qp = a.q + b * a.q_sb + h * a.q_sh + (int64_t)min(qrow, a.S - 1) * a.q_ss;
 #pragma unroll
-    for (int s = 0; s < DS; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh);
+    for (int s = 0; s < DS; ++s) qf[s] = scale_bf16x8(*reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * hh), -a.scale_log2);
   }
   // retire the Q loads here: waited for lazily at first use, the compiler's counted wait would
   // land inside the key loop and (DMA being invisible to it) drain the ring every tile
@@ -840,7 +821,8 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnA
   f32x16 o[DB];
 #pragma unroll
   for (int d = 0; d < DB; ++d) o[d] = zero16();
-  float m = kNegBig, l = 0.f;
+  float m = kNegBig, mi = 0.f, l = 0.f;
+  f32x16 mref = zero16();
   const int kv_end = CAUSAL ? min(a.S, qblk * kRowsWG + kRowsWG) : a.S;
   KVRing64 ring;
   ring.init(a.k + b * a.k_sb + hk * a.k_sh, a.k_ss, a.v + b * a.v_sb + hk * a.v_sh, a.v_ss, smem, smem + 3 * kTile * D,
@@ -857,7 +839,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnA
       f32x16 sc[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        sc[kb] = zero16();
+        sc[kb] = mref;
 #pragma unroll
         for (int s = 0; s < DS; ++s) sc[kb] = mfma(lds_row<D>(tk, kb * 32 + l32, 2 * s + hh), qf[s], sc[kb]);
       }
@@ -866,39 +848,10 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnA
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) sc[kb][r] = kb * 32 + (r & 3) + 8 * (r >> 2) <= lim ? sc[kb][r] : -__builtin_inff();
+          for (int r = 0; r < 16; ++r) sc[kb][r] = kb * 32 + acc_row(r, 0) <= lim ? sc[kb][r] : __builtin_inff();
         }
       }
-      float mx = sc[0][0];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kb][r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float mtile = mx * a.scale_log2;
-      if (__any(mtile > m + kRescaleSlack)) {
-        const float mnew = fmaxf(m, mtile);
-        const float alpha = ex2(m - mnew);
-        l *= alpha;
-#pragma unroll
-        for (int d = 0; d < DB; ++d) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-        }
-        m = mnew;
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = ex2(fmaf(sc[kb][r], a.scale_log2, -m));
-          sc[kb][r] = p;
-          rs += p;
-        }
-      }
-      l += rs;
+      softmax_tile<DB>(sc, o, m, mi, l, mref);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -934,11 +887,16 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_dma_kernel(const MadnnAttnA
 }
 
 // --------------------------------------------------------------- backward: dK, dV
-// ACCD: the tile's -delta rows are read from LDS straight into the dP accumulator before its MFMAs
-// (dP - delta then costs no VALU: dS = P * acc)
-template <int D, bool CAUSAL, bool U2, bool LIM = false, bool ACCD = false>
+// Register-staged dK / dV (D = 128, or a sequence length that is not a multiple of the 64-row
+// tile).  ACCD (D = 64): the tile's -delta rows are read from LDS straight into the dP accumulators
+// before their MFMAs (dS = P * acc: no VALU for delta; -8 % at D = 128, profiles/
+// r4_ab_attn_valu_trees.log).  The LSE stays a per-element subtraction here: started in the S
+// accumulators as in the DMA kernel, the extra LDS reads made hipcc wait on the next tile's staging
+// loads inside the MFMA chain (backward +40 %).  Two tiles per trip (compile-time LDS buffer index).
+template <int D, bool CAUSAL>
 __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
+  constexpr bool ACCD = D == 64;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[2][kTile * D];
   __shared__ __attribute__((aligned(16))) uint16_t sO[2][kTile * D];  // dO
   __shared__ float sL[2][kTile], sD[2][kTile];
@@ -1016,11 +974,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
   }
   __syncthreads();
   int cur_t = 0, nxt_h = 0, nxt_t = 0;  // this tile's query-tile index; the next tile's (head, tile)
-  // U2: two tiles per trip with the LDS buffer index a compile-time constant, so the buffer base
-  // folds into the ds_read immediate offsets instead of costing a VALU op per read address
+  // two tiles per trip with the LDS buffer index a compile-time constant, so the buffer base folds
+  // into the ds_read immediate offsets instead of costing a VALU op per read address
   int it = 0;
   auto tile = [&](auto curc) {
-    const int cur = curc.value;
+    constexpr int cur = decltype(curc)::value;
     const bool more = it + 1 < total;
     if (++nxt_t == nt) {
       nxt_t = 0;
@@ -1055,22 +1013,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
         }
       }
       if (CAUSAL && q0 < k0w + 31) {  // diagonal tile: one wave-uniform masking block
-        if constexpr (LIM) {
-          const int lo = krow - q0 - 4 * hh;  // query offset qb*32 + acc_row(r, 0) must reach it
+        const int lo = krow - q0 - 4 * hh;  // query offset qb*32 + acc_row(r, 0) must reach it
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) {
+        for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : -__builtin_inff();
-          }
-        } else {
-#pragma unroll
-          for (int qb = 0; qb < 2; ++qb) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int qi = qb * 32 + acc_row(r, hh);
-              sc[qb][r] = (krow <= q0 + qi) ? sc[qb][r] : -__builtin_inff();
-            }
-          }
+          for (int r = 0; r < 16; ++r) sc[qb][r] = (qb * 32 + acc_row(r, 0) >= lo) ? sc[qb][r] : -__builtin_inff();
         }
       }
 #pragma unroll
@@ -1106,15 +1053,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const MadnnAttn
     __syncthreads();
     ++it;
   };
-  if constexpr (U2) {
-    while (it + 1 < total) {
-      tile(std::integral_constant<int, 0>{});
-      tile(std::integral_constant<int, 1>{});
-    }
-    if (it < total) tile(std::integral_constant<int, 0>{});
-  } else {
-    while (it < total) tile(RtIndex{it & 1});
+  while (it + 1 < total) {
+    tile(std::integral_constant<int, 0>{});
+    tile(std::integral_constant<int, 1>{});
   }
+  if (it < total) tile(std::integral_constant<int, 0>{});
   // lane holds dK/dV[key = k0w + acc_row(r, hh)][d = 32*db + l32]
   uint16_t* kp = a.dk + b * a.dk_sb + hk * a.dk_sh;
   uint16_t* vp = a.dv + b * a.dv_sb + hk * a.dv_sh;
@@ -1179,28 +1122,19 @@ __global__ __launch_bounds__(1024) void attn_colsum_finalize_kernel(const float*
   }
 }
 
-int g_attn_v2 = 1;  // madnn_attn_tune(0, v): forward version, 1 = V2 (default), 0 = V1
-// (the same two changes in the backward kernels measured neutral at D = 64 and -1.5 % at D = 128:
-// their loops are not VALU-issue-bound)
-int g_attn_fwd_dma = 1;   // madnn_attn_tune(8, v): D = 64 forward on the K / V LDS-DMA ring
-int g_attn_dkdv_dma = 1;  // madnn_attn_tune(7, v): D = 64 dK/dV on the 3-stage LDS-DMA ring (0: register staging)
-int g_attn_dq_delta = 1;  // madnn_attn_tune(1, v): 1 = delta computed in the dQ kernel's prologue, 0 = own pass
-int g_attn_bwd_u2 = 1;    // madnn_attn_tune(2, v): dK/dV loop two tiles per trip (compile-time LDS buffer), 0 = one
-int g_attn_dq_u2 = 1;     // madnn_attn_tune(3, v): the same for the dQ loop
-int g_attn_mask_lim = 1;  // madnn_attn_tune(5, v): backward masks as one compare against a per-lane limit (0: per element)
-// madnn_attn_tune(6, v): dQ and dK/dV kernels start the dP accumulators at -delta (with keys 2/3 and 5 on; D = 64
-// only: backward -1..-2 % at D = 64, +8 % at D = 128, profiles/r4_ab_attn_valu_trees.log)
-int g_attn_dkdv_accd = 1;
+// madnn_attn_tune keys (A/B and the tests of the register-staged fallbacks, which serve sequence
+// lengths that are not multiples of 64 and D = 128): 7 = D = 64 dK/dV on the 3-stage LDS-DMA ring,
+// 8 = D = 64 forward on the K / V LDS-DMA ring (0: the register-staged kernels)
+int g_attn_dkdv_dma = 1;
+int g_attn_fwd_dma = 1;
 
 template <int D, bool CAUSAL>
 hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nqb = (a.S + kRowsWG - 1) / kRowsWG;
   if (D == 64 && g_attn_fwd_dma && a.S % kTile == 0) {
     hipLaunchKernelGGL((attn_fwd_dma_kernel<CAUSAL>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
-  } else if (g_attn_v2) {
-    hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, true>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
   } else {
-    hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL, false>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<D, CAUSAL>), dim3(nqb * a.B * a.H), dim3(kThreads), 0, st, a);
   }
   return hipGetLastError();
 }
@@ -1208,40 +1142,15 @@ hipError_t launch_fwd(const MadnnAttnArgs& a, hipStream_t st) {
 template <int D, bool CAUSAL>
 hipError_t launch_bwd(const MadnnAttnArgs& a, hipStream_t st) {
   const int nb = (a.S + kRowsWG - 1) / kRowsWG;
-  if (g_attn_dq_delta) {
-    if (D == 64 && g_attn_dq_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true, true, D == 64>), dim3(nb * a.B * a.H), dim3(kThreads),
-                         0, st, a);
-    } else if (g_attn_dq_u2 && g_attn_mask_lim) {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st,
-                         a);
-    } else if (g_attn_dq_u2) {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, true, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
-    }
-  } else {
-    const int64_t lanes = (int64_t)a.B * a.S * a.H * (D / 8);
-    hipLaunchKernelGGL((attn_bwd_delta_kernel<D>), dim3((lanes + 255) / 256), dim3(256), 0, st, a);
-    MADNN_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL, false, false>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
-  }
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, CAUSAL>), dim3(nb * a.B * a.H), dim3(kThreads), 0, st, a);
   MADNN_HIP_CHECK(hipGetLastError());
   if (D == 64 && g_attn_dkdv_dma && a.S % kTile == 0) {
     hipLaunchKernelGGL((attn_bwd_dkdv_dma_kernel<CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
-  } else if (D == 64 && g_attn_bwd_u2 && g_attn_mask_lim && g_attn_dkdv_accd) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true, D == 64>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0,
-                       st, a);
-  } else if (g_attn_bwd_u2 && g_attn_mask_lim) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
-  } else if (g_attn_bwd_u2) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, true>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL, false>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, CAUSAL>), dim3(nb * a.B * a.Hkv), dim3(kThreads), 0, st, a);
   }
   return hipGetLastError();
 }
-
 
 }  // namespace attn
 }  // namespace madnn
@@ -1252,12 +1161,9 @@ extern "C" {
 
 int madnn_attn_supported(int D) { return D == 64 || D == 128; }
 
-// A/B knobs: key 0 = forward version (1 = V2, 0 = V1), key 1 = delta in the dQ kernel (1) or its own pass (0),
-// key 2 / 3 = dK/dV / dQ loop unrolled by two (1) or not (0), key 5 = backward masks against a per-lane limit,
-// key 6 = dP accumulators started at -delta;
-// returns the previous value
+// knob keys 7 / 8 (see g_attn_dkdv_dma); returns the previous value, -1 for an unknown key
 int madnn_attn_tune(int key, int value) {
-  int* slot = key == 0 ? &g_attn_v2 : key == 1 ? &g_attn_dq_delta : key == 2 ? &g_attn_bwd_u2 : key == 3 ? &g_attn_dq_u2 : key == 5 ? &g_attn_mask_lim : key == 6 ? &g_attn_dkdv_accd : key == 7 ? &g_attn_dkdv_dma : key == 8 ? &g_attn_fwd_dma : nullptr;
+  int* slot = key == 7 ? &g_attn_dkdv_dma : key == 8 ? &g_attn_fwd_dma : nullptr;
   if (slot == nullptr) return -1;
   const int old = *slot;
   *slot = value ? 1 : 0;

@@ -129,13 +129,13 @@ def test_qkv_bias_grad_from_attention_colsum(cuda, monkeypatch, H, HKV, D, S):
     assert _rel(b.grad, bf.grad) < 2e-2 and _rel(w.grad, wf.grad) < 2e-2 and _rel(x.grad, xf.grad) < 2e-2
 
 
-# the A/B variants kept behind madnn_attn_tune (attn.hip): key -> the non-default value tested
-_VARIANTS = [(0, 0), (1, 0), (2, 0), (3, 0), (5, 0), (6, 1)]
+# madnn_attn_tune keys (attn.hip): 7 = dK/dV on the LDS-DMA ring, 8 = forward on it; value 0 forces the
+# register-staged kernels that otherwise serve only ragged lengths and D = 128
+_VARIANTS = [(7, 0), (8, 0)]
 
 
 @pytest.mark.parametrize("key,value", _VARIANTS)
-@pytest.mark.parametrize("B,S,H,HKV,D,causal", [(1, 200, 4, 2, 64, True), (1, 130, 2, 2, 128, False),
-                                                (1, 384, 4, 1, 128, True)])
+@pytest.mark.parametrize("B,S,H,HKV,D,causal", [(1, 256, 4, 2, 64, True), (2, 192, 2, 2, 64, False)])
 def test_attention_tunable_variants_match_reference(cuda, key, value, B, S, H, HKV, D, causal):
     import ctypes
 
@@ -160,3 +160,31 @@ def test_attention_tunable_variants_match_reference(cuda, key, value, B, S, H, H
     assert _rel(o, orf) < 1e-2
     for g, gr, name in ((q.grad, qr.grad, "dq"), (k.grad, kr.grad, "dk"), (v.grad, vr.grad, "dv")):
         assert _rel(g, gr) < 2e-2, name
+
+
+@pytest.mark.parametrize("S,D", [(512, 64), (320, 64), (384, 128)])
+@pytest.mark.parametrize("order", ["grow", "shrink"])
+def test_attention_online_softmax_rescale_branch(cuda, S, D, order):
+    """The forward's lazy rescale (a row's reference moves only when its max grows by more than the
+    slack) on inputs that force it (cdna_hip_programming.md rule 26): 'grow' multiplies the keys of
+    the second half by 6 so every row's max jumps several tiles in; 'shrink' puts the large keys
+    first, so later tiles sit far below the reference (exp2 of large negatives).  Against fp32."""
+    torch.manual_seed(5)
+    B, H = 1, 2
+    q = torch.randn(B, S, H, D, device=cuda)
+    k = torch.randn(B, S, H, D, device=cuda)
+    v = torch.randn(B, S, H, D, device=cuda)
+    big = slice(S // 2, S) if order == "grow" else slice(0, S // 2)
+    k[:, big] *= 6.0
+    q, k, v = (t.bfloat16().requires_grad_(True) for t in (q, k, v))
+    for causal in (True, False):
+        o = ops.attention(q, k, v, causal=causal)
+        do = torch.randn_like(o)
+        gq, gk, gv = torch.autograd.grad(o, (q, k, v), do)
+        qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+        orf = _ref(qr, kr, vr, causal, D ** -0.5)
+        rq, rk, rv = torch.autograd.grad(orf, (qr, kr, vr), do.float())
+        assert torch.isfinite(o.float()).all()
+        assert _rel(o, orf) < 1.5e-2, (causal, _rel(o, orf))
+        for g, gr, name in ((gq, rq, "dq"), (gk, rk, "dk"), (gv, rv, "dv")):
+            assert _rel(g, gr) < 3e-2, (causal, name, _rel(g, gr))

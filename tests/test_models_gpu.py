@@ -14,19 +14,24 @@ def _models():
 
     return {
         # head dim 64 so K8 attention runs (RoPE + grouped-query heads for Llama)
-        "gpt2": lambda: GPT2(gpt2_config("gpt2-tiny", n_embd=256, n_head=4, n_layer=2, dropout=0.0)),
+        "gpt2": lambda: GPT2(gpt2_config("gpt2-tiny", n_embd=256, n_head=4, n_layer=2, dropout=0.0,
+                                          n_positions=256)),
         "llama": lambda: Llama(llama_config("llama3-tiny", hidden=256, heads=4, kv_heads=2, intermediate=512,
                                             layers=2)),
+        # head dim 128, one KV head (the 8B model's head size)
+        "llama_d128": lambda: Llama(llama_config("llama3-tiny", hidden=512, heads=4, kv_heads=1, intermediate=512,
+                                                 layers=2)),
     }
 
 
-@pytest.mark.parametrize("name", ["gpt2", "llama"])
-def test_causal_lm_does_not_see_the_future(cuda, name):
+@pytest.mark.parametrize("seq", [96, 192])   # ragged key tiles / whole 64-key tiles (DMA-ring forward)
+@pytest.mark.parametrize("name", ["gpt2", "llama", "llama_d128"])
+def test_causal_lm_does_not_see_the_future(cuda, name, seq):
     torch.manual_seed(0)
     model = _models()[name]().to(cuda).bfloat16().eval()
     vocab = model.config.vocab_size
-    ids = torch.randint(0, vocab, (2, 96), device=cuda)
-    t = 70
+    ids = torch.randint(0, vocab, (2, seq), device=cuda)
+    t = seq * 3 // 4 - 2
     ids2 = ids.clone()
     ids2[:, t:] = (ids2[:, t:] + 1 + torch.randint(0, vocab - 1, ids2[:, t:].shape, device=cuda)) % vocab
     with torch.no_grad():
@@ -35,7 +40,7 @@ def test_causal_lm_does_not_see_the_future(cuda, name):
     assert (a[:, t:] - b[:, t:]).abs().max().item() > 1e-2
 
 
-@pytest.mark.parametrize("name", ["gpt2", "llama"])
+@pytest.mark.parametrize("name", ["gpt2", "llama", "llama_d128"])
 def test_fused_lm_loss_is_shifted_cross_entropy(cuda, name):
     torch.manual_seed(1)
     model = _models()[name]().to(cuda).bfloat16()

@@ -842,3 +842,18 @@ def test_gelu_mlp_autograd_node_matches_eager():
     torch.testing.assert_close(y, ref_y)
     for a, b in zip(got, ref):
         torch.testing.assert_close(a, b)
+
+
+def test_position_embedding_models_refuse_long_sequences():
+    """GPT-2 / BERT refuse a sequence longer than their position table on the host (on the GPU the
+    out-of-range gather would fault the device instead of raising)."""
+    import pytest
+    from madnn.models.bert import BertForPreTraining, bert_config
+    from madnn.models.gpt2 import GPT2, gpt2_config
+
+    g = GPT2(gpt2_config("gpt2-tiny"))
+    with pytest.raises(ValueError, match="n_positions"):
+        g(torch.zeros(1, 129, dtype=torch.long))
+    b = BertForPreTraining(bert_config("bert-tiny"))
+    with pytest.raises(ValueError, match="max_position"):
+        b(torch.zeros(1, 129, dtype=torch.long))
