@@ -107,7 +107,6 @@ hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const vo
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
 int madnn_wgrad_splits(int64_t, int64_t, int64_t);
-int madnn_gemm_tune(int, int);
 hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
                               hipStream_t);
 int madnn_gemmp_supported(int64_t, int64_t, int64_t, int);

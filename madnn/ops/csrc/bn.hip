@@ -53,7 +53,6 @@ struct BnTune {
   int reverse = 1;
   int wg_per_cu = 3;
   int hoist = 1;
-  int unroll = 0;  // 1 / 2: apply walks handle two / four chunks per trip (more loads in flight)
   int partials_per_cu = 2;  // reduction passes (statistics, backward sums): workgroups = partial rows per CU
   //                            (ResNet-50 b512, profiles/r4_ab_bn_partials_*: 1 -1.8 %, 4 -0.5 % against 2)
 };
@@ -61,12 +60,9 @@ inline BnTune& bn_tune() {
   static BnTune t;
   return t;
 }
-// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting, bit 2 two
-// chunks per trip, bit 3 four chunks per trip
-inline int bn_walk_flags() {
-  const int u = bn_tune().unroll;
-  return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2) | (u == 1 ? 4 : u >= 2 ? 8 : 0);
-}
+// walk flags passed to the apply kernels: bit 0 reverse, bit 1 no coefficient hoisting (two / four
+// chunks per trip were measured slower at every launch shape and removed)
+inline int bn_walk_flags() { return (bn_tune().reverse ? 1 : 0) | (bn_tune().hoist ? 0 : 2); }
 
 // grid-stride walk of [0, total) in 8-element lane chunks, forward or back-to-front; c0 tracks
 // the channel of the chunk without a 64-bit modulo per step
@@ -281,29 +277,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const void* __restrict__ 
       if (mask) mask[i >> 3] = (unsigned char)bits;
     }
   };
-  // U chunks per trip: every chunk's loads issued before the first store
-  auto trips = [&](auto uc) {
-    constexpr int U = decltype(uc)::value;
-    while (w.n >= U) {
-      int64_t ix[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ix[u] = w.i;
-        w.next();
-      }
-      float v[U][8], r[U][8];
-#pragma unroll
-      for (int u = 0; u < U; ++u) load8<XDT>(x, ix[u], v[u]);
-      if constexpr (RES) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) load8<XDT>(res, ix[u], r[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) body(ix[u], v[u], r[u]);
-    }
-  };
-  if (fixed && (reverse & 8)) trips(std::integral_constant<int, 4>{});
-  if (fixed && (reverse & 4)) trips(std::integral_constant<int, 2>{});
   for (; w.n > 0; w.next()) {
     const int64_t i = w.i;
     if (!fixed) coef(w.c0);
@@ -516,30 +489,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       if (dres != nullptr) store8<XDT>(dres, i, dv);  // null: the consumer masks dy itself (resmask)
     }
   };
-  auto trips = [&](auto uc) {  // U chunks per trip (see bn_apply_kernel)
-    constexpr int U = decltype(uc)::value;
-    while (w.n >= U) {
-      int64_t ix[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        ix[u] = w.i;
-        w.next();
-      }
-      float d[U][8], xv[U][8], q[U][8];
-#pragma unroll
-      for (int u = 0; u < U; ++u) load8<XDT>(dy, ix[u], d[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) load8<XDT>(x, ix[u], xv[u]);
-      if constexpr (RAFF) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) load8<XDT>(rin, ix[u], q[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) body(ix[u], d[u], xv[u], q[u]);
-    }
-  };
-  if (fixed && (reverse & 8)) trips(std::integral_constant<int, 4>{});
-  if (fixed && (reverse & 4)) trips(std::integral_constant<int, 2>{});
   for (; w.n > 0; w.next()) {
     const int64_t i = w.i;
     if (!fixed) coef(w.c0);
@@ -615,15 +564,13 @@ static int bn_grid_rows(int64_t M, int C) {
 extern "C" {
 
 // key 0: apply passes walk back to front (0/1), 1: apply workgroups per CU, 2: coefficient hoisting
-// (0/1), 3: apply chunks per trip (0: one, 1: two, 2: four), 4: reduction workgroups (partial rows) per
-// CU; value < 0 only reads.
+// (0/1), 4: reduction workgroups (partial rows) per CU; value < 0 only reads.
 // Key 4 sizes the partial slabs: change it only between steps (every call sizes its own workspace).
 // Returns the old value (-1 for an unknown key).
 int madnn_bn_tune(int key, int value) {
   int* f = key == 0   ? &madnn::bn_tune().reverse
            : key == 1 ? &madnn::bn_tune().wg_per_cu
            : key == 2 ? &madnn::bn_tune().hoist
-           : key == 3 ? &madnn::bn_tune().unroll
            : key == 4 ? &madnn::bn_tune().partials_per_cu
                       : nullptr;
   if (f == nullptr) return -1;
@@ -631,7 +578,6 @@ int madnn_bn_tune(int key, int value) {
   if (value >= 0)
     *f = key == 1 ? (value < 1 ? 1 : value)
          : key == 4 ? (value < 1 ? 1 : value > 8 ? 8 : value)
-         : key == 3 ? (value > 2 ? 2 : value)
                     : (value != 0);
   return old;
 }

@@ -23,14 +23,14 @@
 // output row (the same orientation as K9, conv.hip).
 //
 // Geometry: 8 waves = 2 groups (wr: i half of the tile) x 4 (wc: 64-column j quarter);
-// each wave owns a 128 x 64 block of D = 4 x 2 v_mfma_f32_32x32x16_bf16 accumulators
+// each wave owns a 128 x 64 block of D = 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators
 // (128 VGPRs).  K steps of 64.  LDS = 2 stages x 4 half-tiles (A i-half 0/1, B j-half 0/1)
 // of 128 x 64 bf16 = 128 KiB, one workgroup per CU.
 //
 // Schedule (per K tile: 4 phases, one per 64x32 quadrant of the wave block):
 //   phase q: LOAD  = ds_read this quadrant's new fragments + issue one half-tile of DMA
 //            s_barrier
-//            MFMA  = 8 MFMAs (setprio 1)
+//            MFMA  = 16 MFMAs (setprio 1)
 //            s_barrier
 //   Q0 reads A(i 0..63) + B(j 0..31), Q1 B(j 32..63), Q2 A(i 64..127), Q3 nothing.
 //   Group 1 issues one extra barrier first, so its LOAD segments coincide with group 0's MFMA
@@ -75,16 +75,7 @@ struct Args {
   int64_t kper;         // reduction elements per split (multiple of kBK)
 };
 
-template <bool COL>
-__device__ __forceinline__ bf16x8 frag(const uint16_t* tile, int s, int x, int lane) {
-  if constexpr (COL) {
-    return lds_col<128>(tile, 16 * s, x, lane);
-  } else {
-    return lds_row(tile, x + (lane & 31), 2 * s + (lane >> 5));
-  }
-}
-
-template <bool A_COL, bool B_COL, bool M16>
+template <bool A_COL, bool B_COL>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[kLds];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
@@ -114,8 +105,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     const int inst = 2 * wave + e;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      off[h][e] = dma_offset<A_COL, M16>(inst, lane, p.lda, i0 + 128 * h, p.I);
-      off[2 + h][e] = dma_offset<B_COL, M16>(inst, lane, p.ldb, j0 + 128 * h, p.J);
+      off[h][e] = dma_offset<A_COL>(inst, lane, p.lda, i0 + 128 * h, p.I);
+      off[2 + h][e] = dma_offset<B_COL>(inst, lane, p.ldb, j0 + 128 * h, p.J);
     }
   }
   // issue half-tile H: 2 DMA instructions per lane into stage (H/4)&1; H%4 = 0,1: B halves,
@@ -144,21 +135,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
     }
   };
 
-  // accumulators: 32x32x16 -> acc[4 i-blocks of 32][2 j-blocks of 32] (f32x16);
-  //               16x16x32 -> ac4[8 i-blocks of 16][4 j-blocks of 16] (f32x4); 128 VGPRs either way
-  f32x16 acc[M16 ? 1 : 4][M16 ? 1 : 2];
-  f32x4 ac4[M16 ? 8 : 1][M16 ? 4 : 1];
-  if constexpr (!M16) {
+  // accumulators: ac4[8 i-blocks of 16][4 j-blocks of 16] of v_mfma_f32_16x16x32_bf16 (128 VGPRs)
+  // (a 32x32x16 variant with the same schedule measured 6-12 % slower at every GPT-2 / square shape,
+  // profiles/r5_gemm_ab_b128_asm_dma.json "k12m32", and was removed)
+  f32x4 ac4[8][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < 8; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
-  } else {
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) ac4[a][b] = zero4();
-  }
+    for (int b = 0; b < 4; ++b) ac4[a][b] = zero4();
 
   // prologue: half-tiles 0..5 (K tile 0 + the B halves of K tile 1)
 #pragma unroll
@@ -174,8 +158,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
 
   bf16x8 af[2][4], bf0[4], bf1[4];
   const int bcol = (wc & 1) * 64;
-  if constexpr (M16) {
-    // same 4-phase schedule, 16 MFMAs per phase: af[a][s] = i-block a (of 4) x k-step s (of 2),
+  {
+    // 4-phase schedule, 16 MFMAs per phase: af[a][s] = i-block a (of 4) x k-step s (of 2),
     // bf0 / bf1 [c][s] = j-blocks 0,1 / 2,3 of the wave's 64 columns
     for (int t = 0; t < nk; ++t) {
       const uint16_t* sa = smem + (t & 1) * kStage + wr * kHalf;
@@ -259,93 +243,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
       barrier();
     }
   }
-  if constexpr (!M16) {
-  for (int t = 0; t < nk; ++t) {
-    const uint16_t* sa = smem + (t & 1) * kStage + wr * kHalf;
-    const uint16_t* sb = smem + (t & 1) * kStage + (2 + (wc >> 1)) * kHalf;
-    const int P = 4 * t;
-    // ---- Q0: A rows 0..63, B cols 0..31
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf0[s] = frag<B_COL>(sb, s, bcol, lane);
-#pragma unroll
-      for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, a * 32, lane);
-    }
-    if (P + 6 < total) stage(P + 6);
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) acc[a][0] = mfma(af[a][s], bf0[s], acc[a][0]);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---- Q1: B cols 32..63
-#pragma unroll
-    for (int s = 0; s < 4; ++s) bf1[s] = frag<B_COL>(sb, s, bcol + 32, lane);
-    if (P + 7 < total) stage(P + 7);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the B half-tiles' last reads
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) acc[a][1] = mfma(af[a][s], bf1[s], acc[a][1]);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---- Q2: A rows 64..127 (the stage's last reads: retire them before the barrier)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) af[a][s] = frag<A_COL>(sa, s, 64 + a * 32, lane);
-    if (P + 8 < total) stage(P + 8);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the A half-tiles' last reads
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) acc[2 + a][1] = mfma(af[a][s], bf1[s], acc[2 + a][1]);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-    // ---- Q3: no reads; retire K tile t+1's DMA (the B halves of K tile t+2 stay in flight)
-    if (P + 9 < total) {
-      stage(P + 9);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else if (P + 8 < total) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int a = 0; a < 2; ++a) acc[2 + a][0] = mfma(af[a][s], bf0[s], acc[2 + a][0]);
-    __builtin_amdgcn_s_setprio(0);
-    barrier();
-  }
-  }  // !M16
   if (wr == 0) barrier();  // balance the stagger: every wave has now passed the same barriers
 
   // every lane owns groups of 4 consecutive i of one j: visit them as (il, jl, v[4])
   auto for_each_group = [&](auto&& fn) {
-    if constexpr (!M16) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 8; ++a)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-            fn(wr * 128 + a * 32 + 8 * g + 4 * hh, wc * 64 + b * 32 + l32,
-               f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]});
-    } else {
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) fn(wr * 128 + a * 16 + 4 * (lane >> 4), wc * 64 + b * 16 + (lane & 15), ac4[a][b]);
-    }
+      for (int b = 0; b < 4; ++b) fn(wr * 128 + a * 16 + 4 * (lane >> 4), wc * 64 + b * 16 + (lane & 15), ac4[a][b]);
   };
 
   if (p.ws != nullptr) {
@@ -445,8 +350,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
-int g_mfma16 = 1;  // K12 MFMA shape: 1 = 16x16x32 (default), 0 = 32x32x16 (madnn_gemm_tune(0, v))
-
 template <bool A_COL, bool B_COL>
 hipError_t launch(Args& p, hipStream_t s) {
   p.i_tiles = (int)((p.I + kT - 1) / kT);
@@ -455,11 +358,7 @@ hipError_t launch(Args& p, hipStream_t s) {
   if (p.kper <= 0) p.kper = p.K;
   const int64_t grid = (int64_t)p.i_tiles * p.j_tiles * p.splits;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  if (g_mfma16) {
-    hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, true>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
-  } else {
-    hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, false>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
-  }
+  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
 }
 
@@ -469,16 +368,6 @@ hipError_t launch(Args& p, hipStream_t s) {
 using namespace madnn::gemm;
 
 extern "C" {
-
-// Tunables: key 0 = MFMA shape (1: 16x16x32, 0: 32x32x16).  Returns the previous value.
-int madnn_gemm_tune(int key, int value) {
-  if (key == 0) {
-    const int old = g_mfma16;
-    g_mfma16 = value ? 1 : 0;
-    return old;
-  }
-  return -1;
-}
 
 // Shapes K12 takes: reduction % 64 == 0, output features % 8 == 0, 16-B aligned rows, and
 // 32-bit-safe per-lane DMA offsets.

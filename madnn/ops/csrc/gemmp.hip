@@ -107,14 +107,14 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
   // per-lane DMA offsets: tiles never clamp here (I, J multiples of 256), so they are tile-free;
   // 32-bit (madnn_gemmp_supported bounds them): 8 VGPRs instead of 16
   // named scalars, selected with ?: (an indexed register array goes to scratch: guide rule 20)
-  const int o00 = (int)dma_offset<A_COL, true>(2 * wave, lane, p.lda, 0, (int64_t)1 << 40);
-  const int o01 = (int)dma_offset<A_COL, true>(2 * wave + 1, lane, p.lda, 0, (int64_t)1 << 40);
-  const int o10 = (int)dma_offset<A_COL, true>(2 * wave, lane, p.lda, 128, (int64_t)1 << 40);
-  const int o11 = (int)dma_offset<A_COL, true>(2 * wave + 1, lane, p.lda, 128, (int64_t)1 << 40);
-  const int o20 = (int)dma_offset<B_COL, true>(2 * wave, lane, p.ldb, 0, (int64_t)1 << 40);
-  const int o21 = (int)dma_offset<B_COL, true>(2 * wave + 1, lane, p.ldb, 0, (int64_t)1 << 40);
-  const int o30 = (int)dma_offset<B_COL, true>(2 * wave, lane, p.ldb, 128, (int64_t)1 << 40);
-  const int o31 = (int)dma_offset<B_COL, true>(2 * wave + 1, lane, p.ldb, 128, (int64_t)1 << 40);
+  const int o00 = (int)dma_offset<A_COL>(2 * wave, lane, p.lda, 0, (int64_t)1 << 40);
+  const int o01 = (int)dma_offset<A_COL>(2 * wave + 1, lane, p.lda, 0, (int64_t)1 << 40);
+  const int o10 = (int)dma_offset<A_COL>(2 * wave, lane, p.lda, 128, (int64_t)1 << 40);
+  const int o11 = (int)dma_offset<A_COL>(2 * wave + 1, lane, p.lda, 128, (int64_t)1 << 40);
+  const int o20 = (int)dma_offset<B_COL>(2 * wave, lane, p.ldb, 0, (int64_t)1 << 40);
+  const int o21 = (int)dma_offset<B_COL>(2 * wave + 1, lane, p.ldb, 0, (int64_t)1 << 40);
+  const int o30 = (int)dma_offset<B_COL>(2 * wave, lane, p.ldb, 128, (int64_t)1 << 40);
+  const int o31 = (int)dma_offset<B_COL>(2 * wave + 1, lane, p.ldb, 128, (int64_t)1 << 40);
 
   // kernel-argument fields as scalars: lambdas capturing the argument struct by reference make
   // hipcc spill it to scratch

@@ -35,12 +35,12 @@ __device__ __forceinline__ void barrier() {
 // (measured: SQ_LDS_BANK_CONFLICT 1.6e8 cycles on the forward, 0 on the all-transposed wgrad).
 __device__ __forceinline__ int swz16(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 6)); }
 
-template <bool COL, bool M16>
+template <bool COL>
 __device__ __forceinline__ int64_t dma_offset(int inst, int lane, int64_t ld, int64_t first, int64_t lim) {
   if constexpr (!COL) {
     // [128 rows][64 k], 128-B rows: LDS slot s of row r holds chunk s ^ f(r) (swz16 / swz<64>)
     const int r = inst * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ (M16 ? (r & 6) : ((((r >> 1) & 1) << 2) | ((r >> 2) & 3)));
+    const int ch = (lane & 7) ^ (r & 6);
     int64_t row = first + r;
     row = row < lim ? row : lim - 1;
     return (row - first) * ld + 8 * ch;

@@ -187,10 +187,10 @@ __global__ __launch_bounds__(kNormThreads) void norm_fwd_kernel(
 // CS: also partial[blk][2H:3H] = sum_rows dx (the written input gradient, residual included): the
 // bias gradient of the Linear that produced this norm's input (the transformer residual stream),
 // so that Linear's backward needs no column-sum pass of its own (ops._LinearFn, `_madnn_colsum`).
-// EARLY: the weight is loaded once per lane (its columns never change across the grid-stride
-// rows) and the next row's x, dy, residual gradient and statistics are loaded before this row's
-// reductions, so their latency hides under them instead of following them (A/B: madnn_norm_tune key 2).
-template <int XDT, int WDT, int TPR, int NC, bool EARLY, bool CS>
+// The weight is loaded once per lane (its columns never change across the grid-stride rows) and
+// the next row's x, dy, residual gradient and statistics are loaded before this row's reductions, so
+// their latency hides under them instead of following them.
+template <int XDT, int WDT, int TPR, int NC, bool CS>
 __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const void* __restrict__ dres,
@@ -212,23 +212,21 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) ds[c][j] = 0.f;
   }
-  float wk[EARLY ? NC : 1][8];
-  if constexpr (EARLY) {
+  float wk[NC][8];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int col = c * TPR * 8 + t * 8;
-      if (col < H) {
-        load8<WDT>(w, col, wk[c]);
-      } else {
+  for (int c = 0; c < NC; ++c) {
+    const int col = c * TPR * 8 + t * 8;
+    if (col < H) {
+      load8<WDT>(w, col, wk[c]);
+    } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) wk[c][j] = 0.f;
-      }
+      for (int j = 0; j < 8; ++j) wk[c][j] = 0.f;
     }
   }
 
-  // EARLY: the next row's x / dy / residual gradient / statistics are loaded into these before the
+  // the next row's x / dy / residual gradient / statistics are loaded into these before the
   // current row's reductions (as in the forward), so a wave always has a row of loads in flight
-  constexpr int NP = EARLY ? NC : 1;
+  constexpr int NP = NC;
   Raw8<XDT> px[NP], pg[NP], pr[NP];
   float pmean = 0.f, prstd = 0.f;
 #pragma unroll
@@ -239,19 +237,17 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
   }
   const int64_t rstep = (int64_t)gridDim.x * RPB;
   auto fetch = [&](int64_t r) {
-    if constexpr (EARLY) {
-      if (r < rows) {
-        pmean = rms ? 0.f : mean_in[r];
-        prstd = rstd_in[r];
-      }
+    if (r < rows) {
+      pmean = rms ? 0.f : mean_in[r];
+      prstd = rstd_in[r];
+    }
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int col = c * TPR * 8 + t * 8;
-        if (r < rows && col < H) {
-          px[c].load(x, r * H + col);
-          pg[c].load(dy, r * H + col);
-          if (dres) pr[c].load(dres, r * H + col);
-        }
+    for (int c = 0; c < NC; ++c) {
+      const int col = c * TPR * 8 + t * 8;
+      if (r < rows && col < H) {
+        px[c].load(x, r * H + col);
+        pg[c].load(dy, r * H + col);
+        if (dres) pr[c].load(dres, r * H + col);
       }
     }
   };
@@ -260,39 +256,28 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
     const int64_t row = row0 + sub;
     const bool live = row < rows;
     float mean, rstd;
-    float xh[NC][8], wdy[NC][8], rv[EARLY ? NC : 1][8];
+    float xh[NC][8], wdy[NC][8], rv[NC][8];
     float xcur[NP][8], gcur[NP][8];
-    if constexpr (EARLY) {
-      mean = live ? pmean : 0.f;
-      rstd = live ? prstd : 0.f;
+    mean = live ? pmean : 0.f;
+    rstd = live ? prstd : 0.f;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        px[c].unpack(xcur[c]);
-        pg[c].unpack(gcur[c]);
-        if (dres) pr[c].unpack(rv[c]);
-      }
-      fetch(row + rstep);  // the next row's loads fly under this row's math and reductions
-    } else {
-      mean = (live && !rms) ? mean_in[row] : 0.f;
-      rstd = live ? rstd_in[row] : 0.f;
+    for (int c = 0; c < NC; ++c) {
+      px[c].unpack(xcur[c]);
+      pg[c].unpack(gcur[c]);
+      if (dres) pr[c].unpack(rv[c]);
     }
+    fetch(row + rstep);  // the next row's loads fly under this row's math and reductions
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int col = c * TPR * 8 + t * 8;
       if (live && col < H) {
         float xv[8], gv[8], wv[8];
-        if constexpr (EARLY) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            xv[j] = xcur[c][j];
-            gv[j] = gcur[c][j];
-            wv[j] = wk[c][j];
-          }
-        } else {
-          load8<XDT>(x, row * H + col, xv);
-          load8<XDT>(dy, row * H + col, gv);
-          load8<WDT>(w, col, wv);
+        for (int j = 0; j < 8; ++j) {
+          xv[j] = xcur[c][j];
+          gv[j] = gcur[c][j];
+          wv[j] = wk[c][j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -319,15 +304,8 @@ __global__ __launch_bounds__(kNormThreads) void norm_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (wdy[c][j] - c2 - xh[c][j] * c1);
         if (dres) {
-          if constexpr (EARLY) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] += rv[c][j];
-          } else {
-            float r[8];
-            load8<XDT>(dres, row * H + col, r);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] += r[j];
-          }
+          for (int j = 0; j < 8; ++j) o[j] += rv[c][j];
         }
         store8<XDT>(dx, row * H + col, o);
         if constexpr (CS) {
@@ -458,15 +436,15 @@ static NormCfg pick_cfg(int H) {
 // backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
 // (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
 // +0.5 % over 16 (4: -0.1 %)
-static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4, g_norm_bwd_early = 1;
+static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4;
 
 extern "C" {
 
 int madnn_norm_tune(int key, int value) {
-  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : key == 2 ? &g_norm_bwd_early : nullptr;
+  int* f = key == 0 ? &g_norm_fwd_wg : key == 1 ? &g_norm_bwd_wg : nullptr;
   if (f == nullptr) return -1;
   const int old = *f;
-  if (value > 0 || key == 2) *f = value;
+  if (value > 0) *f = value;
   return old;
 }
 
@@ -517,14 +495,11 @@ hipError_t madnn_norm_bwd(const void* dy, const void* x, const void* w, const fl
       constexpr int RPB = kNormThreads / TPR;
       const size_t lds = RPB > 1 ? (size_t)RPB * ns * NC * TPR * 8 * sizeof(float) : 0;
       if (dsum != nullptr) {
-        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true, true>), dim3(G), dim3(kNormThreads), lds, stream,
-                           dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
-      } else if (g_norm_bwd_early) {
-        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true, false>), dim3(G), dim3(kNormThreads), lds, stream,
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, true>), dim3(G), dim3(kNormThreads), lds, stream,
                            dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
       } else {
-        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, false, false>), dim3(G), dim3(kNormThreads), lds,
-                           stream, dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
+        hipLaunchKernelGGL((norm_bwd_kernel<XDT, WDT, TPR, NC, false>), dim3(G), dim3(kNormThreads), lds, stream,
+                           dy, x, w, mean_in, rstd_in, dres, dx, workspace, rows, H, rms, has_bias);
       }
       MADNN_HIP_CHECK(hipGetLastError());
       const int fgrid = ((dsum != nullptr ? 3 * H : (has_bias ? 2 * H : H)) + 31) / 32;

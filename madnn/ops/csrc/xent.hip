@@ -160,10 +160,11 @@ __device__ __forceinline__ float h2f(unsigned short u) {
   return XDT == kBF16 ? bf16_to_f32(u) : f16_to_f32(u);
 }
 
-// FX: v_exp_f32 directly (exp2f adds a denormal range reduction: the result is < 2^-126 of the row max
-// only where it cannot matter to the sum) and the vocabulary-end test once per 8-element chunk instead
-// of per element (A/B knob madnn_xent_tune key 0)
-template <int XDT, int CH, bool FX = false>
+// Whole 8-element chunks inside the vocabulary take v_exp_f32 directly (exp2f adds a denormal range
+// reduction: the result is < 2^-126 of the row max only where it cannot matter to the sum) and test the
+// vocabulary end once per chunk instead of per element (GPT-2 medium b64 step +0.32 %,
+// profiles/r4_ab_xent_fast_exp_gpt2m_b64.log); only the chunk that straddles it is tested per element
+template <int XDT, int CH>
 __global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(const void* __restrict__ logits,
                                                                       const int64_t* __restrict__ targets,
                                                                       XentRows R, const float* __restrict__ gscale,
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(const voi
   for (int k = 0; k < CH; ++k) {
     const int c = tid + k * kXentFusedThreads;
     if (c < nch) {
-      if (FX && 8 * c + 8 <= R.V) {
+      if (8 * c + 8 <= R.V) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) m = fmaxf(m, h2f<XDT>(buf[k][j]));
       } else {
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(const voi
     const int c = tid + k * kXentFusedThreads;
     if (c < nch) {
       u16x8 eb;
-      if (FX && 8 * c + 8 <= R.V) {
+      if (8 * c + 8 <= R.V) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float e = __builtin_amdgcn_exp2f(fmaf(h2f<XDT>(buf[k][j]), kLog2e, -ml));
@@ -295,15 +296,6 @@ __global__ __launch_bounds__(256) void xent_rescale_kernel(void* __restrict__ gr
 
 extern "C" {
 
-static int g_xent_fx = 1;  // GPT-2 medium b64 step +0.32 % (profiles/r4_ab_xent_fast_exp_gpt2m_b64.log)
-
-int madnn_xent_tune(int key, int value) {
-  if (key != 0) return -1;
-  const int old = g_xent_fx;
-  if (value >= 0) g_xent_fx = value != 0;
-  return old;
-}
-
 // chunks per lane the fused kernel needs for a row of ld 16-bit elements (0 = not supported)
 int madnn_xent_fused_chunks(int64_t ld) {
   if (ld % 8) return 0;
@@ -323,13 +315,9 @@ hipError_t madnn_xent_fused(const void* logits, int dt, const int64_t* targets, 
     return hipErrorInvalidValue;
   madnn::XentRows R{n_loss_rows, seq, ld, V, ignore_index};
   const dim3 grid((unsigned)n_rows_all), block(madnn::kXentFusedThreads);
-#define MADNN_XF(XDT, CH)                                                                                        \
-  if (g_xent_fx)                                                                                                 \
-    hipLaunchKernelGGL((madnn::xent_fused_kernel<XDT, CH, true>), grid, block, 0, stream, logits, targets, R, gscale, \
-                       loss, grad);                                                                              \
-  else                                                                                                           \
-    hipLaunchKernelGGL((madnn::xent_fused_kernel<XDT, CH>), grid, block, 0, stream, logits, targets, R, gscale, loss, \
-                       grad)
+#define MADNN_XF(XDT, CH)                                                                                         \
+  hipLaunchKernelGGL((madnn::xent_fused_kernel<XDT, CH>), grid, block, 0, stream, logits, targets, R, gscale, loss, \
+                     grad)
 #define MADNN_XF_CH(XDT)                  \
   switch (ch) {                           \
     case 4: MADNN_XF(XDT, 4); break;      \

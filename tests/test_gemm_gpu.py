@@ -17,22 +17,6 @@ def _ops():
     return torch.ops.madnn
 
 
-@pytest.fixture(autouse=True, params=[16, 32], ids=["mfma16x16x32", "mfma32x32x16"])
-def mfma_shape(request):
-    """Every K12 test runs on both MFMA shapes of the kernel (madnn_gemm_tune key 0)."""
-    import ctypes
-
-    from madnn import ops
-
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    assert ops.load_kernels()
-    lib = ctypes.CDLL(str(ops.kernels_path()))
-    old = lib.madnn_gemm_tune(0, 1 if request.param == 16 else 0)
-    yield request.param
-    lib.madnn_gemm_tune(0, old)
-
-
 def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
