@@ -64,7 +64,6 @@ def _flags_kernels():
         "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
         "-DHIP_ENABLE_WARP_SYNC_BUILTINS=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
         "-DTORCH_EXTENSION_NAME=_madnn_kernels", "-Wno-unused-result",
-        "-munsafe-fp-atomics",
     ]
     flags += [f"-I{p}" for p in inc]
     flags += [f"-I{sysconfig.get_paths()['include']}", f"-I{CSRC}"]

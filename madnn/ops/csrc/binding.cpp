@@ -82,7 +82,8 @@ hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int
                                const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr,
                                const unsigned char* = nullptr, int = 0, int = 0);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
-hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, int64_t, int64_t, int64_t, const float*, const float*,
+int64_t madnn_conv1x1_wgrad_ws(int64_t, int64_t, int64_t);
+hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
 hipError_t madnn_bn_coef(const void*, int64_t, int, float, float, const float*, const float*, float*, float*, int64_t*,
                          float*, float*, float*, float*, float*, const float*, int, hipStream_t);
@@ -722,8 +723,11 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::o
   TORCH_CHECK(conv_rows(dy, cout, "dy") == M && dy.dim() == x.dim(), "conv1x1_wgrad: dy / x pixel mismatch");
   TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  at::Tensor dw = at::zeros({cout, cin}, x.options().dtype(at::kFloat));
-  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), M, cin, cout, sc, sh, cur_stream(x)),
+  at::Tensor dw = at::empty({cout, cin}, x.options().dtype(at::kFloat));
+  const int64_t wsn = madnn_conv1x1_wgrad_ws(M, cin, cout);
+  at::Tensor ws = at::empty({wsn > 0 ? wsn : 1}, x.options().dtype(at::kFloat));
+  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), wsn > 0 ? ws.data_ptr<float>() : nullptr,
+                            M, cin, cout, sc, sh, cur_stream(x)),
         "conv1x1_wgrad");
   return dw;
 }

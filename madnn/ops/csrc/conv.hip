@@ -18,9 +18,10 @@
 //   forward : i = co (A = W, row),     j = m  (B = X, row)    -> Y[j][i]
 //   dgrad   : i = ci (A = W, column),  j = m  (B = dY, row)   -> dX[j][i]
 //   wgrad   : i = co (A = dY, column), j = ci (B = X, column), the m reduction split over
-//             workgroups, partial sums added with fp32 atomics (one accumulator register
-//             = two 128-B row segments per wave instruction: the full-rate atomic shape,
-//             MI355X_MICROARCH.md "Global float atomics").
+//             workgroups; each split stores its fp32 partial [Cout][Cin] slab (one accumulator
+//             register = two 128-B row segments per wave instruction) and one streaming pass sums
+//             the slabs in split order -- deterministic, unlike float atomics (no -munsafe-fp-atomics
+//             result that depends on arrival order).
 // In the store epilogue a lane owns 4 consecutive i of one j: one 8-byte store.
 //
 // CDNA4 mapping: v_mfma_f32_32x32x16_bf16; 4 waves per workgroup, each owning a 64x64
@@ -63,7 +64,7 @@ inline Tune& tune() {
   return t;
 }
 
-enum Mode : int { kStoreT = 0, kAtomic = 1 };
+enum Mode : int { kStoreT = 0, kSplit = 1 };
 
 struct GemmArgs {
   const uint16_t* a;
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   const int64_t i0 = (int64_t)it * BI;
   const int nk = (int)((p.K + kBK - 1) / kBK);
   int jt, kbeg, kend, jstride;
-  if constexpr (MODE == kAtomic) {  // one j tile, k steps [kbeg, kend)
+  if constexpr (MODE == kSplit) {  // one j tile, k steps [kbeg, kend)
     jt = grp % p.j_tiles;
     kbeg = (grp / p.j_tiles) * p.k_chunk;
     kend = min(kbeg + p.k_chunk, nk);
@@ -364,8 +365,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
           }
         }
       } else {
+        // this split's partial slab (split = grp / j_tiles)
         const int64_t jw = (int64_t)jt * BJ + wj * NJ * 32 + l32;
-        float* out = static_cast<float*>(p.out);
+        float* out = static_cast<float*>(p.out) + (int64_t)(grp / p.j_tiles) * p.I * p.ldo;
 #pragma unroll
         for (int a = 0; a < NI; ++a)
 #pragma unroll
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
               const int64_t i = i0 + (wi * NI + a) * 32 + acc_row(r, hh);
-              atomicAdd(out + i * p.ldo + jw + b * 32, acc[a][b][r]);
+              out[i * p.ldo + jw + b * 32] = acc[a][b][r];
             }
       }
 #pragma unroll
@@ -424,6 +426,30 @@ inline void plan_persistent(GemmArgs& p, int64_t J, int BI, int64_t I, int64_t K
   const int64_t per = K >= 8 * kBK ? 1 : (total + tune().fwd_wg - 1) / tune().fwd_wg;
   p.j_groups = (int)((p.j_tiles + per - 1) / per);
   p.k_chunk = 0;
+}
+
+// dw[i] = sum over splits of slab[s][i], in split order (deterministic); n % 4 == 0
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n,
+                                                           float* __restrict__ dw) {
+  const int64_t n4 = n / 4;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
+    f32x4 acc = reinterpret_cast<const f32x4*>(slab)[v];
+    for (int s = 1; s < splits; ++s) acc += reinterpret_cast<const f32x4*>(slab + (int64_t)s * n)[v];
+    reinterpret_cast<f32x4*>(dw)[v] = acc;
+  }
+}
+
+// workgroup tiles and m splits of the weight gradient (shared by the launcher and the workspace size)
+inline void wgrad_split(int64_t M, int64_t cin, int64_t cout, int& bi, int& bj, int64_t& tiles, int& k_chunk,
+                        int64_t& splits) {
+  bi = cout % 128 == 0 ? 128 : 64;
+  bj = cin % 128 == 0 ? 128 : 64;
+  tiles = (cout / bi) * (cin / bj);
+  const int64_t nk = (M + kBK - 1) / kBK;
+  splits = (tune().wgrad_wg + tiles - 1) / tiles;
+  splits = splits < 1 ? 1 : (splits > nk ? nk : splits);
+  k_chunk = (int)((nk + splits - 1) / splits);
+  splits = (nk + k_chunk - 1) / k_chunk;
 }
 
 }  // namespace conv
@@ -551,18 +577,26 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
               : launch<true, false, 64, 128, kStoreT, false>(p, grid, s);
 }
 
-// dw: zero-initialised fp32 [cout][cin]; partial sums over m are added atomically
-// bsc/bsh (optional): x is convolved as relu(x * bsc + bsh), as in madnn_conv1x1_fwd
-hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t M, int64_t cin, int64_t cout,
-                               const float* bsc, const float* bsh, hipStream_t s) {
+// fp32 floats of workspace madnn_conv1x1_wgrad needs (0: one split, written straight to dw)
+int64_t madnn_conv1x1_wgrad_ws(int64_t M, int64_t cin, int64_t cout) {
+  int bi, bj, kc;
+  int64_t tiles, splits;
+  wgrad_split(M, cin, cout, bi, bj, tiles, kc, splits);
+  return splits > 1 ? splits * cin * cout : 0;
+}
+
+// dw: fp32 [cout][cin]; ws: madnn_conv1x1_wgrad_ws floats (the per-split partial slabs, summed in
+// split order into dw).  bsc/bsh (optional): x is convolved as relu(x * bsc + bsh), as in
+// madnn_conv1x1_fwd
+hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, float* ws, int64_t M, int64_t cin,
+                               int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
-  if (M <= 0) return hipSuccess;
+  if (M <= 0) return hipMemsetAsync(dw, 0, (size_t)(cin * cout) * sizeof(float), s);
   GemmArgs p{};
   p.a = static_cast<const uint16_t*>(dy);  // A[i = co][k = m] = dY[m][co]: column memory
   p.lda = cout;
   p.b = static_cast<const uint16_t*>(x);  // B[k = m][j = ci] = X[m][ci]: column memory
   p.ldb = cin;
-  p.out = dw;
   p.bsc = bsc;
   p.bsh = bsh;
   p.xcd = tune().xcd;
@@ -570,28 +604,34 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, int64_t
   p.I = cout;
   p.J = cin;
   p.K = M;
-  const int bi = cout % 128 == 0 ? 128 : 64, bj = cin % 128 == 0 ? 128 : 64;
+  int bi, bj;
+  int64_t tiles, splits;
+  wgrad_split(M, cin, cout, bi, bj, tiles, p.k_chunk, splits);
+  if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
+  p.out = splits > 1 ? ws : dw;
   p.i_tiles = (int)(cout / bi);
   p.j_tiles = (int)(cin / bj);
-  const int64_t nk = (M + kBK - 1) / kBK;
-  const int64_t tiles = (int64_t)p.i_tiles * p.j_tiles;
-  int64_t splits = (tune().wgrad_wg + tiles - 1) / tiles;
-  splits = splits < 1 ? 1 : (splits > nk ? nk : splits);
-  p.k_chunk = (int)((nk + splits - 1) / splits);
-  splits = (nk + p.k_chunk - 1) / p.k_chunk;
   const int grid = (int)(tiles * splits);
   p.j_groups = 0;
   if ((bsc == nullptr) != (bsh == nullptr)) return hipErrorInvalidValue;
+  hipError_t e;
   if (bsc != nullptr) {
-    if (bi == 128 && bj == 128) return launch<true, true, 128, 128, kAtomic, false, true>(p, grid, s);
-    if (bi == 128) return launch<true, true, 128, 64, kAtomic, false, true>(p, grid, s);
-    if (bj == 128) return launch<true, true, 64, 128, kAtomic, false, true>(p, grid, s);
-    return launch<true, true, 64, 64, kAtomic, false, true>(p, grid, s);
+    if (bi == 128 && bj == 128) e = launch<true, true, 128, 128, kSplit, false, true>(p, grid, s);
+    else if (bi == 128) e = launch<true, true, 128, 64, kSplit, false, true>(p, grid, s);
+    else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false, true>(p, grid, s);
+    else e = launch<true, true, 64, 64, kSplit, false, true>(p, grid, s);
+  } else {
+    if (bi == 128 && bj == 128) e = launch<true, true, 128, 128, kSplit, false>(p, grid, s);
+    else if (bi == 128) e = launch<true, true, 128, 64, kSplit, false>(p, grid, s);
+    else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false>(p, grid, s);
+    else e = launch<true, true, 64, 64, kSplit, false>(p, grid, s);
   }
-  if (bi == 128 && bj == 128) return launch<true, true, 128, 128, kAtomic, false>(p, grid, s);
-  if (bi == 128) return launch<true, true, 128, 64, kAtomic, false>(p, grid, s);
-  if (bj == 128) return launch<true, true, 64, 128, kAtomic, false>(p, grid, s);
-  return launch<true, true, 64, 64, kAtomic, false>(p, grid, s);
+  if (e != hipSuccess || splits == 1) return e;
+  const int64_t n = cin * cout;
+  const int64_t blocks = (n / 4 + 255) / 256;
+  hipLaunchKernelGGL(split_reduce_kernel, dim3((unsigned)(blocks < 4 * madnn::kNumCU ? blocks : 4 * madnn::kNumCU)), dim3(256), 0, s,
+                     ws, (int)splits, n, dw);
+  return hipGetLastError();
 }
 
 }  // extern "C"

@@ -155,7 +155,13 @@ def restrict_optimizer(opt, params: List[nn.Parameter]):
             groups.append(d)
     if not groups:
         groups = [{"params": params}]
-    return type(opt)(groups, **opt.defaults)
+    # the constructor's own keyword arguments only: a torch optimizer's defaults can carry derived
+    # entries it does not accept back (AdamW: decoupled_weight_decay); the groups keep every value
+    import inspect
+
+    sig = inspect.signature(type(opt).__init__).parameters
+    kw = {k: v for k, v in opt.defaults.items() if k in sig}
+    return type(opt)(groups, **kw)
 
 
 # ----------------------------------------------------------------------------
@@ -902,6 +908,7 @@ class PipelineEngine:
         self._out_meta: Dict[int, tuple] = {}   # chunk -> (shape, dtype) of its sent activation
         self._tied_works = []
         self._needs_tied = False
+        self.unpack_to_params = False   # a plain torch optimizer reads p.grad (build_pipeline)
         self.last_loss = None
         self.stats = {"steps": 0, "p2p_batches": 0}
 
@@ -1128,10 +1135,16 @@ class PipelineEngine:
     # -------------------------------------------------- optimizer protocol
     def finalize_grads(self, wait_tied: bool = True):
         """Idempotent: the stage-local DP reduction, then the cross-stage tied-gradient sum.
-        Called by clip_grad_norm_ AND step; the tied sum is applied exactly once per step."""
+        Called by clip_grad_norm_ AND step; the tied sum is applied exactly once per step.
+        With a plain torch optimizer (``unpack_to_params``) the final flat gradients are then
+        copied into ``p.grad`` -- after the tied sum, so a tied weight's .grad holds both stages'."""
+        pending = self.dp._needs_finalize or self._needs_tied
         self.dp.finalize_grads()
         if wait_tied and self._needs_tied:
             self._wait_tied()
+        if pending and self.unpack_to_params and not self._needs_tied:
+            for bk in self.dp.space.buckets:
+                self.dp.space.unpack_grads_to_params(bk)
 
     def tied_buckets(self) -> set:
         """Buckets holding a tied parameter: the optimizer updates them last, after the others
@@ -1365,13 +1378,23 @@ def build_pipeline(model: nn.Module, optimizer, cfg: Config, plan, loss_fn: Opti
                             lag=_planned_lag(plan),
                             sig_group=sig_groups[groups.dp_idx] if sig_groups else None)
     engine.plan = plan
-    if optimizer is not None:
-        if not _is_fused(optimizer):
-            raise TypeError("pipeline engine needs a madnn fused optimizer (FusedSGD / FusedAdam)")
+    if optimizer is not None and _is_fused(optimizer):
         optimizer.bind(space)
         optimizer.grad_source = engine
         optimizer.nonfinite = cfg.nonfinite
         dp_engine.optimizer = optimizer
+    elif optimizer is not None:
+        # a plain torch optimizer (as the DP path accepts, api._distribute_dp): it steps the stage's
+        # own parameters from p.grad; the engine fills p.grad before the step and re-syncs its flat
+        # master copy after it
+        engine.unpack_to_params = True
+        optimizer.register_step_pre_hook(lambda *a, **k: engine.finalize_grads())
+
+        def _after_plain(*a, **k):
+            space.sync_master_from_model()
+            engine.after_step()
+
+        optimizer.register_step_post_hook(_after_plain)
     get_logger().info("madnn pp: rank %d/%d chunks %s dp=%d microbatches=%d schedule=%s tied=%d", stage, S,
                       ranges, plan.dp, plan.microbatches, schedule, len(tied_local))
     return engine, optimizer

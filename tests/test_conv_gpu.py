@@ -453,3 +453,17 @@ def test_bn_relu_conv1x1_dgrad_epilogue_matches_fp32(cuda, shape):
     assert rel < 0.03, rel
     _close(bn.weight.grad, ref.weight.grad, 6e-2)
     _close(bn.bias.grad, ref.bias.grad, 6e-2)
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 256), (256, 64), (512, 2048)])
+def test_conv1x1_wgrad_split_k_is_deterministic(cuda, cin, cout):
+    """The m reduction is split over workgroups; the per-split fp32 slabs are summed in split order
+    (no float atomics): repeated calls are bitwise equal and match the fp32 reference."""
+    torch.manual_seed(4)
+    n, h = 32, 28
+    x = torch.randn(n, cin, h, h, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, h, h, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    dws = [torch.ops.madnn.conv1x1_wgrad(dy, x) for _ in range(3)]
+    assert all(torch.equal(dws[0], d) for d in dws[1:])
+    dwr = torch.einsum("nkhw,nchw->kc", dy.float(), x.float())
+    _close(dws[0], dwr, 1e-2)

@@ -291,3 +291,40 @@ def _w_plan_tuning_with_shape_change(rank, world):
 
 def test_plan_tuning_survives_a_shape_change_mid_tuning():
     run_dist(_w_plan_tuning_with_shape_change, 4)
+
+
+def _w_pp_plain_optimizer(rank, world, dp):
+    """A plain torch optimizer through the pipeline path (as the DP path accepts one): the engine
+    fills p.grad (after the cross-stage tied-embedding sum) before optimizer.step() and re-syncs its
+    flat master copy after it -- parameters track single-process AdamW."""
+    import madnn
+
+    model = _gpt_tiny(4)
+    x = torch.randint(0, 512, (8, 32), generator=torch.Generator().manual_seed(1))
+    ref = copy.deepcopy(model)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.01)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01)
+    pp = world // dp
+    eng, opt = madnn.distribute(model, opt, strategy="pp" if dp == 1 else "dp_pp", pp_stages=pp, microbatches=2,
+                                schedule="1f1b", example_input=x[:1], loss_fn=model.loss_fn, checkpointing="none",
+                                global_batch=x.shape[0])
+    assert isinstance(opt, torch.optim.AdamW) and eng.unpack_to_params
+    d_idx = eng.groups.dp_idx
+    per = x.shape[0] // dp
+    xr = x[d_idx * per:(d_idx + 1) * per]
+    for _ in range(3):
+        eng.train_step(xr, xr)
+        opt.step()
+        opt.zero_grad()
+        model.loss_fn(ref(x), x).backward()
+        ropt.step()
+        ropt.zero_grad()
+    ref_params = dict(ref.named_parameters(remove_duplicate=False))
+    for name, p in eng.state_dict().items():
+        torch.testing.assert_close(p.detach(), ref_params[name].detach(), atol=1e-3, rtol=1e-3,
+                                   msg=lambda m, name=name: f"{name}: {m}")
+
+
+@pytest.mark.parametrize("world,dp", [(2, 1), (4, 2)])
+def test_pp_plain_torch_optimizer(world, dp):
+    run_dist(_w_pp_plain_optimizer, world, dp)
