@@ -634,8 +634,8 @@ def conv1x1_route(cin: int, cout: int) -> tuple:
       (Cin <= 256, or an expanding Cout >= 2 Cin); MIOpen on the deep contracting reductions;
     * data grad: K9 on the HBM-bound shapes (Cin <= 256 and Cout <= 512), hipBLASLt GEMM on the
       deep ones; both add the identity path's gradient in the epilogue / with beta = 1;
-    * weight grad: MIOpen.  K9's split-M weight grad is faster per call on every ResNet-50 shape
-      in isolation but not in the full step (its zero-fill + cast launches), so MIOpen stays.
+    * weight grad: per shape the fastest of MIOpen, K12 split-K and K9 split-M (timed once,
+      :func:`tuned_wgrad`; K9's slabs are reduced and cast to bf16 in one pass, no zero fill).
     Same-box full-step A/B of these choices: docs/PERF.md ("K9 routing").
     ``MADNN_K9_DGRAD=wide`` / ``MADNN_K9_WGRAD=k9`` select the alternatives.
     """
@@ -725,7 +725,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             dx[:, :, ::2, ::2].add_(sub.to(dx.dtype))
         if ctx.needs_input_grad[1]:
             if wgrad == "k9":
-                dw = torch.ops.madnn.conv1x1_wgrad(dy, x).to(w.dtype).view(w.shape)
+                dw = _k9_wgrad(dy, x, w)
             else:
                 dw = _conv1x1_wgrad_lib(dy, x, w)
         return dx, dw, None, None
@@ -790,7 +790,7 @@ class _BNReluConv1x1Fn(torch.autograd.Function):
         else:
             da = torch.empty_like(y)
             torch.mm(_rows(dout), w.reshape(w.size(0), -1), out=_rows(da))
-        dw = torch.ops.madnn.conv1x1_wgrad(dout, y, scale, shift).to(w.dtype).view(w.shape)
+        dw = _k9_wgrad(dout, y, w, scale, shift)
         need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         dy, dbw, dbb, _ = torch.ops.madnn.bn_bwd(da, y, None, False, bn_w, mean, invstd, scale, shift, True, need_bn)
         return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
@@ -824,7 +824,7 @@ class _BNReluConv1x1EpiFn(torch.autograd.Function):
         dout = _nhwc(dout.to(y.dtype))
         da, part = torch.ops.madnn.conv1x1_dgrad_bnb(dout, w, y, scale, shift)
         if ctx.wgrad == "k9":
-            dw = torch.ops.madnn.conv1x1_wgrad(dout, a).to(w.dtype).view(w.shape)
+            dw = _k9_wgrad(dout, a, w)
         else:
             dw = _conv1x1_wgrad_lib(dout, a, w)
         dy, dbw, dbb = torch.ops.madnn.bn_bwd_ext(da, y, bn_w, mean, invstd, scale, shift, part, True)
@@ -1211,6 +1211,7 @@ _WGRAD_CHOICE: dict = {}
 _GELU_FWD_CHOICE: dict = {}
 _DGELU_CHOICE: dict = {}
 _TUNE = {"timed": 0, "table": None}   # run-time timings taken; the shipped table that was loaded
+_TUNE_MS: dict = {}   # (table, key) -> {implementation: ms for 3 calls} of every run-time timing (the A/B record)
 
 # Per-shape implementation choices measured on MI355X and shipped in-tree, so a job starts
 # without timing anything (a first-use timing runs BOTH implementations, and a library kernel's
@@ -1274,6 +1275,15 @@ def tuning_timings() -> int:
     return _TUNE["timed"]
 
 
+def tuning_measurements() -> list:
+    """Every per-shape timing this process ran: [{"table", "key", "ms": {impl: ms}, "chosen"}]."""
+    out = []
+    for (tab, key), ms in _TUNE_MS.items():
+        chosen = {"wgrad": _WGRAD_CHOICE, "gelu_fwd": _GELU_FWD_CHOICE, "dgelu": _DGELU_CHOICE}[tab].get(key)
+        out.append({"table": tab, "key": repr(key), "ms": {k: round(v, 4) for k, v in ms.items()}, "chosen": chosen})
+    return out
+
+
 def _wgrad_k12_ok(g2, x2, out) -> bool:
     return (_is_dev(g2) and g2.dtype == x2.dtype == out.dtype == torch.bfloat16 and g2.shape[0] % 64 == 0
             and g2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and g2.is_contiguous() and x2.is_contiguous()
@@ -1308,24 +1318,33 @@ def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.T
                        lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0))
 
 
-def tuned_wgrad(key, lib, k12):
+def tuned_wgrad(key, lib, k12, k9=None):
     """Run the weight-gradient implementation that was faster for ``key``: ``lib`` (the library
-    kernel: hipBLASLt / MIOpen) or ``k12`` (K12 split-K) -- from the shipped table
+    kernel: hipBLASLt / MIOpen), ``k12`` (K12 split-K over the rows) or, for NHWC 1x1 convolutions,
+    ``k9`` (K9's split-M kernel, slabs reduced and cast in one pass) -- from the shipped table
     (:func:`load_tuning_table`), else timed once on first use (outside graph capture).
     ``MADNN_WGRAD=lt`` / ``k12`` pin one."""
     if WGRAD == "lt":
         return lib()
     if WGRAD == "k12":
         return k12()
+    cands = {"lib": lib, "k12": k12}
+    if k9 is not None:
+        cands["k9"] = k9
     choice = _WGRAD_CHOICE.get(key)
-    if choice is None:
+    if choice not in cands:
         if torch.cuda.is_current_stream_capturing():
             return lib()
         _TUNE["timed"] += 1
-        t_lib = _time_wgrad(lib)
-        t_k12 = _time_wgrad(k12)
-        choice = _WGRAD_CHOICE[key] = "k12" if t_k12 < t_lib else "lib"
-    return k12() if choice == "k12" else lib()
+        times = {k: _time_wgrad(f) for k, f in cands.items()}
+        _TUNE_MS[("wgrad", key)] = times
+        choice = _WGRAD_CHOICE[key] = min(times, key=times.get)
+    return cands[choice]()
+
+
+def _k9_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, scale=None, shift=None) -> torch.Tensor:
+    """K9's weight gradient in ``w``'s dtype (the split reduction writes it: no cast pass)."""
+    return torch.ops.madnn.conv1x1_wgrad(dy, x, scale, shift, w.dtype == torch.bfloat16).to(w.dtype).view(w.shape)
 
 
 def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -1342,8 +1361,9 @@ def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> to
     probe = torch.empty(0, dtype=w.dtype, device=w.device)
     if not _wgrad_k12_ok(dr, xr, probe) or w.dtype != torch.bfloat16:
         return lib()
+    k9 = (lambda: _k9_wgrad(dy, x, w)) if x.dim() == 4 and conv1x1_supported(x, w.view(w.size(0), -1)) else None
     return tuned_wgrad(("conv1x1", dr.shape[0], dr.shape[1], xr.shape[1]), lib,
-                       lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape))
+                       lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape), k9)
 
 
 LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)
@@ -1404,6 +1424,7 @@ def _timed_choice(table: dict, key, cands: dict, default: str) -> str:
         return default
     _TUNE["timed"] += 1
     times = {k: _time_wgrad(f) for k, f in cands.items()}
+    _TUNE_MS[("gelu_fwd" if table is _GELU_FWD_CHOICE else "dgelu", key)] = times
     choice = table[key] = min(times, key=times.get)
     return choice
 

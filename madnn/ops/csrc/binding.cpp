@@ -83,7 +83,7 @@ hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int
                                const unsigned char* = nullptr, int = 0, int = 0);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 int64_t madnn_conv1x1_wgrad_ws(int64_t, int64_t, int64_t);
-hipError_t madnn_conv1x1_wgrad(const void*, const void*, float*, float*, int64_t, int64_t, int64_t, const float*, const float*,
+hipError_t madnn_conv1x1_wgrad(const void*, const void*, void*, int, float*, int64_t, int64_t, int64_t, const float*, const float*,
                                hipStream_t);
 hipError_t madnn_bn_coef(const void*, int64_t, int, float, float, const float*, const float*, float*, float*, int64_t*,
                          float*, float*, float*, float*, float*, const float*, int, hipStream_t);
@@ -712,9 +712,9 @@ std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnres(const at::Tensor& dy, con
   return {dx, part};
 }
 
-// fp32 [Cout, Cin] weight gradient
+// [Cout, Cin] weight gradient, fp32 (or bf16 with out_bf16: the split reduction casts)
 at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
-                         const c10::optional<at::Tensor>& shift) {
+                         const c10::optional<at::Tensor>& shift, bool out_bf16) {
   const int64_t cout = dy.size(1), cin = x.size(1);
   const float* sc = pro_ptr(scale, cin, "scale");
   const float* sh = pro_ptr(shift, cin, "shift");
@@ -723,11 +723,10 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::o
   TORCH_CHECK(conv_rows(dy, cout, "dy") == M && dy.dim() == x.dim(), "conv1x1_wgrad: dy / x pixel mismatch");
   TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  at::Tensor dw = at::empty({cout, cin}, x.options().dtype(at::kFloat));
-  const int64_t wsn = madnn_conv1x1_wgrad_ws(M, cin, cout);
-  at::Tensor ws = at::empty({wsn > 0 ? wsn : 1}, x.options().dtype(at::kFloat));
-  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), wsn > 0 ? ws.data_ptr<float>() : nullptr,
-                            M, cin, cout, sc, sh, cur_stream(x)),
+  at::Tensor dw = at::empty({cout, cin}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  at::Tensor ws = at::empty({madnn_conv1x1_wgrad_ws(M, cin, cout)}, x.options().dtype(at::kFloat));
+  check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), out_bf16 ? 1 : 0, ws.data_ptr<float>(), M, cin,
+                            cout, sc, sh, cur_stream(x)),
         "conv1x1_wgrad");
   return dw;
 }
@@ -1464,7 +1463,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def(
       "bn_bwd_ext(Tensor dy, Tensor x, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, Tensor shift, "
       "Tensor partial, bool relu) -> (Tensor, Tensor, Tensor)");
-  m.def("conv1x1_wgrad(Tensor dy, Tensor x, Tensor? scale=None, Tensor? shift=None) -> Tensor");
+  m.def("conv1x1_wgrad(Tensor dy, Tensor x, Tensor? scale=None, Tensor? shift=None, bool out_bf16=False) -> Tensor");
   m.def(
       "bn_coef(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, "
       "float momentum, float eps, Tensor? partial=None) -> Tensor[]");

@@ -428,14 +428,21 @@ inline void plan_persistent(GemmArgs& p, int64_t J, int BI, int64_t I, int64_t K
   p.k_chunk = 0;
 }
 
-// dw[i] = sum over splits of slab[s][i], in split order (deterministic); n % 4 == 0
+// dw[i] = sum over splits of slab[s][i], in split order (deterministic), fp32 or bf16; n % 4 == 0
+template <bool BF16>
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n,
-                                                           float* __restrict__ dw) {
+                                                           void* __restrict__ dw) {
   const int64_t n4 = n / 4;
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
     f32x4 acc = reinterpret_cast<const f32x4*>(slab)[v];
     for (int s = 1; s < splits; ++s) acc += reinterpret_cast<const f32x4*>(slab + (int64_t)s * n)[v];
-    reinterpret_cast<f32x4*>(dw)[v] = acc;
+    if constexpr (BF16) {
+      const unsigned lo = (unsigned)f32_to_bf16(acc[0]) | ((unsigned)f32_to_bf16(acc[1]) << 16);
+      const unsigned hi = (unsigned)f32_to_bf16(acc[2]) | ((unsigned)f32_to_bf16(acc[3]) << 16);
+      reinterpret_cast<u32x2*>(dw)[v] = u32x2{lo, hi};
+    } else {
+      reinterpret_cast<f32x4*>(dw)[v] = acc;
+    }
   }
 }
 
@@ -577,21 +584,21 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
               : launch<true, false, 64, 128, kStoreT, false>(p, grid, s);
 }
 
-// fp32 floats of workspace madnn_conv1x1_wgrad needs (0: one split, written straight to dw)
+// fp32 floats of workspace madnn_conv1x1_wgrad needs (the per-split partial slabs)
 int64_t madnn_conv1x1_wgrad_ws(int64_t M, int64_t cin, int64_t cout) {
   int bi, bj, kc;
   int64_t tiles, splits;
   wgrad_split(M, cin, cout, bi, bj, tiles, kc, splits);
-  return splits > 1 ? splits * cin * cout : 0;
+  return splits * cin * cout;
 }
 
-// dw: fp32 [cout][cin]; ws: madnn_conv1x1_wgrad_ws floats (the per-split partial slabs, summed in
-// split order into dw).  bsc/bsh (optional): x is convolved as relu(x * bsc + bsh), as in
-// madnn_conv1x1_fwd
-hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, float* ws, int64_t M, int64_t cin,
+// dw: [cout][cin] fp32 or (dw_bf16) bf16; ws: madnn_conv1x1_wgrad_ws floats (the per-split partial
+// slabs, summed in split order into dw -- one pass that also casts).  bsc/bsh (optional): x is
+// convolved as relu(x * bsc + bsh), as in madnn_conv1x1_fwd
+hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, void* dw, int dw_bf16, float* ws, int64_t M, int64_t cin,
                                int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
-  if (M <= 0) return hipMemsetAsync(dw, 0, (size_t)(cin * cout) * sizeof(float), s);
+  if (M <= 0) return hipMemsetAsync(dw, 0, (size_t)(cin * cout) * (dw_bf16 ? 2 : 4), s);
   GemmArgs p{};
   p.a = static_cast<const uint16_t*>(dy);  // A[i = co][k = m] = dY[m][co]: column memory
   p.lda = cout;
@@ -607,8 +614,8 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, float* 
   int bi, bj;
   int64_t tiles, splits;
   wgrad_split(M, cin, cout, bi, bj, tiles, p.k_chunk, splits);
-  if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
-  p.out = splits > 1 ? ws : dw;
+  if (ws == nullptr) return hipErrorInvalidValue;
+  p.out = ws;
   p.i_tiles = (int)(cout / bi);
   p.j_tiles = (int)(cin / bj);
   const int grid = (int)(tiles * splits);
@@ -626,11 +633,15 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, float* dw, float* 
     else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false>(p, grid, s);
     else e = launch<true, true, 64, 64, kSplit, false>(p, grid, s);
   }
-  if (e != hipSuccess || splits == 1) return e;
+  if (e != hipSuccess) return e;
   const int64_t n = cin * cout;
   const int64_t blocks = (n / 4 + 255) / 256;
-  hipLaunchKernelGGL(split_reduce_kernel, dim3((unsigned)(blocks < 4 * madnn::kNumCU ? blocks : 4 * madnn::kNumCU)), dim3(256), 0, s,
-                     ws, (int)splits, n, dw);
+  const dim3 grid_r((unsigned)(blocks < 4 * madnn::kNumCU ? blocks : 4 * madnn::kNumCU));
+  if (dw_bf16) {
+    hipLaunchKernelGGL(split_reduce_kernel<true>, grid_r, dim3(256), 0, s, ws, (int)splits, n, dw);
+  } else {
+    hipLaunchKernelGGL(split_reduce_kernel<false>, grid_r, dim3(256), 0, s, ws, (int)splits, n, dw);
+  }
   return hipGetLastError();
 }
 

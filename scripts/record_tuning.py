@@ -6,7 +6,7 @@ weight-gradient / GELU-Linear implementations (``ops.tuned_wgrad``), and MIOpen'
 convolution problems its find-db does not hold yet (that is where round 3's 76 s warm-up went:
 ``profiles/r4_first_steps_resnet50_b2048_*.json``).  This script runs the bench
 configurations (ResNet-50 at 2048 and 512 images, GPT-2 medium at every microbatch size the
-pipeline planner may choose) from an EMPTY choice table with MIOpen's user db pointed at
+pipeline planner may choose, BERT-large at 128 sequences) from an EMPTY choice table with MIOpen's user db pointed at
 ``--out``, then writes
 
   <out>/choices_gfx950.json   -> madnn/tuning/choices_gfx950.json
@@ -32,7 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/tuning")
     ap.add_argument("--resnet-batches", default="2048,512")
-    ap.add_argument("--gpt2-batches", default="64,32,16,8,4")
+    ap.add_argument("--gpt2-batches", default="128,64,32,16,8,4")
+    ap.add_argument("--bert-batches", default="128")
     ap.add_argument("--steps", type=int, default=2)
     args = ap.parse_args()
     out = Path(args.out)
@@ -103,9 +104,30 @@ def main():
         del model, opt, engine, ids
         torch.cuda.empty_cache()
 
+    from madnn.models.bert import BertForPreTraining, bert_config
+
+    for b in [int(v) for v in args.bert_batches.split(",") if v]:
+        torch.manual_seed(0)
+        cfg = bert_config("bert-large")
+        model = BertForPreTraining(cfg)
+        opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
+        engine, opt = madnn.distribute(model, opt, strategy="dp", checkpointing="none",
+                                       example_input=torch.zeros(1, 512, dtype=torch.long))
+        ids = torch.randint(0, cfg.vocab_size, (b, 512)).to(dev)
+
+        def step():
+            engine.train_step(ids, ids)
+            opt.step()
+
+        run(f"bert-large_b{b}", step, args.steps)
+        del model, opt, engine, ids
+        torch.cuda.empty_cache()
+
     ops.export_choices(str(out / "choices_gfx950.json"))
     (out / "record.json").write_text(json.dumps(rec, indent=1) + "\n")
-    print(json.dumps({"choices": len(ops._WGRAD_CHOICE) + len(ops._GELU_FWD_CHOICE),
+    # the per-shape A/B behind every choice (ms for 3 calls of each implementation)
+    (out / "measurements.json").write_text(json.dumps(ops.tuning_measurements(), indent=1) + "\n")
+    print(json.dumps({"choices": len(ops._WGRAD_CHOICE) + len(ops._GELU_FWD_CHOICE) + len(ops._DGELU_CHOICE),
                       "miopen_db": sorted(p.name for p in db.iterdir())}), flush=True)
 
 

@@ -467,3 +467,6 @@ def test_conv1x1_wgrad_split_k_is_deterministic(cuda, cin, cout):
     assert all(torch.equal(dws[0], d) for d in dws[1:])
     dwr = torch.einsum("nkhw,nchw->kc", dy.float(), x.float())
     _close(dws[0], dwr, 1e-2)
+    # bf16 output straight from the split reduction: the fp32 result rounded once
+    db = torch.ops.madnn.conv1x1_wgrad(dy, x, None, None, True)
+    assert db.dtype == torch.bfloat16 and torch.equal(db, dws[0].bfloat16())
