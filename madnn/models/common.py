@@ -66,13 +66,11 @@ class SelfAttention(nn.Module):
         drop = self.dropout if self.training else 0.0
         if ops.attention_supported(qkv, self.head_dim, drop):
             # K8 HIP attention on the [B, S, heads, D] layout the projection produced: no
-            # transposes; without RoPE it reads q/k/v and writes dQKV in place
-            if self.rope is None:
-                o = ops.attention_qkvpacked(qkv, self.heads, self.kv_heads, causal=self.causal)
-            else:
-                q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
-                q, k = self.rope(q, k, seq_dim=1)
-                o = ops.attention(q, k, v, causal=self.causal)
+            # transposes; it reads q/k/v and writes dQKV in place
+            if self.rope is not None:
+                # K14: q and k rotated in one pass into a packed buffer (backward: in place on dQKV)
+                qkv = ops.rope_qkv(qkv.contiguous(), self.rope.cos, self.rope.sin, self.heads + self.kv_heads)
+            o = ops.attention_qkvpacked(qkv, self.heads, self.kv_heads, causal=self.causal)
             return linear(self.proj, o.view(b, s, self.heads * self.head_dim))
         q, k, v = qkv.split([self.heads, self.kv_heads, self.kv_heads], dim=2)
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
@@ -107,6 +105,14 @@ class RotaryEmbedding(nn.Module):
         cos, sin = self._tables(self.cos.device)
         self.cos.copy_(cos)
         self.sin.copy_(sin)
+
+    def _apply(self, fn, *args, **kwargs):
+        # a module-wide dtype cast (model.bfloat16()) must not round the tables: K14 reads them in
+        # fp32 (recomputed exactly on the tables' device, never converted back from bf16)
+        super()._apply(fn, *args, **kwargs)
+        if self.cos.dtype != torch.float32 and self.cos.device.type != "meta":
+            self.cos, self.sin = self._tables(self.cos.device)
+        return self
 
     @staticmethod
     def _rot(x):

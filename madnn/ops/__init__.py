@@ -614,6 +614,81 @@ def attention_qkvpacked(qkv, heads: int, kv_heads: int, *, causal: bool = True, 
     return reference.attention(q, k, v, causal=causal, scale=scale)
 
 
+# ---------------------------------------------------------------- K14 / K15
+def _rope_rotate(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, inverse: bool) -> torch.Tensor:
+    """Eager reference of K14 on [B, S, heads, D] (fp32 math): (a, b) -> (a c -+ b s, b c +- a s)."""
+    d = x.size(-1) // 2
+    c, sn = cos[: x.size(1), None, :d].float(), sin[: x.size(1), None, :d].float()
+    a, b = x[..., :d].float(), x[..., d:].float()
+    if inverse:
+        return torch.cat([a * c + b * sn, b * c - a * sn], -1).to(x.dtype)
+    return torch.cat([a * c - b * sn, b * c + a * sn], -1).to(x.dtype)
+
+
+class _RopeQKVFn(torch.autograd.Function):
+    """RoPE on the q and k heads of a packed QKV projection (K14): one pass writes a new packed
+    tensor (q, k rotated, v copied) that the attention reads in place; the backward applies the
+    transpose rotation in place on the incoming dQKV (the attention backward's own fresh output,
+    consumed only here), so the packed gradient flows on to the projection with no copy."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, rot_heads):
+        ctx.save_for_backward(cos, sin)
+        ctx.rot = rot_heads
+        if _is_dev(qkv):
+            return torch.ops.madnn.rope_qkv(qkv, cos, sin, rot_heads, False)
+        out = qkv.clone()
+        out[:, :, :rot_heads] = _rope_rotate(qkv[:, :, :rot_heads], cos, sin, False)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        cos, sin = ctx.saved_tensors
+        g = g.contiguous()
+        if _is_dev(g):
+            torch.ops.madnn.rope_qkv_(g, cos, sin, ctx.rot, True)
+        else:
+            g = g.clone()
+            g[:, :, : ctx.rot] = _rope_rotate(g[:, :, : ctx.rot], cos, sin, True)
+        return g, None, None, None
+
+
+def rope_qkv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_heads: int) -> torch.Tensor:
+    """``qkv`` [B, S, heads, D] with heads ``0..rot_heads-1`` (q then k) rotated by the RoPE tables
+    ``cos`` / ``sin`` (fp32 [>= S, D], halves duplicated), as a new packed tensor.  HIP bf16
+    contiguous inputs run K14 (``madnn/ops/csrc/glue.hip``); others the eager reference."""
+    if _is_dev(qkv):
+        _need_native("rope_qkv")
+        if not (qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and qkv.size(-1) % 16 == 0
+                and cos.dtype == torch.float32 and cos.is_contiguous()):
+            raise ValueError("rope_qkv: needs a contiguous bf16 qkv (D % 16 == 0) and fp32 tables")
+    return _RopeQKVFn.apply(qkv, cos, sin, rot_heads)
+
+
+class _SwiGLUFn(torch.autograd.Function):
+    """h = silu(g) * u from the fused gate_up output [..., 2I] (K15); the backward writes the packed
+    d[g | u] the gate_up Linear consumes (no split / cat)."""
+
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        return torch.ops.madnn.swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return torch.ops.madnn.swiglu_bwd(dh, gu)
+
+
+def swiglu(gu: torch.Tensor) -> torch.Tensor:
+    """``silu(g) * u`` with ``g, u = gu.chunk(2, -1)``: K15 on contiguous HIP bf16, eager otherwise."""
+    if _is_dev(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.size(-1) % 16 == 0:
+        _need_native("swiglu")
+        return _SwiGLUFn.apply(gu)
+    g, u = gu.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
 # ---------------------------------------------------------------------- K9
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()

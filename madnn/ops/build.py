@@ -35,7 +35,8 @@ MANIFEST = HERE / "_madnn_build_manifest.json"
 
 ARCH = os.environ.get("MADNN_OFFLOAD_ARCH", "gfx950")
 KERNEL_SOURCES = ["bucket.hip", "optim.hip", "norm.hip", "bn.hip", "xent.hip", "pool.hip", "attn.hip", "conv.hip",
-                  "stem.hip", "bias.hip", "gemm.hip", "gemmp.hip", "conv3.hip", "xgmi.hip", "probe.hip", "binding.cpp", "lt.cpp"]
+                  "stem.hip", "bias.hip", "gemm.hip", "gemmp.hip", "conv3.hip", "xgmi.hip", "probe.hip", "glue.hip",
+                  "binding.cpp", "lt.cpp"]
 RUNTIME_SOURCES = ["runtime.cpp"]
 # per-source extra flags: MFMA kernels keep their accumulators in the (unified) VGPR file
 # instead of AGPRs, which removes a v_accvgpr_read/write around every softmax element

@@ -40,6 +40,9 @@ int madnn_bias_grad_supported(int64_t, int);
 int madnn_bias_grad_rows(int64_t, int, int);
 hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, hipStream_t);
 hipError_t madnn_gelu_fwd(const void*, void*, int64_t, int, hipStream_t);
+hipError_t madnn_rope_qkv(const void*, void*, const float*, const float*, int64_t, int, int, int, int, int, hipStream_t);
+hipError_t madnn_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
+hipError_t madnn_swiglu_bwd(const void*, const void*, void*, int64_t, int, hipStream_t);
 int madnn_attn_supported(int);
 hipError_t madnn_attn_fwd(const MadnnAttnArgs*, int, int, hipStream_t);
 hipError_t madnn_attn_bwd(const MadnnAttnArgs*, int, int, hipStream_t);
@@ -1279,6 +1282,65 @@ at::Tensor gelu_fwd(const at::Tensor& x) {
   return y;
 }
 
+// K14: heads 0..rot_heads-1 of the packed bf16 QKV [B, S, NH, D] rotated (inverse: the transpose
+// rotation); in place (rope_qkv_, the backward on dQKV) or into a new packed tensor (rope_qkv, the
+// v heads copied); cos / sin fp32 [>= S][D]
+at::Tensor rope_qkv_impl(const at::Tensor& qkv, at::Tensor out, const at::Tensor& cos, const at::Tensor& sin,
+                         int64_t rot_heads, bool inverse) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 4 && qkv.is_contiguous(),
+              "rope_qkv_: qkv must be a contiguous bf16 [B, S, heads, D]");
+  const int64_t S = qkv.size(1), NH = qkv.size(2), D = qkv.size(3);
+  TORCH_CHECK(D % 16 == 0 && rot_heads >= 0 && rot_heads <= NH, "rope_qkv_: D % 16 and rot_heads <= heads");
+  for (const at::Tensor* t : {&cos, &sin}) {
+    TORCH_CHECK(t->device() == qkv.device() && t->scalar_type() == at::kFloat && t->dim() == 2 && t->is_contiguous() &&
+                    t->size(0) >= S && t->size(1) == D,
+                "rope_qkv_: cos / sin must be contiguous fp32 [>= S, D] on the device");
+  }
+  at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  check(madnn_rope_qkv(qkv.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), qkv.size(0) * S,
+                       (int)S, (int)NH, (int)rot_heads, (int)D, inverse ? 1 : 0, cur_stream(qkv)),
+        "rope_qkv");
+  return out;
+}
+
+at::Tensor rope_qkv_(at::Tensor qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t rot_heads, bool inverse) {
+  return rope_qkv_impl(qkv, qkv, cos, sin, rot_heads, inverse);
+}
+
+at::Tensor rope_qkv(const at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, int64_t rot_heads,
+                    bool inverse) {
+  check_dev(qkv, "qkv");
+  return rope_qkv_impl(qkv, at::empty_like(qkv), cos, sin, rot_heads, inverse);
+}
+
+// K15: h = silu(g) * u of the fused gate_up output gu [..., 2I] -> [..., I]
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  check_dev(gu, "gu");
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && gu.is_contiguous() && gu.size(-1) % 16 == 0,
+              "swiglu: gu must be contiguous bf16 with a last dim that is a multiple of 16");
+  const int64_t I = gu.size(-1) / 2, M = gu.numel() / (2 * I);
+  auto shape = gu.sizes().vec();
+  shape.back() = I;
+  at::hip::HIPGuardMasqueradingAsCUDA guard(gu.device());
+  at::Tensor h = at::empty(shape, gu.options());
+  check(madnn_swiglu_fwd(gu.data_ptr(), h.data_ptr(), M, (int)I, cur_stream(gu)), "swiglu_fwd");
+  return h;
+}
+
+// K15 backward: d[g | u] from dh [..., I] and gu [..., 2I]
+at::Tensor swiglu_bwd(const at::Tensor& dh, const at::Tensor& gu) {
+  check_dev(gu, "gu");
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && gu.is_contiguous() && gu.size(-1) % 16 == 0, "swiglu_bwd: gu");
+  const int64_t I = gu.size(-1) / 2, M = gu.numel() / (2 * I);
+  at::Tensor d = dh.to(at::kBFloat16).contiguous();
+  TORCH_CHECK(d.numel() == M * I, "swiglu_bwd: dh must have gu's rows and I columns");
+  at::hip::HIPGuardMasqueradingAsCUDA guard(gu.device());
+  at::Tensor dgu = at::empty_like(gu);
+  check(madnn_swiglu_bwd(d.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, (int)I, cur_stream(gu)), "swiglu_bwd");
+  return dgu;
+}
+
 // K8 attention.  q: [B, S, H, D], k/v: [B, S, Hkv, D] bf16 views with a contiguous last dim
 // (any other strides, e.g. slices of one packed QKV projection).
 void attn_check(const at::Tensor& t, const char* name, int64_t D) {
@@ -1480,6 +1542,10 @@ TORCH_LIBRARY(madnn, m) {
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
+  m.def("rope_qkv_(Tensor(a!) qkv, Tensor cos, Tensor sin, int rot_heads, bool inverse) -> Tensor(a!)");
+  m.def("rope_qkv(Tensor qkv, Tensor cos, Tensor sin, int rot_heads, bool inverse) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor dh, Tensor gu) -> Tensor");
   m.def("maxpool_fwd(Tensor x, int k, int s, int p, bool need_arg) -> (Tensor, Tensor)");
   m.def("pool_bn_fwd(Tensor y, Tensor scale, Tensor shift, int p) -> (Tensor, Tensor)");
   m.def(
@@ -1531,6 +1597,10 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("pool_bn_bwd", pool_bn_bwd);
   m.impl("bias_grad", bias_grad);
   m.impl("gelu_fwd", gelu_fwd);
+  m.impl("rope_qkv_", rope_qkv_);
+  m.impl("rope_qkv", rope_qkv);
+  m.impl("swiglu_fwd", swiglu_fwd);
+  m.impl("swiglu_bwd", swiglu_bwd);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_bwd", attn_bwd);
   m.impl("maxpool_bwd", maxpool_bwd);

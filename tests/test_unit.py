@@ -857,3 +857,36 @@ def test_position_embedding_models_refuse_long_sequences():
     b = BertForPreTraining(bert_config("bert-tiny"))
     with pytest.raises(ValueError, match="max_position"):
         b(torch.zeros(1, 129, dtype=torch.long))
+
+
+def test_rope_qkv_autograd_matches_rotary_embedding():
+    """ops.rope_qkv (on a view of the packed projection, eager path on CPU) equals the
+    RotaryEmbedding rotation of q and k, leaves v alone, and its backward is the transpose rotation:
+    gradients match autograd through the reference."""
+    from madnn import ops
+    from madnn.models.common import RotaryEmbedding
+
+    torch.manual_seed(0)
+    B, S, H, HKV, D = 2, 12, 4, 2, 32
+    rope = RotaryEmbedding(D, 10000.0, 64)
+    x = torch.randn(B, S, 16, requires_grad=True)
+    w = torch.randn((H + 2 * HKV) * D, 16)
+    qkv = (x @ w.t()).view(B, S, H + 2 * HKV, D)
+    out = ops.rope_qkv(qkv, rope.cos, rope.sin, H + HKV)
+    g = torch.randn_like(out)
+    (out * g).sum().backward()
+    xr = x.detach().clone().requires_grad_(True)
+    q, k, v = (xr @ w.t()).view(B, S, H + 2 * HKV, D).split([H, HKV, HKV], dim=2)
+    qr, kr = rope(q, k, seq_dim=1)
+    ref = torch.cat([qr, kr, v], dim=2)
+    torch.testing.assert_close(out.detach(), ref.detach(), atol=1e-5, rtol=1e-5)
+    (ref * g).sum().backward()
+    torch.testing.assert_close(x.grad, xr.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_swiglu_eager_path():
+    from madnn import ops
+
+    gu = torch.randn(3, 5, 32)
+    g, u = gu.chunk(2, -1)
+    torch.testing.assert_close(ops.swiglu(gu), torch.nn.functional.silu(g) * u)
