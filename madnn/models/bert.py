@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .. import ops
 from ..nn.norm import FusedLayerNorm
 from .common import init_module_, SelfAttention, init_normal_, linear, mlm_loss
 
@@ -84,7 +85,13 @@ class BertLayer(nn.Module):
 
     def forward(self, x):
         y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
-        z, _ = self.ffn_norm(self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y)))), residual=y)
+        if (self.drop.p == 0.0 or not self.training) and ops.FUSED_LINEAR and type(self.fc1) is nn.Linear \
+                and type(self.fc2) is nn.Linear:
+            # one fused autograd node: the exact GELU and its backward in the two GEMMs' epilogues
+            h = ops.gelu_mlp(y, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, approximate="none")
+        else:
+            h = self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y))))
+        z, _ = self.ffn_norm(h, residual=y)
         return z
 
 

@@ -1239,33 +1239,45 @@ def _gelu_tanh_grad(p: torch.Tensor) -> torch.Tensor:
     return 0.5 * (1 + t) + 0.5 * p * (1 - t * t) * k0 * (1 + 3 * k1 * p * p)
 
 
-def bias_grad(dy: torch.Tensor, pre: Optional[torch.Tensor] = None, bias_dtype: Optional[torch.dtype] = None):
+GELU_KIND = {"tanh": 1, "none": 2}   # F.gelu's ``approximate`` -> the kernels' GELU kind (gelu.h)
+
+
+def _gelu_grad_ref(p: torch.Tensor, kind: int) -> torch.Tensor:
+    if kind == 1:
+        return _gelu_tanh_grad(p)
+    cdf = 0.5 * (1.0 + torch.erf(p * 0.7071067811865476))
+    return cdf + p * torch.exp(-0.5 * p * p) * 0.3989422804014327
+
+
+def bias_grad(dy: torch.Tensor, pre: Optional[torch.Tensor] = None, bias_dtype: Optional[torch.dtype] = None,
+              kind: int = 1):
     """A Linear's bias gradient: the column sum of ``dy`` over every leading dim (K11, bias.hip).
 
-    With ``pre`` (the tanh-GELU input) the GELU backward is fused into the same pass: returns
-    ``(db, dp)`` with ``dp = dy * gelu'(pre)`` and ``db = sum(dp)``; otherwise ``(db, None)``."""
+    With ``pre`` (the GELU input; ``kind`` 1 tanh / 2 erf GELU) the GELU backward is fused into the
+    same pass: returns ``(db, dp)`` with ``dp = dy * gelu'(pre)`` and ``db = sum(dp)``; otherwise
+    ``(db, None)``."""
     bias_dtype = bias_dtype or dy.dtype
     n = dy.shape[-1]
     if not _is_dev(dy) or n % 8:
         acc = torch.promote_types(dy.dtype, torch.float32)
         g = dy.to(acc)
         if pre is not None:
-            g = g * _gelu_tanh_grad(pre.to(acc))
+            g = g * _gelu_grad_ref(pre.to(acc), kind)
         return g.reshape(-1, n).sum(0).to(bias_dtype), (g.to(dy.dtype) if pre is not None else None)
-    db, dp = _need_native("bias_grad").bias_grad(dy, pre, bias_dtype)
+    db, dp = _need_native("bias_grad").bias_grad(dy, pre, bias_dtype, kind)
     return db, (dp.view(dy.shape) if pre is not None else None)
 
 
 GELU_KERNEL = os.environ.get("MADNN_GELU_KERNEL", "1") != "0"  # K11 GELU forward (A/B switch)
 
 
-def gelu_tanh(x: torch.Tensor) -> torch.Tensor:
-    """tanh-approximate GELU forward: the K11-family streaming kernel on HIP tensors (16-byte
-    accesses, v_exp-based tanh), ``F.gelu(approximate="tanh")`` elsewhere.  No autograd: the
-    caller (the fused Linear) saves the pre-activation and runs the GELU backward in K11."""
+def gelu_tanh(x: torch.Tensor, kind: int = 1) -> torch.Tensor:
+    """GELU forward (``kind`` 1: tanh approximation, 2: exact erf): the K11-family streaming kernel
+    on HIP tensors (16-byte accesses, v_exp-based), ``F.gelu`` elsewhere.  No autograd: the caller
+    (the fused Linear / MLP) saves the pre-activation and runs the GELU backward in K11 / K12P."""
     if GELU_KERNEL and _is_dev(x) and x.numel() % 8 == 0 and x.dtype in (torch.bfloat16, torch.float32):
-        return _need_native("gelu_tanh").gelu_fwd(x)
-    return F.gelu(x, approximate="tanh")
+        return _need_native("gelu_tanh").gelu_fwd(x, kind)
+    return F.gelu(x, approximate="tanh" if kind == 1 else "none")
 
 
 def grad_sink(weight: torch.Tensor) -> Optional[torch.Tensor]:
@@ -1504,9 +1516,9 @@ def _timed_choice(table: dict, key, cands: dict, default: str) -> str:
     return choice
 
 
-def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]):
-    """``(gelu_tanh(pre), pre)`` with ``pre = x W^T + b``, from whichever implementation was
-    faster for the shape (timed once on first use, like :func:`tuned_wgrad`):
+def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], kind: int = 1):
+    """``(gelu(pre), pre)`` with ``pre = x W^T + b`` (``kind`` 1 tanh / 2 erf GELU), from whichever
+    implementation was faster for the shape (timed once on first use, like :func:`tuned_wgrad`):
 
     * ``lt``: hipBLASLt GEMM (bias epilogue), then the K11 streaming GELU pass (hipBLASLt has no
       GELU+AUX algorithm at GPT-2's 65536-row shapes on gfx950);
@@ -1522,13 +1534,15 @@ def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 
     def lt():
         pre = F.linear(x2, weight, bias if bias is None or bias.dtype == x2.dtype else bias.to(x2.dtype))
-        return gelu_tanh(pre), pre
+        return gelu_tanh(pre, kind), pre
 
     def k12():
-        return torch.ops.madnn.linear_fwd(x2, weight, bias, None, 1, True)
+        return torch.ops.madnn.linear_fwd(x2, weight, bias, None, kind, True)
 
     def k12p():
-        return torch.ops.madnn.linear_fwd_p(x2, weight, bias, 1)
+        return torch.ops.madnn.linear_fwd_p(x2, weight, bias, kind)
+
+    tag = () if kind == 1 else ("erf",)
 
     ok12 = _k12_fwd_ok(x2, weight, bias)
     okp = ok12 and _k12p_ok(x2, weight, weight.shape[0], x2.shape[0], x2.shape[1], bias is not None)
@@ -1538,10 +1552,10 @@ def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
     if choice not in ("lt", "k12", "k12p"):
         choice = "lt"
         if okp:
-            key = ("p", tuple(x2.shape), tuple(weight.shape), bias is not None)
+            key = ("p", tuple(x2.shape), tuple(weight.shape), bias is not None) + tag
             choice = _timed_choice(_GELU_FWD_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")
         elif ok12:
-            key = (tuple(x2.shape), tuple(weight.shape), bias is not None)
+            key = (tuple(x2.shape), tuple(weight.shape), bias is not None) + tag
             choice = _timed_choice(_GELU_FWD_CHOICE, key, {"lt": lt, "k12": k12}, "lt")
     y, pre = {"lt": lt, "k12": k12, "k12p": k12p}[choice]()
     return y.view(out_shape), pre.view(out_shape)
@@ -1550,8 +1564,9 @@ def _gelu_linear_fwd(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch
 DGELU = os.environ.get("MADNN_DGELU", "auto")  # c_proj dgrad + GELU backward: auto | lt | k12p
 
 
-def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dtype: torch.dtype):
-    """``(dh, db)``: the data gradient of the Linear after a tanh-GELU (``da = g2 @ w2``) pushed
+def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dtype: torch.dtype, kind: int = 1):
+    """``(dh, db)``: the data gradient of the Linear after a GELU (``kind`` 1 tanh / 2 erf;
+    ``da = g2 @ w2``) pushed
     through that GELU (``dh = da * gelu'(pre)``) plus the GELU Linear's bias gradient
     (``db = sum(dh)``), from whichever was faster for the shape:
 
@@ -1562,11 +1577,11 @@ def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dty
 
     ``MADNN_DGELU=lt`` / ``k12p`` pin one."""
     def lt():
-        db, dh = bias_grad(g2 @ w2, pre2, bias_dtype)
+        db, dh = bias_grad(g2 @ w2, pre2, bias_dtype, kind)
         return dh, db
 
     def k12p():
-        return tuple(torch.ops.madnn.linear_dgrad_p(g2, w2, pre2, bias_dtype))
+        return tuple(torch.ops.madnn.linear_dgrad_p(g2, w2, pre2, bias_dtype, kind))
 
     ok = (bias_dtype in (torch.float32, torch.bfloat16) and _is_dev(pre2) and pre2.dtype == g2.dtype
           and pre2.is_contiguous() and pre2.data_ptr() % 16 == 0
@@ -1577,7 +1592,7 @@ def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dty
     if choice == "auto":
         choice = "lt"
         if ok:
-            key = (tuple(g2.shape), tuple(w2.shape), str(bias_dtype))
+            key = (tuple(g2.shape), tuple(w2.shape), str(bias_dtype)) + (() if kind == 1 else ("erf",))
             choice = _timed_choice(_DGELU_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")
     return lt() if choice == "lt" else k12p()
 
@@ -1665,15 +1680,16 @@ class _LinearFn(torch.autograd.Function):
 def _linear_residual_fwd(a: torch.Tensor, weight, bias, residual):
     """``a W^T + b (+ residual)``: one hipBLASLt call with the bias / residual epilogue when it
     takes it, else ``F.linear`` + add."""
-    if residual is not None and _lt_ok(a, weight, False, True):
+    if _lt_ok(a, weight, False, residual is not None):
         a2 = a.reshape(-1, a.shape[-1])
         if not a2.is_contiguous():
             a2 = a2.contiguous()
-        r2 = residual.reshape(-1, weight.shape[0]).contiguous()
+        r2 = residual.reshape(-1, weight.shape[0]).contiguous() if residual is not None else None
         out = _lt_linear(a2, weight, bias if bias is None or bias.is_contiguous() else bias.contiguous(), r2, False)
         if out is not None:
             return out[0].view(*a.shape[:-1], weight.shape[0])
-    y = F.linear(a, weight, bias)
+    # an fp32 bias (kept in fp32 by the data-parallel space) joins a bf16 GEMM in the GEMM's dtype
+    y = F.linear(a, weight, bias if bias is None or bias.dtype == a.dtype else bias.to(a.dtype))
     return y + residual if residual is not None else y
 
 
@@ -1701,8 +1717,9 @@ class _GeluMLPFn(torch.autograd.Function):
     (nodemodule.lua:133-159)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, residual):
-        a, pre = _gelu_linear_fwd(x, w1, b1)
+    def forward(ctx, x, w1, b1, w2, b2, residual, kind=1):
+        a, pre = _gelu_linear_fwd(x, w1, b1, kind)
+        ctx.kind = kind
         y = _linear_residual_fwd(a, w2, b2, residual)
         ctx.save_for_backward(x, w1, pre, a, w2)
         ctx.b1_dtype = b1.dtype if b1 is not None else None
@@ -1730,26 +1747,30 @@ class _GeluMLPFn(torch.autograd.Function):
             g2 = g2.contiguous()
         a2 = a.reshape(-1, a.shape[-1])
         dw2 = _weight_grad(g2, a2, p2) if need[3] else None
-        dh, db1 = dgrad_dgelu(g2, w2, pre.reshape(-1, pre.shape[-1]), ctx.b1_dtype or g2.dtype)
+        dh, db1 = dgrad_dgelu(g2, w2, pre.reshape(-1, pre.shape[-1]), ctx.b1_dtype or g2.dtype, ctx.kind)
         if ctx.b1_dtype is None or not need[2]:
             db1 = None
         x2 = x.reshape(-1, x.shape[-1])
         dw1 = _weight_grad(dh, x2, p1) if need[1] else None
         dx = (dh @ w1).view(*x.shape[:-1], w1.shape[1]) if need[0] else None
-        return dx, dw1, db1, dw2, db2, (g if ctx.has_res else None)
+        return dx, dw1, db1, dw2, db2, (g if ctx.has_res else None), None
 
 
 def gelu_mlp(x: torch.Tensor, w1: torch.Tensor, b1: Optional[torch.Tensor], w2: torch.Tensor,
-             b2: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``linear(gelu_tanh(linear(x, w1, b1)), w2, b2) (+ residual)``: the transformer MLP as one
-    fused autograd node on HIP tensors (:class:`_GeluMLPFn`), eager ops elsewhere."""
+             b2: Optional[torch.Tensor], residual: Optional[torch.Tensor] = None,
+             approximate: str = "tanh") -> torch.Tensor:
+    """``linear(gelu(linear(x, w1, b1)), w2, b2) (+ residual)``: the transformer MLP as one fused
+    autograd node on HIP tensors (:class:`_GeluMLPFn`), eager ops elsewhere.  ``approximate`` as
+    in ``F.gelu``: "tanh" (GPT-2) or "none" (the exact erf GELU, BERT)."""
     if residual is not None and residual.shape[:-1] != x.shape[:-1]:
         raise ValueError("gelu_mlp: residual must have the output's shape")
+    if approximate not in GELU_KIND:
+        raise ValueError(f"gelu_mlp: approximate must be 'tanh' or 'none', not {approximate!r}")
     if not _is_dev(x) or not torch.is_grad_enabled() or w1.shape[0] % 8 or w2.shape[0] % 8:
-        h = F.gelu(F.linear(x, w1, b1), approximate="tanh")
+        h = F.gelu(F.linear(x, w1, b1), approximate=approximate)
         y = F.linear(h, w2, b2)
         return y + residual if residual is not None else y
-    return _GeluMLPFn.apply(x, w1, b1, w2, b2, residual)
+    return _GeluMLPFn.apply(x, w1, b1, w2, b2, residual, GELU_KIND[approximate])
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,

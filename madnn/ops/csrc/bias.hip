@@ -22,7 +22,7 @@ constexpr int kBiasLanes = 256;
 
 // 8 elements per lane per access (16-byte loads/stores), U accesses in flight per lane,
 // grid-stride over the flat tensor.  HBM-bound: reads x, writes y, nothing else.
-template <int DT, int U = 4>
+template <int DT, int U, int GK>
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ x, void* __restrict__ y,
                                                        int64_t n8) {
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[u][j] = gelu_tanh(v[u][j]);
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu_act<GK>(v[u][j]);
       store8<DT>(y, (i + u * stride) * 8, v[u]);
     }
   }
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const void* __restrict__ 
     float v[8];
     load8<DT>(x, i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_act<GK>(v[j]);
     store8<DT>(y, i * 8, v);
   }
 }
@@ -59,8 +59,8 @@ __host__ __device__ inline BiasGeom bias_geom(int N) {
 }
 
 // U: rows per lane in flight in the main loop (the GELU variant at 2 / 8 measured -0.08 % / -0.54 % on
-// the GPT-2 medium step against 4, round 4)
-template <int XDT, bool GELU, int U = 4>
+// the GPT-2 medium step against 4, round 4).  GELU: 0 none, kGeluTanh / kGeluErf (gelu.h)
+template <int XDT, int GELU, int U = 4>
 __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __restrict__ dy,
                                                                const void* __restrict__ pre, void* __restrict__ dp,
                                                                int64_t M, int N, float* __restrict__ partial) {
@@ -80,14 +80,14 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
       float v[U][8];
 #pragma unroll
       for (int u = 0; u < U; ++u) load8<XDT>(dy, (r + u * step) * N + col, v[u]);
-      if constexpr (GELU) {
+      if constexpr (GELU != 0) {
         float p[U][8];
 #pragma unroll
         for (int u = 0; u < U; ++u) load8<XDT>(pre, (r + u * step) * N + col, p[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_tanh_grad(p[u][j]);
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_act_grad<GELU>(p[u][j]);
           store8<XDT>(dp, (r + u * step) * N + col, v[u]);
         }
       }
@@ -99,11 +99,11 @@ __global__ __launch_bounds__(kBiasLanes) void bias_grad_kernel(const void* __res
     for (; r < M; r += step) {
       float v[8];
       load8<XDT>(dy, r * N + col, v);
-      if constexpr (GELU) {
+      if constexpr (GELU != 0) {
         float p[8];
         load8<XDT>(pre, r * N + col, p);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_tanh_grad(p[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_act_grad<GELU>(p[j]);
         store8<XDT>(dp, r * N + col, v);
       }
 #pragma unroll
@@ -196,7 +196,9 @@ int madnn_gelu_tune(int key, int value) {
   return old;
 }
 
-hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t stream) {
+// kind: kGeluTanh (1) or kGeluErf (2)
+hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, int kind, hipStream_t stream) {
+  if (kind != kGeluTanh && kind != kGeluErf) return hipErrorInvalidValue;
   if (n % 8) return hipErrorInvalidValue;
   const int64_t n8 = n / 8;
   const int U = g_gelu_unroll >= 16 ? 16 : g_gelu_unroll >= 8 ? 8 : 4;
@@ -204,32 +206,44 @@ hipError_t madnn_gelu_fwd(const void* x, void* y, int64_t n, int dt, hipStream_t
   const int64_t cap = (int64_t)g_gelu_wg * kNumCU;  // a few waves per CU, grid-stride beyond that
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
-  MADNN_DISPATCH_DT(dt, DT, {
-    if (U == 16) {
-      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 16>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-    } else if (U == 8) {
-      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 8>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-    } else {
-      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 4>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);
-    }
-  });
+#define MADNN_GELU_U(GK)                                                                                     \
+  MADNN_DISPATCH_DT(dt, DT, {                                                                                \
+    if (U == 16) {                                                                                           \
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 16, GK>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8); \
+    } else if (U == 8) {                                                                                     \
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 8, GK>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);  \
+    } else {                                                                                                 \
+      hipLaunchKernelGGL((gelu_fwd_kernel<DT, 4, GK>), dim3((unsigned)grid), dim3(256), 0, stream, x, y, n8);  \
+    }                                                                                                        \
+  })
+  if (kind == kGeluErf) {
+    MADNN_GELU_U(kGeluErf);
+  } else {
+    MADNN_GELU_U(kGeluTanh);
+  }
+#undef MADNN_GELU_U
   return hipGetLastError();
 }
 
 // dy, pre, dp: [M, N] of dtype xdt; partial: [R, N] fp32 with R = madnn_bias_grad_rows(M, N, pre != 0);
-// db: [N] of odt
+// db: [N] of odt; kind: the GELU whose backward runs on pre (kGeluTanh / kGeluErf)
 hipError_t madnn_bias_grad(const void* dy, const void* pre, void* dp, int64_t M, int N, int xdt, float* partial,
-                           void* db, int odt, hipStream_t stream) {
+                           void* db, int odt, int kind, hipStream_t stream) {
   if (!madnn_bias_grad_supported(M, N)) return hipErrorInvalidValue;
+  if (pre != nullptr && kind != kGeluTanh && kind != kGeluErf) return hipErrorInvalidValue;
   const BiasGeom g = bias_geom(N);
   const int R = madnn_bias_grad_rows(M, N, pre != nullptr);
   const dim3 grid(g.strips, R);
   MADNN_DISPATCH_DT(xdt, XDT, {
-    if (pre) {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, true>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N, partial);
+    if (pre && kind == kGeluErf) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, kGeluErf>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
+                         partial);
+    } else if (pre) {
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, kGeluTanh>), grid, dim3(kBiasLanes), 0, stream, dy, pre, dp, M, N,
+                         partial);
     } else {
-      hipLaunchKernelGGL((bias_grad_kernel<XDT, false>), grid, dim3(kBiasLanes), 0, stream, dy, nullptr, nullptr,
-                         M, N, partial);
+      hipLaunchKernelGGL((bias_grad_kernel<XDT, 0>), grid, dim3(kBiasLanes), 0, stream, dy, nullptr, nullptr, M, N,
+                         partial);
     }
   });
   hipError_t e = hipGetLastError();

@@ -38,8 +38,8 @@ hipError_t madnn_bn_fwd(const void*, const void*, void*, unsigned char*, int64_t
                         const float*, int, hipStream_t);
 int madnn_bias_grad_supported(int64_t, int);
 int madnn_bias_grad_rows(int64_t, int, int);
-hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, hipStream_t);
-hipError_t madnn_gelu_fwd(const void*, void*, int64_t, int, hipStream_t);
+hipError_t madnn_bias_grad(const void*, const void*, void*, int64_t, int, int, float*, void*, int, int, hipStream_t);
+hipError_t madnn_gelu_fwd(const void*, void*, int64_t, int, int, hipStream_t);
 hipError_t madnn_rope_qkv(const void*, void*, const float*, const float*, int64_t, int, int, int, int, int, hipStream_t);
 hipError_t madnn_swiglu_fwd(const void*, void*, int64_t, int, hipStream_t);
 hipError_t madnn_swiglu_bwd(const void*, const void*, void*, int64_t, int, hipStream_t);
@@ -116,7 +116,7 @@ hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int,
 int madnn_gemmp_supported(int64_t, int64_t, int64_t, int);
 hipError_t madnn_linear_fwd_p(const void*, const void*, const void*, int, void*, void*, int, int64_t, int64_t,
                               int64_t, hipStream_t);
-hipError_t madnn_linear_dgrad_p(const void*, const void*, const void*, void*, float*, int64_t, int64_t, int64_t,
+hipError_t madnn_linear_dgrad_p(const void*, const void*, const void*, void*, float*, int64_t, int64_t, int64_t, int,
                                 hipStream_t);
 hipError_t madnn_colsum_finalize(const float*, int, int64_t, void*, int, hipStream_t);
 hipError_t madnn_hwq_wait(const int*, int, int64_t, int*, hipStream_t);
@@ -743,7 +743,7 @@ void gemm_check(const at::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "linear: ", name, " must be 16-B aligned");
 }
 
-// y = x w^T (+ bias) (-> tanh-GELU) (+ res); with save_aux the pre-activation is returned too
+// y = x w^T (+ bias) (-> GELU: act 1 tanh / 2 erf) (+ res); with save_aux the pre-activation is returned too
 std::tuple<at::Tensor, at::Tensor> linear_fwd(const at::Tensor& x, const at::Tensor& w,
                                               const c10::optional<at::Tensor>& bias,
                                               const c10::optional<at::Tensor>& res, int64_t act, bool save_aux) {
@@ -859,10 +859,11 @@ std::tuple<at::Tensor, at::Tensor> linear_fwd_p(const at::Tensor& x, const at::T
   std::vector<int64_t> shape(x.sizes().begin(), x.sizes().end());
   shape.back() = N;
   at::Tensor y = at::empty(shape, x.options());
-  at::Tensor aux = act == 1 ? at::empty(shape, x.options()) : at::empty({0}, x.options());
+  TORCH_CHECK(act >= 0 && act <= 2, "linear_fwd_p: act 0 (none), 1 (tanh GELU) or 2 (erf GELU)");
+  at::Tensor aux = act != 0 ? at::empty(shape, x.options()) : at::empty({0}, x.options());
   check(madnn_linear_fwd_p(x.data_ptr(), w.data_ptr(), hb ? bias->data_ptr() : nullptr,
                            hb && bias->scalar_type() == at::kFloat ? 1 : 0, y.data_ptr(),
-                           act == 1 ? aux.data_ptr() : nullptr, (int)act, M, N, K, cur_stream(x)),
+                           act != 0 ? aux.data_ptr() : nullptr, (int)act, M, N, K, cur_stream(x)),
         "linear_fwd_p");
   return {y, aux};
 }
@@ -870,7 +871,9 @@ std::tuple<at::Tensor, at::Tensor> linear_fwd_p(const at::Tensor& x, const at::T
 // dx = dy w; with pre: (dx * gelu'(pre), column sums of that in bias_dtype) -- the GELU backward
 // and c_fc's bias gradient fused into the data-gradient GEMM
 std::tuple<at::Tensor, at::Tensor> linear_dgrad_p(const at::Tensor& dy, const at::Tensor& w,
-                                                  const c10::optional<at::Tensor>& pre, at::ScalarType bias_dtype) {
+                                                  const c10::optional<at::Tensor>& pre, at::ScalarType bias_dtype,
+                                                  int64_t gelu_kind) {
+  TORCH_CHECK(gelu_kind == 1 || gelu_kind == 2, "linear_dgrad_p: gelu_kind 1 (tanh) or 2 (erf)");
   gemm_check(dy, "dy");
   gemm_check(w, "w");
   const int64_t N = dy.size(-1), K = w.size(1), M = dy.numel() / std::max<int64_t>(N, 1);
@@ -891,7 +894,7 @@ std::tuple<at::Tensor, at::Tensor> linear_dgrad_p(const at::Tensor& dy, const at
   const int rows = (int)(M / 256 * 4);
   if (hp) part = at::empty({rows, K}, dy.options().dtype(at::kFloat));
   check(madnn_linear_dgrad_p(dy.data_ptr(), w.data_ptr(), hp ? pre->data_ptr() : nullptr, dx.data_ptr(),
-                             hp ? part.data_ptr<float>() : nullptr, M, N, K, cur_stream(dy)),
+                             hp ? part.data_ptr<float>() : nullptr, M, N, K, (int)gelu_kind, cur_stream(dy)),
         "linear_dgrad_p");
   if (hp)
     check(madnn_colsum_finalize(part.data_ptr<float>(), rows, K, db.data_ptr(), bias_dtype == at::kFloat ? 1 : 0,
@@ -1249,7 +1252,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> pool_bn_bwd(const at::Tensor& dp,
 // K11 Linear bias gradient.  dy (and pre): [..., N], row-major contiguous.  Returns
 // (db [N] in bias_dtype, dp) where dp = dy * gelu_tanh'(pre) when pre is given (else empty).
 std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::optional<at::Tensor>& pre,
-                                             at::ScalarType bias_dtype) {
+                                             at::ScalarType bias_dtype, int64_t gelu_kind) {
+  TORCH_CHECK(gelu_kind == 1 || gelu_kind == 2, "bias_grad: gelu_kind 1 (tanh) or 2 (erf)");
   check_dev(dy, "dy");
   at::Tensor g = dy.contiguous();
   const int64_t N = g.size(-1), M = g.numel() / N;
@@ -1266,19 +1270,22 @@ std::tuple<at::Tensor, at::Tensor> bias_grad(const at::Tensor& dy, const c10::op
   at::Tensor partial = at::empty({R, N}, g.options().dtype(at::kFloat));
   at::Tensor db = at::empty({N}, g.options().dtype(bias_dtype));
   check(madnn_bias_grad(g.data_ptr(), pc.defined() ? pc.data_ptr() : nullptr, pc.defined() ? dp.data_ptr() : nullptr,
-                        M, (int)N, dt_code(g), partial.data_ptr<float>(), db.data_ptr(), dt_code(db), cur_stream(g)),
+                        M, (int)N, dt_code(g), partial.data_ptr<float>(), db.data_ptr(), dt_code(db), (int)gelu_kind,
+                        cur_stream(g)),
         "bias_grad");
   return {db, dp};
 }
 
-// tanh-GELU forward (K11 family): y = gelu(x), x any contiguous float tensor with numel % 8 == 0.
-at::Tensor gelu_fwd(const at::Tensor& x) {
+// GELU forward (K11 family, kind 1 tanh / 2 erf): y = gelu(x), x contiguous float, numel % 8 == 0.
+at::Tensor gelu_fwd(const at::Tensor& x, int64_t kind) {
+  TORCH_CHECK(kind == 1 || kind == 2, "gelu_fwd: kind 1 (tanh) or 2 (erf)");
   check_dev(x, "x");
   at::Tensor xc = x.contiguous();
   TORCH_CHECK(xc.numel() % 8 == 0, "gelu_fwd: numel must be a multiple of 8");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = at::empty_like(xc);
-  if (xc.numel()) check(madnn_gelu_fwd(xc.data_ptr(), y.data_ptr(), xc.numel(), dt_code(xc), cur_stream(xc)), "gelu_fwd");
+  if (xc.numel())
+    check(madnn_gelu_fwd(xc.data_ptr(), y.data_ptr(), xc.numel(), dt_code(xc), (int)kind, cur_stream(xc)), "gelu_fwd");
   return y;
 }
 
@@ -1536,12 +1543,12 @@ TORCH_LIBRARY(madnn, m) {
   m.def("wgrad_splits(int M, int N, int K) -> int", &wgrad_splits);
   m.def("gemmp_supported(int I, int J, int K, bool has_bias) -> bool", &gemmp_supported);
   m.def("linear_fwd_p(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
-  m.def("linear_dgrad_p(Tensor dy, Tensor w, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
+  m.def("linear_dgrad_p(Tensor dy, Tensor w, Tensor? pre, ScalarType bias_dtype, int gelu_kind=1) -> (Tensor, Tensor)");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, bool out_bf16) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
-  m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype) -> (Tensor, Tensor)");
-  m.def("gelu_fwd(Tensor x) -> Tensor");
+  m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype, int gelu_kind=1) -> (Tensor, Tensor)");
+  m.def("gelu_fwd(Tensor x, int kind=1) -> Tensor");
   m.def("rope_qkv_(Tensor(a!) qkv, Tensor cos, Tensor sin, int rot_heads, bool inverse) -> Tensor(a!)");
   m.def("rope_qkv(Tensor qkv, Tensor cos, Tensor sin, int rot_heads, bool inverse) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");

@@ -69,7 +69,7 @@ struct Args {
   int64_t lda, ldb, ldo, ldr, ldx;
   int64_t I, J, K;
   int i_tiles, j_tiles;
-  int bias_f32, act;    // act: 0 none, 1 tanh-GELU
+  int bias_f32, act;    // act: 0 none, 1 tanh-GELU, 2 erf-GELU
   float* ws;            // split-K: fp32 partial slabs [splits][J][I] (null: bf16 epilogue)
   int splits;           // workgroups per output tile along the reduction
   int64_t kper;         // reduction elements per split (multiple of kBK)
@@ -303,7 +303,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const Args p) {
         for (int e = 0; e < 4; ++e) {
           float x0 = bf16_to_f32((unsigned short)(v[e] & 0xffffu));
           float x1 = bf16_to_f32((unsigned short)(v[e] >> 16));
-          if (p.act == 1) {
+          if (p.act == kGeluErf) {
+            x0 = round_bf16(gelu_erf(x0));
+            x1 = round_bf16(gelu_erf(x1));
+          } else if (p.act == kGeluTanh) {
             x0 = round_bf16(gelu_tanh(x0));
             x1 = round_bf16(gelu_tanh(x1));
           }

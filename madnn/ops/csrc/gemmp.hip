@@ -76,7 +76,7 @@ __device__ __forceinline__ u32x4 swap_pairs(unsigned x0, unsigned x1, unsigned y
   return u32x4{d0[0], d1[0], d0[1], d1[1]};
 }
 
-template <bool A_COL, bool B_COL, int EPI>
+template <bool A_COL, bool B_COL, int EPI, int GK = kGeluTanh>
 __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
   // ONE LDS array (cdna_hip_programming.md §5 'Projection GEMM' item 4a): stages + fp32 bias
   __shared__ __attribute__((aligned(16))) uint16_t smem[kLds + 2 * kBiasMax];
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
             const u32x4 d = swap_pairs(pack2(X[0], X[1]), pack2(X[2], X[3]), pack2(Y[0], Y[1]), pack2(Y[2], Y[3]));
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const float v0 = lo16(d[k]) * gelu_tanh_grad(lo16(pv[mm][b][k]));
-              const float v1 = hi16(d[k]) * gelu_tanh_grad(hi16(pv[mm][b][k]));
+              const float v0 = lo16(d[k]) * gelu_act_grad<GK>(lo16(pv[mm][b][k]));
+              const float v1 = hi16(d[k]) * gelu_act_grad<GK>(hi16(pv[mm][b][k]));
               cs[2 * k] += v0;
               cs[2 * k + 1] += v1;
               ov[mm][b][k] = pack2(v0, v1);
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kThreads) void gemmp_kernel(const PArgs p) {
             *reinterpret_cast<u32x4*>(p.aux + (jb + 16 * b) * p.ldo + ib + 32 * m + io) = h;
             u32x4 o;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) o[k] = pack2(gelu_tanh(lo16(h[k])), gelu_tanh(hi16(h[k])));
+            for (int k = 0; k < 4; ++k) o[k] = pack2(gelu_act<GK>(lo16(h[k])), gelu_act<GK>(hi16(h[k])));
             *reinterpret_cast<u32x4*>(dst) = o;
           } else {
             *reinterpret_cast<u32x4*>(dst) = h;
@@ -462,7 +462,7 @@ int num_cus() {
   return g_num_cus;
 }
 
-template <bool A_COL, int EPI>
+template <bool A_COL, int EPI, int GK = kGeluTanh>
 hipError_t launch(PArgs& p, hipStream_t s) {
   p.i_tiles = (int)(p.I / kT);
   p.j_tiles = (int)(p.J / kT);
@@ -470,7 +470,7 @@ hipError_t launch(PArgs& p, hipStream_t s) {
   p.ntile = p.i_tiles * p.j_tiles;
   if (p.ntile <= 0 || (int64_t)p.i_tiles * p.j_tiles > 0x7fffffff) return hipErrorInvalidValue;
   const int grid = p.ntile < num_cus() ? p.ntile : num_cus();
-  hipLaunchKernelGGL((gemmp_kernel<A_COL, false, EPI>), dim3(grid), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL((gemmp_kernel<A_COL, false, EPI, GK>), dim3(grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
 }
 
@@ -478,6 +478,8 @@ hipError_t launch(PArgs& p, hipStream_t s) {
 }  // namespace madnn
 
 using namespace madnn::gemmp;
+using madnn::kGeluErf;
+using madnn::kGeluTanh;
 
 extern "C" {
 
@@ -492,10 +494,12 @@ int madnn_gemmp_supported(int64_t I, int64_t J, int64_t K, int has_bias) {
   return 1;
 }
 
-// Y[m][n] = X[m][k] W[n][k] (+ bias[n]); act 1: aux = that pre-activation, Y = gelu(aux)
+// Y[m][n] = X[m][k] W[n][k] (+ bias[n]); act 1 / 2 (tanh / erf GELU): aux = that pre-activation,
+// Y = gelu(aux)
 hipError_t madnn_linear_fwd_p(const void* x, const void* w, const void* bias, int bias_f32, void* y, void* aux,
                               int act, int64_t M, int64_t N, int64_t K, hipStream_t s) {
-  if (!madnn_gemmp_supported(N, M, K, bias != nullptr) || (act == 1 && aux == nullptr)) return hipErrorInvalidValue;
+  if (!madnn_gemmp_supported(N, M, K, bias != nullptr) || (act != 0 && aux == nullptr) || act < 0 || act > 2)
+    return hipErrorInvalidValue;
   PArgs p{};
   p.a = static_cast<const uint16_t*>(w);
   p.lda = K;
@@ -509,13 +513,16 @@ hipError_t madnn_linear_fwd_p(const void* x, const void* w, const void* bias, in
   p.I = N;
   p.J = M;
   p.K = K;
-  return act == 1 ? launch<false, kGelu>(p, s) : launch<false, kPlain>(p, s);
+  return act == kGeluTanh ? launch<false, kGelu, kGeluTanh>(p, s)
+         : act == kGeluErf ? launch<false, kGelu, kGeluErf>(p, s)
+                           : launch<false, kPlain>(p, s);
 }
 
-// dX[m][k] = dY[m][n] W[n][k]; with pre: dX = that * gelu'(pre) and the fp32 column sums of dX as
+// dX[m][k] = dY[m][n] W[n][k]; with pre: dX = that * gelu'(pre) (gelu_kind 1 tanh / 2 erf) and the
+// fp32 column sums of dX as
 // [M / 256 * 4][K] partial rows in colsum (madnn_colsum_finalize turns them into the bias grad)
 hipError_t madnn_linear_dgrad_p(const void* dy, const void* w, const void* pre, void* dx, float* colsum, int64_t M,
-                                int64_t N, int64_t K, hipStream_t s) {
+                                int64_t N, int64_t K, int gelu_kind, hipStream_t s) {
   if (!madnn_gemmp_supported(K, M, N, 0) || (pre != nullptr && colsum == nullptr)) return hipErrorInvalidValue;
   PArgs p{};
   p.a = static_cast<const uint16_t*>(w);
@@ -529,7 +536,8 @@ hipError_t madnn_linear_dgrad_p(const void* dy, const void* w, const void* pre, 
   p.I = K;
   p.J = M;
   p.K = N;
-  return pre != nullptr ? launch<true, kDGelu>(p, s) : launch<true, kPlain>(p, s);
+  if (pre == nullptr) return launch<true, kPlain>(p, s);
+  return gelu_kind == kGeluErf ? launch<true, kDGelu, kGeluErf>(p, s) : launch<true, kDGelu, kGeluTanh>(p, s);
 }
 
 hipError_t madnn_colsum_finalize(const float* part, int R, int64_t I, void* out, int out_f32, hipStream_t s) {

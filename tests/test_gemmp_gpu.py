@@ -54,17 +54,20 @@ def test_linear_fwd_p_plain_and_bias(cuda, M, N, K):
         assert torch.equal(yb, yb12)
 
 
+@pytest.mark.parametrize("kind,approx", [(1, "tanh"), (2, "none")])
 @pytest.mark.parametrize("M,N,K", SHAPES[1:])
-def test_linear_fwd_p_gelu_epilogue(cuda, M, N, K):
+def test_linear_fwd_p_gelu_epilogue(cuda, M, N, K, kind, approx):
     m = _ops()
     g, x, w = _data(M, N, K, 3 * M + N)
     b = torch.randn(N, device="cuda", generator=g) * 0.5
-    y, pre = m.linear_fwd_p(x, w, b, 1)
+    y, pre = m.linear_fwd_p(x, w, b, kind)
     ref_pre = x.float() @ w.float().t() + b
     torch.testing.assert_close(pre.float(), ref_pre, atol=3e-2, rtol=2e-2)
-    torch.testing.assert_close(y.float(), F.gelu(ref_pre, approximate="tanh"), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(y.float(), F.gelu(ref_pre, approximate=approx), atol=3e-2, rtol=2e-2)
     # the fused epilogue rounds exactly as the standalone K11 GELU pass over the same pre-activation
-    assert torch.equal(y, m.gelu_fwd(pre))
+    assert torch.equal(y, m.gelu_fwd(pre, kind))
+    # and K11 matches F.gelu on the same bf16 input to the output rounding
+    torch.testing.assert_close(y.float(), F.gelu(pre.float(), approximate=approx), atol=1e-2, rtol=8e-3)
 
 
 # data gradient of a Linear(K -> N): dx[M, K] = dy[M, N] w[N, K] (K12P's output features = K)
@@ -89,25 +92,26 @@ def test_linear_dgrad_p_plain(cuda, M, N, K):
     assert torch.equal(dx, m.linear_dgrad(dy, w, None, False))
 
 
+@pytest.mark.parametrize("kind,approx", [(1, "tanh"), (2, "none")])
 @pytest.mark.parametrize("M,N,K", DSHAPES[1:])
 @pytest.mark.parametrize("bias_dtype", [torch.float32, torch.bfloat16])
-def test_linear_dgrad_p_dgelu_colsum(cuda, M, N, K, bias_dtype):
+def test_linear_dgrad_p_dgelu_colsum(cuda, M, N, K, bias_dtype, kind, approx):
     """c_proj's data gradient with c_fc's GELU backward and bias gradient fused: against the fp32
     reference and bitwise against the unfused path (K12 dgrad, then the K11 dGELU + bias pass)."""
     m = _ops()
     g, dy, w = _ddata(M, N, K, 7 * M + N)
     pre = (torch.randn(M, K, device="cuda", generator=g) * 2).bfloat16()
-    dh, db = m.linear_dgrad_p(dy, w, pre, bias_dtype)
+    dh, db = m.linear_dgrad_p(dy, w, pre, bias_dtype, kind)
     da = (dy.float() @ w.float()).bfloat16().float()
     pf = pre.float().requires_grad_(True)
-    F.gelu(pf, approximate="tanh").backward(da)
+    F.gelu(pf, approximate=approx).backward(da)
     ref = pf.grad
     torch.testing.assert_close(dh.float(), ref, atol=4e-2, rtol=3e-2)
     assert db.dtype == bias_dtype and db.shape == (K,)
     torch.testing.assert_close(db.float(), ref.sum(0), atol=2e-1 + 2e-3 * M ** 0.5, rtol=2e-2)
     # unfused: the K12 data gradient, then the K11 dGELU + column-sum pass
     da12 = m.linear_dgrad(dy, w, None, False)
-    db11, dh11 = m.bias_grad(da12, pre, bias_dtype)
+    db11, dh11 = m.bias_grad(da12, pre, bias_dtype, kind)
     assert torch.equal(dh, dh11)
     # same fp32 sums in another order; a bf16 bias gradient may then round one ulp apart
     tol = 1e-4 if bias_dtype == torch.float32 else 8e-3
@@ -126,8 +130,9 @@ def test_gemmp_refuses_edge_tiles(cuda):
         m.linear_fwd_p(x, w, None, 0)
 
 
+@pytest.mark.parametrize("approx", ["tanh", "none"])
 @pytest.mark.parametrize("impl", ["k12p", "lt"])
-def test_gelu_mlp_node_against_fp32(cuda, impl, monkeypatch):
+def test_gelu_mlp_node_against_fp32(cuda, impl, approx, monkeypatch):
     """GPT-2's MLP as one autograd node (ops.gelu_mlp) with the K12P epilogues forced, and with the
     hipBLASLt + K11 path forced: forward and every gradient against fp32 eager autograd."""
     from madnn import ops
@@ -142,13 +147,37 @@ def test_gelu_mlp_node_against_fp32(cuda, impl, monkeypatch):
     b1 = (torch.randn(4 * H, device="cuda") * 0.1).requires_grad_(True)
     w2 = (torch.randn(H, 4 * H, device="cuda") * (4 * H) ** -0.5).bfloat16().requires_grad_(True)
     b2 = (torch.randn(H, device="cuda") * 0.1).requires_grad_(True)
-    y = ops.gelu_mlp(x, w1, b1, w2, b2, r)
+    y = ops.gelu_mlp(x, w1, b1, w2, b2, r, approximate=approx)
     gy = torch.randn_like(y)
     got = torch.autograd.grad(y, (x, w1, b1, w2, b2, r), gy)
     xs = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2, b2, r)]
-    ref_y = F.linear(F.gelu(F.linear(xs[0], xs[1], xs[2]), approximate="tanh"), xs[3], xs[4]) + xs[5]
+    ref_y = F.linear(F.gelu(F.linear(xs[0], xs[1], xs[2]), approximate=approx), xs[3], xs[4]) + xs[5]
     ref = torch.autograd.grad(ref_y, xs, gy.float())
     assert _rel(y, ref_y) < 1e-2
     for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2", "dres"), got, ref):
         assert a.dtype == b.dtype or a.dtype == torch.bfloat16, name
+        assert _rel(a, b) < 2e-2, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("impl", ["k12", "lt"])
+def test_gelu_mlp_erf_on_ragged_rows(cuda, impl, monkeypatch):
+    """Rows that are not a multiple of 256 (no K12P): the exact-GELU MLP on K12's one-tile epilogue
+    (or hipBLASLt + K11) and the K11 erf dGELU pass, against fp32 eager autograd."""
+    from madnn import ops
+
+    monkeypatch.setattr(ops, "GELU_FWD", impl)
+    torch.manual_seed(3)
+    x = torch.randn(300, 256, device="cuda").bfloat16().requires_grad_(True)
+    w1 = (torch.randn(1024, 256, device="cuda") * 256 ** -0.5).bfloat16().requires_grad_(True)
+    b1 = (torch.randn(1024, device="cuda") * 0.1).requires_grad_(True)
+    w2 = (torch.randn(256, 1024, device="cuda") * 1024 ** -0.5).bfloat16().requires_grad_(True)
+    b2 = (torch.randn(256, device="cuda") * 0.1).requires_grad_(True)
+    y = ops.gelu_mlp(x, w1, b1, w2, b2, approximate="none")
+    gy = torch.randn_like(y)
+    got = torch.autograd.grad(y, (x, w1, b1, w2, b2), gy)
+    xs = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    ref_y = F.linear(F.gelu(F.linear(xs[0], xs[1], xs[2])), xs[3], xs[4])
+    ref = torch.autograd.grad(ref_y, xs, gy.float())
+    assert _rel(y, ref_y) < 1e-2
+    for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2"), got, ref):
         assert _rel(a, b) < 2e-2, (name, _rel(a, b))
