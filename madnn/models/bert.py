@@ -87,10 +87,12 @@ class BertLayer(nn.Module):
         y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
         if (self.drop.p == 0.0 or not self.training) and ops.FUSED_LINEAR and type(self.fc1) is nn.Linear \
                 and type(self.fc2) is nn.Linear:
-            # one fused autograd node: the exact GELU and its backward in the two GEMMs' epilogues
-            h = ops.gelu_mlp(y, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, approximate="none")
-        else:
-            h = self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y))))
+            # one fused autograd node: the exact GELU and its backward in the two GEMMs' epilogues, the
+            # residual y added in fc2's epilogue and its gradient inside y's data-gradient GEMM
+            h = ops.gelu_mlp(y, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=y,
+                             approximate="none")
+            return self.ffn_norm(h)
+        h = self.drop(linear(self.fc2, F.gelu(linear(self.fc1, y))))
         z, _ = self.ffn_norm(h, residual=y)
         return z
 

@@ -1727,6 +1727,9 @@ class _GeluMLPFn(torch.autograd.Function):
         ctx.bias_dtype = ctx.b2_dtype   # the output's bias: consumers attach its column sum (_linear_bias_dtype)
         ctx.params = (w1, w2)
         ctx.has_res = residual is not None
+        # the residual IS the input (a post-LN block: y + MLP(y)): its gradient is added inside the
+        # input's data-gradient GEMM (beta = 1) instead of by autograd's accumulation pass
+        ctx.res_is_x = residual is x
         return y
 
     @staticmethod
@@ -1752,6 +1755,9 @@ class _GeluMLPFn(torch.autograd.Function):
             db1 = None
         x2 = x.reshape(-1, x.shape[-1])
         dw1 = _weight_grad(dh, x2, p1) if need[1] else None
+        if ctx.res_is_x and need[0]:
+            dx = torch.addmm(g2, dh, w1).view(*x.shape[:-1], w1.shape[1])
+            return dx, dw1, db1, dw2, db2, None, None
         dx = (dh @ w1).view(*x.shape[:-1], w1.shape[1]) if need[0] else None
         return dx, dw1, db1, dw2, db2, (g if ctx.has_res else None), None
 

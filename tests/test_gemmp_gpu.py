@@ -181,3 +181,25 @@ def test_gelu_mlp_erf_on_ragged_rows(cuda, impl, monkeypatch):
     assert _rel(y, ref_y) < 1e-2
     for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2"), got, ref):
         assert _rel(a, b) < 2e-2, (name, _rel(a, b))
+
+
+def test_gelu_mlp_residual_is_input(cuda):
+    """A post-LN block's ``y + MLP(y)``: the residual is the MLP's own input; its gradient is added
+    inside the input's data-gradient GEMM (beta = 1) -- equal to fp32 eager autograd."""
+    from madnn import ops
+
+    torch.manual_seed(4)
+    x = torch.randn(2, 512, 256, device="cuda").bfloat16().requires_grad_(True)
+    w1 = (torch.randn(1024, 256, device="cuda") * 256 ** -0.5).bfloat16().requires_grad_(True)
+    b1 = (torch.randn(1024, device="cuda") * 0.1).requires_grad_(True)
+    w2 = (torch.randn(256, 1024, device="cuda") * 1024 ** -0.5).bfloat16().requires_grad_(True)
+    b2 = (torch.randn(256, device="cuda") * 0.1).requires_grad_(True)
+    y = ops.gelu_mlp(x, w1, b1, w2, b2, residual=x, approximate="none")
+    gy = torch.randn_like(y)
+    got = torch.autograd.grad(y, (x, w1, b1, w2, b2), gy)
+    xs = [t.detach().float().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    ref_y = F.linear(F.gelu(F.linear(xs[0], xs[1], xs[2])), xs[3], xs[4]) + xs[0]
+    ref = torch.autograd.grad(ref_y, xs, gy.float())
+    assert _rel(y, ref_y) < 1e-2
+    for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2"), got, ref):
+        assert _rel(a, b) < 2e-2, (name, _rel(a, b))
