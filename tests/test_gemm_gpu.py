@@ -18,7 +18,8 @@ def _ops():
 
 
 def _rel(a, b):
-    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
 SHAPES = [(512, 256, 64), (300, 200, 128), (1024, 384, 1024), (777, 1032, 320), (4096, 1024, 4096)]

@@ -20,7 +20,8 @@ def _ops():
 
 
 def _rel(a, b):
-    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
 # (M tokens, N out features, K reduction)

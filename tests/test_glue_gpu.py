@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _rel(a, b):
-    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
 @pytest.mark.parametrize("H,HKV,D,S", [(4, 4, 64, 96), (8, 2, 128, 200), (32, 8, 128, 64)])
