@@ -253,8 +253,10 @@ __device__ __forceinline__ void softmax_tile(f32x16 (&sc)[2], f32x16 (&o)[DB], f
   l += rs;
 }
 
+// D = 128 is built for 2 waves per SIMD (256 VGPRs, a few spills; 348 and one wave unbounded):
+// +27 % at Llama-3 8B's shape, profiles/r5_attn_ab_occupancy.json
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs a) {
+__global__ __launch_bounds__(kThreads, D == 128 ? 2 : 1) void attn_fwd_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t sK[2][kTile * D];
   __shared__ __attribute__((aligned(16))) uint16_t sV[2][kTile * D];
@@ -355,10 +357,14 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const MadnnAttnArgs 
 // so dS = P * acc costs no subtraction (at D = 128 that tuple's 16 registers cost more than the
 // subtraction: -8 %, profiles/r4_ab_attn_valu_trees.log).  delta = rowsum(dO * O) is formed in the
 // prologue and written for the dK/dV kernel.  Two tiles per trip (compile-time LDS buffer index).
+// KSPLIT (D = 128): built for 2 waves per SIMD, the key tile's two 32-key halves run one after the
+// other (one half's S / dP accumulators live) and the LSE is a per-element subtraction: 256 VGPRs
+// (380 and one wave before), backward +11 % at Llama-3 8B's shape (profiles/r5_attn_ab_occupancy.json;
+// at D = 64 the 2-wave build measured neutral).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
+__global__ __launch_bounds__(kThreads, D == 128 ? 2 : 1) void attn_bwd_dq_kernel(const MadnnAttnArgs a) {
   constexpr int DS = D / 16, DB = D / 32;
-  constexpr bool ACCD = D == 64;
+  constexpr bool ACCD = D == 64, KSPLIT = D == 128;
   // K and V stages in one block: after the loop the column-sum epilogue reuses all of it as a
   // [128 rows][D] fp32 image (4 * 64 * D bf16 = 128 * D fp32)
   __shared__ __attribute__((aligned(16))) uint16_t sKV[4][kTile * D];
@@ -392,7 +398,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
     dl += __shfl_xor(dl, 32, kWave);
   }
   const int64_t srow = ((int64_t)b * a.H + h) * a.S + qc;
-  const f32x16 lse16 = splat16(a.lse[srow]);
+  const float lse = a.lse[srow];
+  const f32x16 lse16 = splat16(lse);
   if (hh == 0 && qrow < a.S) a.delta[srow] = dl;
   const uint16_t* kb_ = a.k + b * a.k_sb + hk * a.k_sh;
   const uint16_t* vb_ = a.v + b * a.v_sb + hk * a.v_sh;
@@ -419,7 +426,32 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const MadnnAttnAr
       stv.load(vb_, a.v_ss, (t + 1) * kTile, a.S, tid);
     }
     const int k0 = t * kTile;
-    if (!CAUSAL || k0 <= q0w + 31) {
+    if (KSPLIT && (!CAUSAL || k0 <= q0w + 31)) {
+      // one 32-key half at a time: S, dP, dS and its dQ products, so only one half's accumulators live
+      const bool edge = (k0 + kTile > a.S) || (CAUSAL && k0 + kTile - 1 > q0w);
+      const int lim = (CAUSAL ? min(qrow, a.S - 1) : a.S - 1) - k0 - 4 * hh;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f32x16 sc = zero16(), dp = zero16();
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+          sc = mfma(lds_row<D>(sK[cur], kb * 32 + l32, 2 * s + hh), qf[s], sc);
+          dp = mfma(lds_row<D>(sV[cur], kb * 32 + l32, 2 * s + hh), df[s], dp);
+        }
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sc[r] = (kb * 32 + acc_row(r, 0) <= lim) ? sc[r] : __builtin_inff();
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = ex2(-sc[r] - lse) * (dp[r] - dl);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 sf = pack_acc(sc, s);
+#pragma unroll
+          for (int d = 0; d < DB; ++d) dq[d] = mfma(lds_tr<D>(sK[cur], kb * 32 + 16 * s, d * 32, lane), sf, dq[d]);
+        }
+      }
+    } else if (!CAUSAL || k0 <= q0w + 31) {
       f32x16 sc[2], dp[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
