@@ -434,9 +434,10 @@ static NormCfg pick_cfg(int H) {
 
 // launch grids (A/B knobs, madnn_norm_tune): forward workgroups per CU (grid-stride over rows beyond),
 // backward workgroups per CU (each writes one dgamma/dbeta partial row).  GPT-2 medium A/B at 64 x 1024
-// (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %), forward 8 per CU
-// +0.5 % over 16 (4: -0.1 %)
-static int g_norm_fwd_wg = 8, g_norm_bwd_wg = 4;
+// (profiles/r2_ab_madnn_norm_tune_*.json): backward 4 per CU +0.9 % over 2 (8: +0.7 %).  Forward at the
+// b128 shapes (bench/norm_probe.py, round 5; 98 VGPRs = 5 waves per SIMD resident): 32 per CU 103 us
+// against 8 per CU 113 us at 131072 x 1024 (5.2 vs 4.8 TB/s), 48.5 vs 51.0 us at 65536 x 1024
+static int g_norm_fwd_wg = 32, g_norm_bwd_wg = 4;
 
 extern "C" {
 
