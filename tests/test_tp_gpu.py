@@ -49,7 +49,7 @@ def _w_tp_gpu(rank, world, oneshot=False):
         rl.backward()
         ropt.step()
         ropt.zero_grad()
-        assert abs(float(loss) - float(rl)) < 2e-2 * float(rl), (float(loss), float(rl))
+        assert abs(float(loss) - float(rl.detach())) < 2e-2 * float(rl.detach()), (float(loss), float(rl.detach()))
 
 
 def test_tp2_gpt_on_device(cuda):
