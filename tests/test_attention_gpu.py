@@ -30,6 +30,7 @@ CASES = [
     (1, 77, 3, 3, 64, False),
     (2, 384, 4, 1, 128, True),
     (1, 130, 2, 2, 128, False),
+    (1, 200, 4, 2, 128, True),    # D = 128 dQ key-half split on a ragged causal edge
     (1, 1024, 16, 16, 64, True),
 ]
 
