@@ -5,8 +5,9 @@ torchvision is not installed.  BASELINE config 2:
 The bottleneck 1x1 convolutions (stride 1) run on madnn's K9 MFMA GEMM kernels,
 which also compute the following BatchNorm's batch statistics in their epilogue; the stride-1
 3x3 convolutions run on K13 (MFMA implicit GEMM over an LDS-staged input halo, statistics in the
-epilogue, data grad on the flipped weight); the stride-2 convolutions run on MIOpen through
-PyTorch-ROCm; the 7x7 stem runs on K10 (MFMA
+epilogue, data grad on the flipped weight); the stride-2 3x3 on the 14x14 map runs its forward on
+K13's stride-2 variant (statistics in the epilogue), the larger stride-2 3x3s on MIOpen / CK through
+PyTorch-ROCm (a committed per-shape A/B: profiles/r5_conv3x3_s2_ab.json); the 7x7 stem runs on K10 (MFMA
 forward with the BatchNorm statistics in its epilogue, MFMA weight gradient); the stem max-pool is madnn's
 NHWC kernel (K7, byte argmax + gather backward); every
 BatchNorm is madnn's fused NHWC kernel (K5) with the following ReLU and, at the
@@ -116,7 +117,8 @@ class Bottleneck(nn.Module):
 
     def _bn1_conv2(self, y, st):
         """conv2(relu(bn1(y))): with conv2 on K13, bn1's backward reduction is taken in conv2's
-        data-grad epilogue (ops.bn_relu_conv3x3); the stride-2 conv2s stay on the module path."""
+        data-grad epilogue (ops.bn_relu_conv3x3); the stride-2 conv2s take the module path (K13's stride-2
+        forward on small maps, the library otherwise)."""
         if isinstance(y, torch.Tensor) and isinstance(self.bn1, BN) and isinstance(self.conv2, FusedConv2d) \
                 and self.conv2._k13(y) \
                 and bn_relu_conv3x3_supported(y, self.bn1, self.conv2.weight):

@@ -9,7 +9,8 @@ epilogue, so the BatchNorm skips its statistics pass.  Every other configuration
 ``nn.Conv2d`` (MIOpen on the GPU), except the ResNet stem (7x7, stride 2, pad 3, 3 -> 64
 channels), which runs on K10 (``madnn.ops.stem_conv``, also with the BatchNorm statistics), and
 3x3 / stride 1 / pad 1 convolutions with channel counts that are multiples of 64, which run on K13
-(``madnn.ops.conv3x3``: forward with the statistics, data grad; weight grad on MIOpen).
+(``madnn.ops.conv3x3``: forward with the statistics, data grad; weight grad on MIOpen or K13), and
+3x3 / stride 2 ones on small maps (``madnn.ops.conv3x3_s2``: K13 forward with the statistics).
 ``MADNN_CONV1X1=0`` / ``MADNN_STEM=0`` / ``MADNN_CONV3X3=0`` disable the K9 / K10 / K13 paths
 (A/B runs).
 """
@@ -36,6 +37,11 @@ class FusedConv2d(nn.Conv2d):
                 and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
                 and self.padding_mode == "zeros" and ops.conv3x3_supported(x, self.weight))
 
+    def _k13s2(self, x: torch.Tensor) -> bool:
+        return (self.kernel_size == (3, 3) and self.stride == (2, 2) and self.padding == (1, 1)
+                and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
+                and self.padding_mode == "zeros" and ops.conv3x3_s2_supported(x, self.weight))
+
     def _k10(self, x: torch.Tensor) -> bool:
         return (self.kernel_size == (7, 7) and self.stride == (2, 2) and self.padding == (3, 3)
                 and self.dilation == (1, 1) and self.groups == 1 and self.bias is None
@@ -50,6 +56,8 @@ class FusedConv2d(nn.Conv2d):
             return ops.conv1x1(x, self.weight, stats=stats, fork=fork)
         if not fork and self._k13(x):
             return ops.conv3x3(x, self.weight, stats=stats)
+        if not fork and self._k13s2(x):
+            return ops.conv3x3_s2(x, self.weight, stats=stats)
         if not fork and self._k10(x):
             return ops.stem_conv(x, self.weight, stats=stats)
         out = [super().forward(x)]
@@ -74,5 +82,5 @@ class FusedConv2d(nn.Conv2d):
 
     def extra_repr(self):
         k = {(1, 1): ", kernel=madnn.K9", (7, 7): ", kernel=madnn.K10",
-             (3, 3): ", kernel=madnn.K13" if self.stride == (1, 1) else ""}.get(self.kernel_size, "")
+             (3, 3): ", kernel=madnn.K13" if self.stride in ((1, 1), (2, 2)) else ""}.get(self.kernel_size, "")
         return super().extra_repr() + k

@@ -1153,6 +1153,56 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False):
     return (y, part) if stats else y
 
 
+# K13 at stride 2 (forward with the BN statistics; data / weight gradients on the library): taken up
+# to this input width.  bench/conv3x3_s2_ab.py at ResNet-50's shapes (profiles/r5_conv3x3_s2_ab.json):
+# K13 822 vs 834 us at 14 -> 7 (b2048; 222 vs 241 at b512) and the library needs a statistics pass
+# besides; at 28 -> 14 and 56 -> 28 the taller stride-2 halo leaves K13 one or two workgroups per CU
+# and MIOpen / CK run 38-43 % faster.
+_K13_S2_MAX_W = int(os.environ.get("MADNN_CONV3X3_S2_MAX_W", "16"))
+
+
+def conv3x3_s2_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """The stride-2 / pad-1 3x3 inputs K13 takes (even H and W up to ``MADNN_CONV3X3_S2_MAX_W``)."""
+    if not _K13 or x.device.type != "cuda" or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.numel() == 0:
+        return False
+    if w.dim() != 4 or tuple(w.shape[1:]) != (x.size(1), 3, 3):
+        return False
+    H, W = x.size(2), x.size(3)
+    return (x.size(1) % 64 == 0 and w.size(0) % 64 == 0 and H % 2 == 0 and W % 2 == 0 and 2 <= W <= _K13_S2_MAX_W
+            and H <= 4 * _K13_S2_MAX_W)
+
+
+class _Conv3x3S2Fn(torch.autograd.Function):
+    """3x3 / stride 2 / pad 1 convolution: K13's stride-2 forward (the halo is rows 2r-1 .. 2r+1 of
+    each output row r, still one contiguous NHWC range) with the BatchNorm statistics in its
+    epilogue; both gradients on the library (convolution_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stats):
+        y, part = torch.ops.madnn.conv3x3_fwd_s2(x, _cl(w), bool(stats))
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        dy = _nhwc(dy.to(x.dtype))
+        dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, (2, 2), (1, 1), (1, 1), False, (0, 0), 1,
+                                                        (ctx.needs_input_grad[0], ctx.needs_input_grad[1], False))
+        return dx, dw, None
+
+
+def conv3x3_s2(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False):
+    """``conv2d(x, w, stride=2, padding=1)`` of an NHWC bf16 HIP tensor, forward on K13 (see
+    :func:`conv3x3_s2_supported`); ``stats`` as in :func:`conv3x3`."""
+    _need_native("conv3x3_s2")
+    y, part = _Conv3x3S2Fn.apply(x, w, stats)
+    return (y, part) if stats else y
+
+
 # ---------------------------------------------------------------------- K10
 _K10 = os.environ.get("MADNN_STEM", "1") != "0"
 

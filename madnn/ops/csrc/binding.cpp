@@ -99,6 +99,9 @@ int madnn_gemm_supported(int64_t, int64_t, int64_t, int64_t, int64_t);
 int madnn_conv3x3_supported(int, int, int, int);
 int madnn_conv3x3_stat_rows(int64_t);
 hipError_t madnn_conv3x3_fwd(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
+int madnn_conv3x3_s2_supported(int, int, int, int);
+int madnn_conv3x3_s2_stat_rows(int, int, int);
+hipError_t madnn_conv3x3_fwd_s2(const void*, const void*, void*, float*, int, int, int, int, int, hipStream_t);
 int64_t madnn_conv3x3_wgrad_ws(int, int, int, int, int);
 hipError_t madnn_conv3x3_fwd_bnb(const void*, const void*, void*, float*, const void*, const float*, const float*, int,
                                  int, int, int, int, hipStream_t);
@@ -905,6 +908,28 @@ std::tuple<at::Tensor, at::Tensor> linear_dgrad_p(const at::Tensor& dy, const at
 
 // ---- K13 NHWC 3x3 / stride 1 / pad 1 convolution on MFMA --------------------------------------
 // x: [N, Ci, H, W] channels_last bf16; w: [Co, Ci, 3, 3] channels_last ([Co][3][3][Ci] in memory).
+// stride 2 / pad 1 (K13 SD = 2): y [N, Co, H/2, W/2] channels_last (+ BN statistics partial rows)
+std::tuple<at::Tensor, at::Tensor> conv3x3_fwd_s2(const at::Tensor& x, const at::Tensor& w, bool stats) {
+  check_dev(x, "x");
+  check_dev(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv3x3_s2: bf16 only");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv3x3_s2: x must be NHWC 4-D");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_s2: w must be a channels_last [Co, Ci, 3, 3]");
+  const int N = (int)x.size(0), Ci = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3), Co = (int)w.size(0);
+  TORCH_CHECK(madnn_conv3x3_s2_supported(H, W, Ci, Co), "conv3x3_s2: unsupported shape Ci=", Ci, " Co=", Co, " H=", H,
+              " W=", W);
+  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({N, Co, H / 2, W / 2}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t rows = stats ? madnn_conv3x3_s2_stat_rows(N, H, W) : 0;
+  at::Tensor part = at::empty({rows, 2, Co}, x.options().dtype(at::kFloat));
+  check(madnn_conv3x3_fwd_s2(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, N,
+                             H, W, Ci, Co, cur_stream(x)),
+        "conv3x3_fwd_s2");
+  return {y, part};
+}
+
 std::tuple<at::Tensor, at::Tensor> conv3x3_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
   check_dev(x, "x");
   check_dev(w, "w");
@@ -1545,6 +1570,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("linear_fwd_p(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
   m.def("linear_dgrad_p(Tensor dy, Tensor w, Tensor? pre, ScalarType bias_dtype, int gelu_kind=1) -> (Tensor, Tensor)");
   m.def("conv3x3_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
+  m.def("conv3x3_fwd_s2(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
   m.def("conv3x3_wgrad(Tensor dy, Tensor x, bool out_bf16) -> Tensor");
   m.def("stem_wgrad(Tensor dy, Tensor x) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor? pre, ScalarType bias_dtype, int gelu_kind=1) -> (Tensor, Tensor)");
@@ -1622,6 +1648,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_fwd_p", linear_fwd_p);
   m.impl("linear_dgrad_p", linear_dgrad_p);
   m.impl("conv3x3_fwd", conv3x3_fwd);
+  m.impl("conv3x3_fwd_s2", conv3x3_fwd_s2);
   m.impl("conv3x3_wgrad", conv3x3_wgrad);
   m.impl("hwq_wait", hwq_wait);
   m.impl("hwq_set", hwq_set);

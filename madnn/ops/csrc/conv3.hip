@@ -52,8 +52,10 @@ struct Args {
   const uint16_t* bny;  // BNB epilogue: the BatchNorm input y [M][Co] whose backward sums are taken
   const float* bnsc;    //   its forward scale / shift (ReLU mask = y * sc + sh > 0)
   const float* bnsh;
-  int64_t M;
-  int H, W, Ci, Co;
+  int64_t M;           // output pixels
+  int64_t Min;         // input pixels (= M at stride 1)
+  int H, W, Ci, Co;    // INPUT image height / width
+  int Wo;              // output width (W / SD)
   int halo_px;         // LDS halo capacity in pixels
   int m_tiles, co_tiles;
 };
@@ -73,12 +75,15 @@ struct Chunk {
   static __device__ __forceinline__ int off(int row, int ch) { return row * RB + 16 * (ch ^ f(row)); }
 };
 
-__host__ __device__ inline int halo_rows_px(int W, int rpi) {  // halo capacity in pixels
-  return ((kBJ - 1) / W * W + 4 * W + rpi - 1) / rpi * rpi;
+// halo capacity in pixels: a tile of kBJ output pixels spans at most (kBJ - 1) / Wo + 2 output rows,
+// i.e. SD * ((kBJ - 1) / Wo + 1) + 3 input rows of W pixels (stride 1: (kBJ - 1) / W + 4)
+__host__ __device__ inline int halo_rows_px(int W, int rpi, int sd = 1) {
+  const int Wo = W / sd;
+  return ((sd * ((kBJ - 1) / Wo + 1) + 3) * W + rpi - 1) / rpi * rpi;
 }
 
-__host__ inline size_t conv3x3_lds(int W, int CH) {
-  const size_t rb = 2 * CH, cap = (size_t)halo_rows_px(W, 1024 / (int)rb) * rb + rb + 2 * 64 * rb;
+__host__ inline size_t conv3x3_lds(int W, int CH, int sd = 1) {
+  const size_t rb = 2 * CH, cap = (size_t)halo_rows_px(W, 1024 / (int)rb, sd) * rb + rb + 2 * 64 * rb;
   return cap > 32 * 1024 ? cap : 32 * 1024;  // the epilogue's [256][64] bf16 tile reuses the whole image
 }
 
@@ -86,7 +91,11 @@ __host__ inline size_t conv3x3_lds(int W, int CH) {
 // BatchNorm backward's two sums over its output tile, sum g and sum g*y with g = out * [y*sc+sh > 0]
 // (out = the bf16-rounded input gradient it stores), as the [m_tiles][2][Co] partial rows of
 // bn.hip's backward finalize -- the BN backward then skips its reduction pass over (dx, y).
-template <int CH, bool STATS, bool BNB = false>
+// SD = 2 (ResNet's stride-2 3x3, H and W even): output pixel (n, ho, wo) reads input rows 2 ho - 1 ..
+// 2 ho + 1 -- global output row r maps to global input row 2 r (n H + 2 ho), so a tile's halo is still
+// ONE contiguous NHWC range, rows 2 r_first - 1 .. 2 r_last + 1, and a tap is still a uniform shift
+// of the lane's centre pixel (2 wo in its row); only the halo is about twice as tall.
+template <int CH, bool STATS, bool BNB = false, int SD = 1>
 __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(const Args p) {
   static_assert(!(STATS && BNB), "one statistics epilogue per launch");
   using C = Chunk<CH>;
@@ -106,11 +115,11 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
   const int cot = wid % p.co_tiles, mt = wid / p.co_tiles;
   const int64_t j0 = (int64_t)mt * kBJ;
   const int co0 = cot * kBI;
-  const int W = p.W, H = p.H;
-  const int64_t r_first = j0 / W;
+  const int W = p.W, H = p.H, Wo = SD == 1 ? p.W : p.Wo, Ho = H / SD;
+  const int64_t r_first = j0 / Wo;                     // output rows (global over N x Ho)
   const int64_t j_last = min(j0 + kBJ, p.M) - 1;
-  const int64_t hrow0 = r_first - 1;                   // first halo row (may be -1: clamped, never read)
-  const int hpx = (int)((j_last / W - r_first + 3) * W);  // halo pixels this tile
+  const int64_t hrow0 = SD * r_first - 1;              // first halo row (may be -1: clamped, never read)
+  const int hpx = (int)((SD * (j_last / Wo - r_first) + 3) * W);  // halo pixels this tile
 
   // per-lane output pixels (two 32-pixel blocks of this wave): centre-tap halo index + edge flags
   int hb[2];
@@ -119,10 +128,12 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
   for (int jb = 0; jb < 2; ++jb) {
     int64_t m = j0 + wave * 64 + jb * 32 + l32;
     m = m < p.M ? m : p.M - 1;
-    const int64_t r = m / W;
-    const int wc = (int)(m - r * W);
-    const int h = (int)(r % H);
-    hb[jb] = (int)(r - hrow0) * W + wc;
+    const int64_t r = m / Wo;
+    const int wo = (int)(m - r * Wo);
+    const int ho = (int)(r % Ho);
+    // centre input pixel (SD ho, SD wo); with SD = 2 the row below / column right always exist
+    const int h = SD * ho, wc = SD * wo;
+    hb[jb] = (int)(SD * r - hrow0) * W + wc;
     edge[jb] = (h >= 1 ? 1u : 0u) | (h <= H - 2 ? 2u : 0u) | (wc >= 1 ? 4u : 0u) | (wc <= W - 2 ? 8u : 0u);
   }
   if (tid < C::NC) *reinterpret_cast<u32x4*>(zrow + tid * 8) = u32x4{0u, 0u, 0u, 0u};
@@ -138,7 +149,7 @@ __global__ __launch_bounds__(kThreads, CH == 32 ? 4 : 2) void conv3x3_kernel(con
       const int prow = i * C::RPI + lane / C::NC;
       const int ch = (lane % C::NC) ^ C::f(prow);
       int64_t src = hrow0 * W + prow;
-      src = src < 0 ? 0 : (src >= p.M ? p.M - 1 : src);
+      src = src < 0 ? 0 : (src >= p.Min ? p.Min - 1 : src);
       __builtin_amdgcn_global_load_lds((const void*)(p.x + src * p.Ci + c * CH + 8 * ch),
                                        (lds_void*)(halo + i * 512), 16, 0, 0);
     }
@@ -496,8 +507,10 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
   p.stats = stats;
   p.M = (int64_t)N * H * W;
   if (p.M <= 0) return hipSuccess;
+  p.Min = p.M;
   p.H = H;
   p.W = W;
+  p.Wo = W;
   p.Ci = Ci;
   p.Co = Co;
   const int CH = k13_ch(Ci);
@@ -518,6 +531,49 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
   return hipGetLastError();
 }
 
+// Stride 2 (pad 1): x [N, H, W, Ci] with H, W even -> y [N, H/2, W/2, Co]; stats as above over the
+// output.  The halo is about twice as tall as at stride 1: one workgroup per CU at W = 56 (82 KiB).
+int madnn_conv3x3_s2_supported(int H, int W, int Ci, int Co) {
+  if (H < 2 || W < 2 || (H & 1) || (W & 1) || Ci % 64 || Co % 64 || Ci < 64 || Co < 64 || Ci > 8192) return 0;
+  return conv3x3_lds(W, k13_ch(Ci), 2) <= 160 * 1024 ? 1 : 0;
+}
+
+int madnn_conv3x3_s2_stat_rows(int N, int H, int W) { return (int)(((int64_t)N * (H / 2) * (W / 2) + kBJ - 1) / kBJ); }
+
+hipError_t madnn_conv3x3_fwd_s2(const void* x, const void* w, void* y, float* stats, int N, int H, int W, int Ci,
+                                int Co, hipStream_t s) {
+  if (!madnn_conv3x3_s2_supported(H, W, Ci, Co)) return hipErrorInvalidValue;
+  Args p{};
+  p.x = static_cast<const uint16_t*>(x);
+  p.w = static_cast<const uint16_t*>(w);
+  p.y = static_cast<uint16_t*>(y);
+  p.stats = stats;
+  p.M = (int64_t)N * (H / 2) * (W / 2);
+  if (p.M <= 0) return hipSuccess;
+  p.Min = (int64_t)N * H * W;
+  p.H = H;
+  p.W = W;
+  p.Wo = W / 2;
+  p.Ci = Ci;
+  p.Co = Co;
+  const int CH = k13_ch(Ci);
+  p.halo_px = halo_rows_px(W, 1024 / (2 * CH), 2);
+  p.m_tiles = (int)((p.M + kBJ - 1) / kBJ);
+  p.co_tiles = Co / kBI;
+  const int64_t grid = (int64_t)p.m_tiles * p.co_tiles;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  const size_t lds = conv3x3_lds(W, CH, 2);
+  const dim3 g((unsigned)grid), b(kThreads);
+  if (CH == 32) {
+    if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true, false, 2>), g, b, lds, s, p);
+    else hipLaunchKernelGGL((conv3x3_kernel<32, false, false, 2>), g, b, lds, s, p);
+  } else {
+    if (stats) hipLaunchKernelGGL((conv3x3_kernel<64, true, false, 2>), g, b, lds, s, p);
+    else hipLaunchKernelGGL((conv3x3_kernel<64, false, false, 2>), g, b, lds, s, p);
+  }
+  return hipGetLastError();
+}
+
 // Data grad with the BatchNorm-backward sums in the epilogue (see BNB): x = the output gradient,
 // w = the flipped / transposed weight, y = dx; partial [ceil(M/256)][2][Co] = (sum g, sum g*bny)
 hipError_t madnn_conv3x3_fwd_bnb(const void* x, const void* w, void* y, float* partial, const void* bny,
@@ -534,8 +590,10 @@ hipError_t madnn_conv3x3_fwd_bnb(const void* x, const void* w, void* y, float* p
   p.bnsh = bnsh;
   p.M = (int64_t)N * H * W;
   if (p.M <= 0) return hipSuccess;
+  p.Min = p.M;
   p.H = H;
   p.W = W;
+  p.Wo = W;
   p.Ci = Ci;
   p.Co = Co;
   const int CH = k13_ch(Ci);

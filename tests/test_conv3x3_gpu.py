@@ -54,6 +54,63 @@ def test_conv3x3_exact_small_integers():
     assert torch.equal(y, F.conv2d(x.float(), w.float(), None, 1, 1).bfloat16())
 
 
+# stride 2 (SD = 2): ResNet-50's three stride-2 3x3 shapes, tiles spanning image seams, tiny images
+S2_SHAPES = [(2, 128, 128, 56, 56), (3, 256, 256, 28, 28), (4, 512, 512, 14, 14), (5, 64, 128, 8, 6),
+             (3, 64, 64, 2, 2)]
+
+
+@pytest.mark.parametrize("N,Ci,Co,H,W", S2_SHAPES)
+def test_conv3x3_stride2_fwd_and_stats(N, Ci, Co, H, W):
+    _ops()
+    g = torch.Generator(device="cuda").manual_seed(N * 10 + Ci + W)
+    x = _cl(torch.randn(N, Ci, H, W, device="cuda", generator=g).bfloat16())
+    w = _cl((torch.randn(Co, Ci, 3, 3, device="cuda", generator=g) * (9 * Ci) ** -0.5).bfloat16())
+    y, part = torch.ops.madnn.conv3x3_fwd_s2(x, w, True)
+    ref = F.conv2d(x.float(), w.float(), None, 2, 1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    yf = y.float()
+    s = part.sum(0)
+    torch.testing.assert_close(s[0], yf.sum((0, 2, 3)), atol=1e-2 * yf.numel() ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(s[1], (yf * yf).sum((0, 2, 3)), atol=1e-2 * yf.numel() ** 0.5, rtol=1e-3)
+
+
+def test_conv3x3_stride2_exact_small_integers():
+    """Exact integer arithmetic: the stride-2 taps / halo rows / image seams bit for bit."""
+    _ops()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    N, Ci, Co, H, W = 3, 128, 64, 12, 10
+    x = _cl(torch.randint(-2, 3, (N, Ci, H, W), device="cuda", generator=g).bfloat16())
+    w = _cl(torch.randint(-1, 2, (Co, Ci, 3, 3), device="cuda", generator=g).bfloat16())
+    w[:, :, 2, 0] += 1  # asymmetric kernel
+    y, _ = torch.ops.madnn.conv3x3_fwd_s2(x, w, False)
+    assert torch.equal(y, F.conv2d(x.float(), w.float(), None, 2, 1).bfloat16())
+
+
+def test_conv3x3_stride2_module_path_autograd():
+    """FusedConv2d(stride 2) on a 14x14 map routes its forward to K13's stride-2 kernel (statistics
+    included); output, dx and dw match an fp32 nn.Conv2d."""
+    ops = _ops()
+    from madnn.nn.conv import FusedConv2d
+
+    torch.manual_seed(7)
+    conv = FusedConv2d(128, 128, 3, stride=2, padding=1, bias=False).cuda().bfloat16()
+    conv = conv.to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(4, 128, 14, 14, device="cuda").bfloat16()).requires_grad_(True)
+    assert conv._k13s2(x) and ops.conv3x3_s2_supported(x, conv.weight)
+    y, part = conv(x, stats=True)
+    assert part is not None and part.shape[1:] == (2, 128)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xf = x.detach().float().requires_grad_(True)
+    wf = conv.weight.detach().float().requires_grad_(True)
+    ref = F.conv2d(xf, wf, None, 2, 1)
+    ref.backward(g.float())
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    for a, b in ((x.grad, xf.grad), (conv.weight.grad, wf.grad)):
+        assert float((a.float() - b).norm() / b.norm()) < 1e-2
+
+
 @pytest.mark.parametrize("N,Ci,Co,H,W", [(2, 64, 64, 56, 56), (3, 128, 64, 14, 14), (2, 64, 128, 7, 9)])
 def test_conv3x3_autograd(N, Ci, Co, H, W):
     ops = _ops()
