@@ -42,7 +42,7 @@ def test_resnet18_dp_bf16_tracks_fp32_eager(cuda):
         rl.backward()
         ropt.step()
         ropt.zero_grad()
-        assert abs(float(loss) - float(rl.detach())) < 0.05 * max(1.0, float(rl.detach())), (step, float(loss), float(rl.detach()))
+        assert abs(float(loss.detach()) - float(rl.detach())) < 0.05 * max(1.0, float(rl.detach())), (step, float(loss.detach()), float(rl.detach()))
     # BN running stats updated by the fused kernel match eager within bf16 noise (after 4 bf16
     # SGD steps single channels drift by up to ~0.07 from the fp32 run; MIOpen's weight-grad
     # solvers accumulate with atomics, so the exact drift varies run to run)
