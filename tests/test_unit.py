@@ -890,3 +890,26 @@ def test_swiglu_eager_path():
     gu = torch.randn(3, 5, 32)
     g, u = gu.chunk(2, -1)
     torch.testing.assert_close(ops.swiglu(gu), torch.nn.functional.silu(g) * u)
+
+
+def test_fused_conv2d_stride2_3x3_routes_to_library_on_cpu_and_matches_conv2d():
+    """FusedConv2d's stride-2 3x3 (K13 SD = 2 on the GPU for small maps) is nn.Conv2d on CPU tensors:
+    same output and gradients, and the K13 predicates refuse CPU inputs."""
+    from madnn import ops
+    from madnn.nn.conv import FusedConv2d
+
+    torch.manual_seed(0)
+    conv = FusedConv2d(64, 64, 3, stride=2, padding=1, bias=False)
+    ref = torch.nn.Conv2d(64, 64, 3, stride=2, padding=1, bias=False)
+    ref.load_state_dict(conv.state_dict())
+    x = torch.randn(2, 64, 14, 14, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    assert not conv._k13s2(x) and not ops.conv3x3_s2_supported(x, conv.weight)
+    y, part = conv(x, stats=True)
+    assert part is None
+    yr = ref(xr)
+    torch.testing.assert_close(y, yr)
+    y.sum().backward()
+    yr.sum().backward()
+    torch.testing.assert_close(x.grad, xr.grad)
+    assert "K13" in conv.extra_repr()
