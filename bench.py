@@ -42,9 +42,13 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-import torch.nn.functional as F
+# the hosts' drivers support only dmabuf IPC: RCCL's cross-process buffers need the non-legacy mode,
+# set before the HSA runtime initialises (a launcher that exports it already wins)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 
 METRIC = "samples/sec whole-node ResNet-50 DP + GPT-2 PP at 1/2/4/8 MI355X; scaling eff"
 
