@@ -302,3 +302,43 @@ def test_resume_on_larger_tp_mesh_keeps_tp_groups_on_one_rng_stream(tmp_path, mo
     # ... the saved replica keeps its own, the new replica gets a different one
     assert torch.equal(state_at(0, 3), shared)
     assert not torch.equal(state_at(1, 0), shared)
+
+
+def _w_pp_plain_opt_resume(rank, world, path, phase):
+    """Pipeline engine + plain torch AdamW: save after 2 steps, then either keep training (phase
+    "save", losses kept) or resume a fresh replica from the checkpoint (phase "resume"): the next
+    steps' losses must match -- weights AND the AdamW moments come back through the checkpoint."""
+    import madnn
+    from madnn import ckpt
+
+    torch.manual_seed(0 if phase == "save" else 42)
+    m = _gpt()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-2, weight_decay=0.01)
+    eng, opt = madnn.distribute(m, opt, strategy="pp", pp_stages=world, microbatches=2,
+                                example_input=_data()[0][:1], checkpointing="none")
+    assert isinstance(opt, torch.optim.AdamW)
+    x, y = _data()
+
+    def step():
+        loss = eng.train_step(x, y)
+        opt.step()
+        opt.zero_grad()
+        return torch.as_tensor(float(loss) if loss is not None else 0.0)
+
+    mine = os.path.join(path, f"plain-losses-{rank}.pt")
+    if phase == "save":
+        step()
+        step()
+        ckpt.save(path, eng, opt, step=2)
+        torch.save(torch.stack([step() for _ in range(3)]), mine)
+        return
+    ckpt.load(path, eng, opt)
+    got = torch.stack([step() for _ in range(3)])
+    want = torch.load(mine, weights_only=True)
+    torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
+
+
+def test_pp_plain_optimizer_checkpoint_resume(tmp_path):
+    path = str(tmp_path / "pp_plain")
+    run_dist(_w_pp_plain_opt_resume, 2, path, "save")
+    run_dist(_w_pp_plain_opt_resume, 2, path, "resume")
