@@ -84,9 +84,15 @@ class BertLayer(nn.Module):
         return [(("fc1",), "fc2")]
 
     def forward(self, x):
-        y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
-        if (self.drop.p == 0.0 or not self.training) and ops.FUSED_LINEAR and type(self.fc1) is nn.Linear \
-                and type(self.fc2) is nn.Linear:
+        fused = (self.drop.p == 0.0 or not self.training) and ops.FUSED_LINEAR
+        if fused and type(self.attn) is SelfAttention:
+            # LN(x + attn(x)): x's residual gradient is summed inside the QKV projection's data-gradient
+            # GEMM (ops.linear_tee), not by a separate pass over x's two gradients
+            a, xr = self.attn.forward_tee(x)
+            y, _ = self.attn_norm(a, residual=xr)
+        else:
+            y, _ = self.attn_norm(self.drop(self.attn(x)), residual=x)
+        if fused and type(self.fc1) is nn.Linear and type(self.fc2) is nn.Linear:
             # one fused autograd node: the exact GELU and its backward in the two GEMMs' epilogues, the
             # residual y added in fc2's epilogue and its gradient inside y's data-gradient GEMM
             h = ops.gelu_mlp(y, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, residual=y,

@@ -62,7 +62,20 @@ class SelfAttention(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         b, s, _ = x.shape
-        qkv = linear(self.qkv, x).view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
+        return self.attend(linear(self.qkv, x), b, s)
+
+    def forward_tee(self, x: torch.Tensor):
+        """``(attn(x), x')``: the QKV projection through :func:`ops.linear_tee`, so a residual path
+        that uses ``x'`` has its gradient summed inside the projection's data-gradient GEMM."""
+        b, s, _ = x.shape
+        if ops.FUSED_LINEAR and type(self.qkv) is nn.Linear:
+            qkv, xr = ops.linear_tee(x, self.qkv.weight, self.qkv.bias)
+            return self.attend(qkv, b, s), xr
+        return self.forward(x), x
+
+    def attend(self, qkv: torch.Tensor, b: int, s: int) -> torch.Tensor:
+        """Attention and the output projection on the QKV projection's output ``[b, s, (H + 2 Hkv) D]``."""
+        qkv = qkv.view(b, s, self.heads + 2 * self.kv_heads, self.head_dim)
         drop = self.dropout if self.training else 0.0
         if ops.attention_supported(qkv, self.head_dim, drop):
             # K8 HIP attention on the [B, S, heads, D] layout the projection produced: no

@@ -1743,6 +1743,62 @@ def _linear_residual_fwd(a: torch.Tensor, weight, bias, residual):
     return y + residual if residual is not None else y
 
 
+def _dgrad_plus(g2: torch.Tensor, weight: torch.Tensor, res2: torch.Tensor) -> torch.Tensor:
+    """``g2 @ weight + res2`` (a data gradient plus a residual path's gradient) as ONE hipBLASLt GEMM
+    with the residual epilogue reading res2 as its C operand -- the weight transposed into a small
+    contiguous copy (a few MB) instead of ``addmm``'s copy of res2 into the output (rows x features)."""
+    if _lt_ok(g2, weight, False, True) and g2.is_contiguous():
+        out = _lt_linear(g2, weight.t().contiguous(), None, res2.contiguous().to(g2.dtype), False)
+        if out is not None:
+            return out[0]
+    return torch.addmm(res2.to(g2.dtype), g2, weight)
+
+
+class _LinearTeeFn(torch.autograd.Function):
+    """``(x W^T + b, x)``: a Linear whose input also feeds a residual path (BERT's post-LN attention
+    sublayer, LN(x + attn(x))).  Both uses of x are this node, so the residual's gradient (the second
+    output's) joins the data-gradient GEMM as its C operand (beta = 1) instead of a separate
+    accumulation pass over x's two gradients.  Bias gradient and weight gradient as _LinearFn."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.param = weight
+        ctx.save_for_backward(x, weight)
+        return _linear_residual_fwd(x, weight, bias, None), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g, gx):
+        x, weight = ctx.saved_tensors
+        db = None
+        if ctx.bias_dtype is not None and ctx.needs_input_grad[2]:
+            cs = _attached(g, "_madnn_colsum")  # the attention backward's dQKV column sums
+            if cs is not None and cs.numel() == g.shape[-1]:
+                db = cs.to(ctx.bias_dtype)
+            else:
+                db, _ = bias_grad(g, None, ctx.bias_dtype)
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if gx is None:
+                dx = g2 @ weight
+            else:
+                dx = _dgrad_plus(g2, weight, gx.reshape(-1, weight.shape[1]))
+            dx = dx.view(*x.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = _weight_grad(g2, x.reshape(-1, x.shape[-1]), ctx.param)
+        ctx.param = None
+        return dx, dw, db
+
+
+def linear_tee(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
+    """``(F.linear(x, weight, bias), x')`` where ``x'`` is ``x`` for a residual path whose gradient
+    is summed inside this Linear's data-gradient GEMM (:class:`_LinearTeeFn`); eager on CPU."""
+    if not torch.is_grad_enabled() or not _is_dev(x) or weight.shape[0] % 8:
+        return F.linear(x, weight, bias if bias is None or bias.dtype == x.dtype else bias.to(x.dtype)), x
+    return _LinearTeeFn.apply(x, weight, bias)
+
+
 def _weight_grad(g2: torch.Tensor, x2: torch.Tensor, param: torch.Tensor) -> torch.Tensor:
     """A Linear's weight gradient, written into the reducer's bucket slot when it has one."""
     sink = grad_sink(param)
@@ -1806,7 +1862,7 @@ class _GeluMLPFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         dw1 = _weight_grad(dh, x2, p1) if need[1] else None
         if ctx.res_is_x and need[0]:
-            dx = torch.addmm(g2, dh, w1).view(*x.shape[:-1], w1.shape[1])
+            dx = _dgrad_plus(dh, w1, g2).view(*x.shape[:-1], w1.shape[1])
             return dx, dw1, db1, dw2, db2, None, None
         dx = (dh @ w1).view(*x.shape[:-1], w1.shape[1]) if need[0] else None
         return dx, dw1, db1, dw2, db2, (g if ctx.has_res else None), None

@@ -204,3 +204,30 @@ def test_gelu_mlp_residual_is_input(cuda):
     assert _rel(y, ref_y) < 1e-2
     for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2"), got, ref):
         assert _rel(a, b) < 2e-2, (name, _rel(a, b))
+
+
+def test_bert_layer_residual_tee_matches_eager(cuda, monkeypatch):
+    """BERT's post-LN sublayers with both residual gradients folded into data-gradient GEMMs (attention:
+    ops.linear_tee on the QKV projection; MLP: gelu_mlp(residual=y)) vs the same model with the fused
+    Linear paths off: loss and every gradient agree (bf16)."""
+    from madnn import ops
+    from madnn.models.bert import BertForPreTraining, bert_config
+
+    torch.manual_seed(3)
+    cfg = bert_config("bert-tiny", hidden=256, heads=4, intermediate=512, layers=2)
+    model = BertForPreTraining(cfg).to(cuda).bfloat16()
+    ids = torch.randint(0, cfg.vocab_size, (2, 128), device=cuda)
+    calls = []
+    real = ops._LinearTeeFn.apply
+    monkeypatch.setattr(ops._LinearTeeFn, "apply", lambda *a: calls.append(1) or real(*a))
+    loss = model.loss_fn(model(ids), ids)
+    loss.backward()
+    assert len(calls) == cfg.layers
+    got = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    model.zero_grad()
+    monkeypatch.setattr(ops, "FUSED_LINEAR", False)
+    loss2 = model.loss_fn(model(ids), ids)
+    loss2.backward()
+    torch.testing.assert_close(loss.float(), loss2.float(), atol=2e-2, rtol=2e-2)
+    for n, p in model.named_parameters():
+        assert _rel(got[n], p.grad) < 5e-2, (n, _rel(got[n], p.grad))

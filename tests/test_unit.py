@@ -913,3 +913,28 @@ def test_fused_conv2d_stride2_3x3_routes_to_library_on_cpu_and_matches_conv2d():
     yr.sum().backward()
     torch.testing.assert_close(x.grad, xr.grad)
     assert "K13" in conv.extra_repr()
+
+
+def test_linear_tee_sums_the_residual_gradient_in_the_data_gradient():
+    """ops._LinearTeeFn: (x W^T + b, x) with dx = dy W + d(residual) from one addmm, dW, db as eager."""
+    from madnn import ops
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, requires_grad=True)
+    w = torch.randn(24, 16, requires_grad=True)
+    b = torch.randn(24, requires_grad=True)
+    y, xr = ops._LinearTeeFn.apply(x, w, b)
+    gy, gr = torch.randn_like(y), torch.randn_like(xr)
+    (y * gy).sum().add((xr * gr).sum()).backward()
+    xe, we, be = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    ye = torch.nn.functional.linear(xe, we, be)
+    (ye * gy).sum().add((xe * gr).sum()).backward()
+    torch.testing.assert_close(y, ye)
+    torch.testing.assert_close(xr, x)
+    for a, e in ((x.grad, xe.grad), (w.grad, we.grad), (b.grad, be.grad)):
+        torch.testing.assert_close(a, e, atol=1e-5, rtol=1e-5)
+    # the residual output unused: dx is the projection's data gradient alone
+    x.grad = None
+    y, _ = ops._LinearTeeFn.apply(x, w, b)
+    (y * gy).sum().backward()
+    torch.testing.assert_close(x.grad, gy.reshape(-1, 24).mm(w.detach()).view_as(x), atol=1e-5, rtol=1e-5)
