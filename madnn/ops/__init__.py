@@ -214,7 +214,7 @@ def _linear_bias_dtype(x: torch.Tensor):
     gf = x.grad_fn
     if gf is not None and type(gf).__name__ in _VIEW_NODES and len(gf.next_functions) == 1:
         gf = gf.next_functions[0][0]
-    if gf is None or type(gf).__name__ not in ("_LinearFnBackward", "_GeluMLPFnBackward"):
+    if gf is None or type(gf).__name__ not in ("_LinearFnBackward", "_GeluMLPFnBackward", "_LinearTeeFnBackward"):
         return None
     return getattr(gf, "bias_dtype", None)
 
@@ -1743,14 +1743,20 @@ def _linear_residual_fwd(a: torch.Tensor, weight, bias, residual):
     return y + residual if residual is not None else y
 
 
+_LT_KN_FAILED = []  # the [K, N]-weight residual GEMM was refused once: addmm from then on
+
+
 def _dgrad_plus(g2: torch.Tensor, weight: torch.Tensor, res2: torch.Tensor) -> torch.Tensor:
     """``g2 @ weight + res2`` (a data gradient plus a residual path's gradient) as ONE hipBLASLt GEMM
-    with the residual epilogue reading res2 as its C operand -- the weight transposed into a small
-    contiguous copy (a few MB) instead of ``addmm``'s copy of res2 into the output (rows x features)."""
-    if _lt_ok(g2, weight, False, True) and g2.is_contiguous():
-        out = _lt_linear(g2, weight.t().contiguous(), None, res2.contiguous().to(g2.dtype), False)
-        if out is not None:
-            return out[0]
+    reading the [out, in] weight as it is stored (op N) and res2 as its C operand -- not ``addmm``,
+    which first copies res2 (rows x features) into its output."""
+    if not _LT_KN_FAILED and _lt_ok(g2, weight, False, True) and g2.is_contiguous():
+        try:
+            y, _ = _need_native("lt_linear").lt_linear(g2, weight, None, res2.contiguous().to(g2.dtype), False, False,
+                                                       True)
+            return y
+        except RuntimeError as e:  # noqa: PERF203 - once
+            _LT_KN_FAILED.append(e)
     return torch.addmm(res2.to(g2.dtype), g2, weight)
 
 

@@ -57,19 +57,20 @@ struct Plan {
   size_t ws = 0;
 };
 
-using Key = std::tuple<int64_t, int64_t, int64_t, int, int, int, int, int, size_t>;
+using Key = std::tuple<int64_t, int64_t, int64_t, int, int, int, int, int, size_t>;  // [7]: w given [K, N]
 std::map<Key, Plan> g_plans;
 std::mutex g_mu;
 
 Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEpilogue_t epi, hipDataType dt,
-               hipDataType bias_dt, bool has_c, size_t ws_cap, const void* bias_ptr, void* aux_ptr) {
-  Key key{M, N, K, (int)epi, (int)dt, (int)bias_dt, (int)has_c, 0, ws_cap};
+               hipDataType bias_dt, bool has_c, size_t ws_cap, const void* bias_ptr, void* aux_ptr,
+               bool w_kn = false) {
+  Key key{M, N, K, (int)epi, (int)dt, (int)bias_dt, (int)has_c, w_kn ? 1 : 0, ws_cap};
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_plans.find(key);
   if (it != g_plans.end()) return it->second;
   Plan p;
   LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
-  hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  hipblasOperation_t ta = w_kn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
@@ -86,7 +87,11 @@ Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEp
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux_ptr,
                                              sizeof(aux_ptr)));
   }
-  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt, K, N, K));  // W: K x N col-major, op T
+  if (w_kn) {
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt, N, K, N));  // W [K, N] row-major: N x K col-major, op N
+  } else {
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt, K, N, K));  // W [N, K] row-major: K x N col-major, op T
+  }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, dt, K, M, K));  // X: K x M col-major
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.c, dt, N, M, N));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p.d, dt, N, M, N));
@@ -106,15 +111,17 @@ Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEp
 }
 
 // x [M, K], w [N, K] (both contiguous, same dtype), bias [N] or None, residual [M, N] or None.
+// w_kn: w is given as [K, N] instead (y = x @ w, e.g. a Linear's data gradient dy @ W, no transposed copy).
 // Returns (y [M, N], pre [M, N] when gelu && want_pre, else an empty tensor).
 std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tensor& w,
                                              const c10::optional<at::Tensor>& bias,
-                                             const c10::optional<at::Tensor>& residual, bool gelu, bool want_pre) {
+                                             const c10::optional<at::Tensor>& residual, bool gelu, bool want_pre,
+                                             bool w_kn) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 2 && w.dim() == 2, "lt_linear: 2-D HIP tensors");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "lt_linear: contiguous x and w");
   TORCH_CHECK(x.scalar_type() == w.scalar_type(), "lt_linear: x and w dtypes differ");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K, "lt_linear: shape mismatch");
+  const int64_t M = x.size(0), K = x.size(1), N = w_kn ? w.size(1) : w.size(0);
+  TORCH_CHECK((w_kn ? w.size(0) : w.size(1)) == K, "lt_linear: shape mismatch");
   const bool has_bias = bias.has_value() && bias->defined();
   const bool has_res = residual.has_value() && residual->defined();
   if (has_bias) TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "lt_linear: bias [N]");
@@ -138,7 +145,7 @@ std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tens
   at::Tensor pre;
   if (gelu && want_pre) pre = at::empty({M, N}, x.options());
   Plan& p = get_plan(h, M, N, K, epi, dt, bdt, has_res, ws_cap, has_bias ? bias->data_ptr() : nullptr,
-                     pre.defined() ? pre.data_ptr() : nullptr);
+                     pre.defined() ? pre.data_ptr() : nullptr, w_kn);
   if (has_bias) {
     const void* bp = bias->data_ptr();
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
@@ -207,7 +214,7 @@ int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(madnn, m) {
-  m.def("lt_linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu, bool want_pre) -> (Tensor, Tensor)");
+  m.def("lt_linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu, bool want_pre, bool w_kn=False) -> (Tensor, Tensor)");
   // no tensor arguments -> nothing to dispatch on: a catch-all kernel
   m.def("lt_probe(int M, int N, int K, int epi, int bias_code, int aux_code, bool has_c, int dummy_ptr) -> int",
         TORCH_FN(lt_probe));

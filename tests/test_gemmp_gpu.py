@@ -231,3 +231,20 @@ def test_bert_layer_residual_tee_matches_eager(cuda, monkeypatch):
     torch.testing.assert_close(loss.float(), loss2.float(), atol=2e-2, rtol=2e-2)
     for n, p in model.named_parameters():
         assert _rel(got[n], p.grad) < 5e-2, (n, _rel(got[n], p.grad))
+
+
+@pytest.mark.parametrize("M,O,I", [(4096, 3072, 1024), (1000, 1024, 4096)])
+def test_dgrad_plus_kn_weight_gemm_matches_fp32(cuda, M, O, I):
+    """ops._dgrad_plus: g @ W + r as one hipBLASLt GEMM reading W [O, I] untransposed (op N) with r as
+    the C operand, vs fp32."""
+    from madnn import ops
+
+    torch.manual_seed(5)
+    g = torch.randn(M, O, device=cuda).bfloat16()
+    w = (torch.randn(O, I, device=cuda) * O ** -0.5).bfloat16()
+    r = torch.randn(M, I, device=cuda).bfloat16()
+    out = ops._dgrad_plus(g, w, r)
+    assert not ops._LT_KN_FAILED, ops._LT_KN_FAILED
+    ref = g.float() @ w.float() + r.float()
+    assert out.dtype == torch.bfloat16 and out.shape == (M, I)
+    assert _rel(out, ref) < 1e-2
