@@ -49,5 +49,5 @@ def test_hf_model_runs_madnn_kernels(cuda, kind):
         rl.backward()
         ropt.step()
         ropt.zero_grad()
-        assert abs(float(loss) - float(rl.detach())) < 3e-2 * float(rl.detach()), (kind, step, float(loss), float(rl.detach()))
+        assert abs(float(loss.detach()) - float(rl.detach())) < 3e-2 * float(rl.detach()), (kind, step, float(loss.detach()), float(rl.detach()))
     assert attention_stats()["k8"] > before, "attention did not run on K8"
