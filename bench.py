@@ -38,6 +38,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -301,8 +302,12 @@ def bench_gpt2(args, world, rank):
     ids = torch.randint(0, cfg.vocab_size, (per_replica if stages > 1 else gbatch // world, args.seq_len),
                         generator=g).to(dev)
 
+    accum = {"microbatches": args.microbatches} if stages == 1 and args.microbatches else {}
+
     def step():
-        loss = engine.train_step(ids, ids)
+        # 1 GPU: --microbatches M accumulates M microbatches under no_sync, as a pipeline rank
+        # computes its share of the step
+        loss = engine.train_step(ids, ids, **accum)
         opt.step()
         return loss
 
@@ -321,18 +326,45 @@ def bench_gpt2(args, world, rank):
         loss = step()
     _sync_all()
     dt = time.perf_counter() - t0
-    lv = None
-    if loss is not None and (stages == 1 or rank % stages == stages - 1):
-        lv = float(loss.detach())
+    lv = float(loss.detach()) if loss is not None else float("-inf")
+    if stages > 1 and dist.is_initialized():   # the last stage holds it: bring it to rank 0
+        t = torch.tensor([lv], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lv = float(t.item())
+    lv = None if lv == float("-inf") else lv
+    held = _heldout_loss(engine, model, cfg.vocab_size, ids.shape, 98765 + rank // stages, stages, rank)
     info = {"model": args.gpt2_config, "global_batch": gbatch, "per_gpu_batch": args.gpt2_batch_per_gpu,
             "seq_len": args.seq_len, "parallelism": par, "microbatches": getattr(engine, "M", 1) if stages > 1 else 1,
             "planned_step_ms": round(engine.plan.est_step_s * 1e3, 2) if getattr(engine, "plan", None) else None,
             "schedule": getattr(engine, "schedule", None) if stages > 1 else None,
             "virtual_stages": getattr(engine, "V", None) if stages > 1 else None,
             "optimizer": "FusedAdam", "steps": steps, "warmup": warm, "plan_tuning_steps": extra,
-            "loss_last_stage": lv,
+            "loss_last_stage": lv, "heldout_loss": held, "ln_vocab": round(math.log(cfg.vocab_size), 4),
+            "accum_microbatches": args.microbatches if stages == 1 and args.microbatches else None,
             "peak_mem_gib": _peak_gib(), "plan": _plan_info(plan), **_comm_fields(engine, plan)}
     return dt, steps, gbatch, info
+
+
+def _heldout_loss(engine, model, vocab: int, shape, seed: int, stages: int, rank: int):
+    """The loss on a fresh random token batch the model never trained on: forward only, outside
+    the timed region (the reference scores its trained net on held-out data,
+    cifar_example/sgd-torchad_nn-cifar.lua:266-275).  Next to a low training loss on the one
+    repeated batch, a held-out loss near ln(V) says the model memorised it; a low held-out loss
+    on a causal model would mean it sees the tokens it predicts.  Pipeline: every rank joins the
+    forward, the last stage's value reaches rank 0 (MAX all-reduce)."""
+    import madnn
+
+    dev = madnn.device()
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ids = torch.randint(0, vocab, tuple(shape), generator=g).to(dev)
+    with torch.no_grad():
+        out = engine.forward_step(ids) if stages > 1 else engine(ids)
+        lv = float(model.loss_fn(out, ids)) if out is not None else float("-inf")
+    if stages > 1 and dist.is_initialized():
+        t = torch.tensor([lv], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lv = float(t.item())
+    return round(lv, 4) if lv != float("-inf") else None
 
 
 TF_METRIC = {"bert-large": "tokens/s BERT-large auto-partition + activation checkpointing + fused Adam (BASELINE "
@@ -398,6 +430,7 @@ def bench_transformer(args, world, rank):
     _sync_all()
     dt = _max_over_ranks(time.perf_counter() - t0)
     lv = float(loss.detach()) if loss is not None else None
+    held = _heldout_loss(engine, model, cfg.vocab_size, ids.shape, 98765 + replica, stages, rank)
     ck = sum(bool(c) for c in plan.checkpoint) if plan is not None and plan.checkpoint else 0
     nl = len(plan.checkpoint) if plan is not None and plan.checkpoint else None
     tok = gbatch * seq * args.steps / dt
@@ -409,7 +442,8 @@ def bench_transformer(args, world, rank):
             "config": {"model": args.tf_config or name, "global_batch": gbatch, "per_gpu_batch": per_gpu,
                        "seq_len": seq, "parallelism": _parallelism(plan, world), "optimizer": "FusedAdam",
                        "checkpointed_layers": ck, "layers": nl, "peak_mem_gib": _peak_gib(),
-                       "warmup_s": round(t0 - tw, 1), "loss": lv, "plan": _plan_info(plan),
+                       "warmup_s": round(t0 - tw, 1), "loss": lv, "heldout_loss": held,
+                       "ln_vocab": round(math.log(cfg.vocab_size), 4), "plan": _plan_info(plan),
                        "plan_table": plan.table() if plan is not None else None,
                        "samples_per_s": round(gbatch * args.steps / dt, 2)}}
 
@@ -442,11 +476,74 @@ def _release(*objs):
         torch.cuda.reset_peak_memory_stats()
 
 
+def _fail(msg: str, rc: int = 2):
+    print(f"bench: error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(rc)
+
+
+def _self_launch(args) -> int:
+    """``bench.py --gpus N`` (N > 1) without a launcher: start N ranks here, with the
+    ``madnn.launch`` contract (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, teardown of every rank
+    at the first failure) -- the reference's one-command ``mpirun -n $nodes`` launch
+    (cifar_example/train.sh:14).  This process makes no GPU call: it only counts devices (no HIP
+    initialisation on this image), spawns the children (never ``exec``) and returns the exit code
+    of the job; rank 0's JSON line reaches stdout through the inherited descriptor."""
+    n = args.gpus
+    if args.device != "cpu":
+        avail = torch.cuda.device_count()
+        if avail < n:
+            _fail(f"--gpus {n} needs {n} visible devices, this host shows {avail}"
+                  f" (HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES')!r},"
+                  f" CUDA_VISIBLE_DEVICES={os.environ.get('CUDA_VISIBLE_DEVICES')!r})")
+    from madnn.launch import main as launch
+
+    print(f"bench: no launcher environment: starting {n} ranks (madnn.launch)", file=sys.stderr, flush=True)
+    return launch(["--nproc", str(n), os.path.abspath(__file__)] + sys.argv[1:])
+
+
+def _check_ranks(args) -> dict:
+    """Every rank checks that the job is what ``--gpus`` says: the process group has exactly N
+    ranks and, on GPUs, each rank holds its own existing device (distinct across ranks).  Any
+    mismatch exits non-zero with the reason instead of measuring a smaller world."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world != args.gpus:
+        _fail(f"--gpus {args.gpus} but the process group has {world} rank(s)")
+    import socket
+
+    dev = "cpu"
+    if args.device != "cpu":
+        if not torch.cuda.is_available():
+            _fail(f"--device {args.device}: no GPU visible to rank {dist.get_rank() if dist.is_initialized() else 0}")
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # --backend gloo on GPUs is the one-GPU rehearsal of the N-rank path (RCCL refuses two
+        # ranks per device): ranks may share the device there, and the record says so
+        rehearsal = args.backend == "gloo"
+        if local >= torch.cuda.device_count() and not rehearsal:
+            _fail(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} device(s) are visible")
+        props = torch.cuda.get_device_properties(torch.cuda.current_device())
+        ident = getattr(props, "uuid", None) or getattr(props, "pci_bus_id", None) or torch.cuda.current_device()
+        dev = f"{socket.gethostname()}/cuda:{torch.cuda.current_device()}/{ident}"
+    devices = [dev]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, dev)
+        if args.device != "cpu" and len(set(devices)) != world and args.backend != "gloo":
+            _fail(f"ranks share devices: {devices}")
+    out = {"ranks_seen": world, "devices": devices}
+    if args.device != "cpu" and len(set(devices)) != world:
+        out["shared_devices"] = "gloo rehearsal"
+    return out
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        _fail(f"--gpus {args.gpus}")
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(_self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        _fail(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} rank(s)")
     if not args.no_pg and "RANK" not in os.environ:
         # no launcher: join a world-1 group anyway (same RCCL path as the N-GPU run)
         from madnn.launch import _free_port
@@ -457,6 +554,7 @@ def main():
 
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
     madnn.init(device=args.device, backend=args.backend)
+    _RANKS.update(_check_ranks(args))
     rank = madnn.get_rank()
     on_gpu = madnn.device().type == "cuda"
     if args.seq_len is None:
@@ -530,9 +628,12 @@ def main():
     madnn.shutdown()
 
 
+_RANKS: dict = {}   # ranks_seen / devices of this job (_check_ranks), added to every record
+
+
 def _emit(res, rank, args):
     if rank == 0:
-        line = json.dumps(res)
+        line = json.dumps(dict(res, **_RANKS))
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:

@@ -64,6 +64,52 @@ def test_bench_py_single_process_joins_world1_group():
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert res["n_gpus"] == 1 and res["config"]["process_group"] == "gloo"
     assert res["config"]["parallelism"] == "dp1" and res["gpt2_pp"]["parallelism"] == "dp1"
+    assert res["ranks_seen"] == 1 and res["devices"] == ["cpu"]
+
+
+def _no_launcher_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", MADNN_LOG_LEVEL="WARNING", **extra)
+    return env
+
+
+def test_bench_py_self_launches_n_ranks_without_launcher():
+    """``bench.py --gpus 2`` with no launcher starts two ranks itself (the reference's one-command
+    ``mpirun -n``, cifar_example/train.sh:14): the record says n_gpus 2 and the process group
+    really had two ranks."""
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", "--device", "cpu",
+           "--model", "resnet50", "--batch", "2", "--std-batch", "0", "--image-size", "32", "--strategy", "dp"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=_no_launcher_env())
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["ranks_seen"] == 2 and len(res["devices"]) == 2
+    assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 4
+
+
+def test_bench_py_impossible_gpu_count_fails_loudly():
+    """More ranks than devices (this container shows no GPU) must exit non-zero with the reason,
+    never fall back to a smaller world."""
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1", "--model", "resnet50"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=_no_launcher_env(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES=""))
+    assert out.returncode != 0
+    assert "needs 4 visible devices" in out.stderr
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_py_launcher_world_mismatch_fails():
+    """Under a launcher, a WORLD_SIZE that differs from --gpus is an error on every rank."""
+    port = free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "1",
+           "--device", "cpu", "--model", "resnet50", "--batch", "2", "--image-size", "32"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert out.returncode != 0
+    assert "WORLD_SIZE=2" in out.stderr
 
 
 def test_launcher_tears_down_on_failure():
@@ -102,6 +148,8 @@ def test_bench_py_gpt2_pipeline_four_ranks_cpu():
     assert res["config"]["parallelism"] == "pp4" and res["config"]["global_batch"] == 4
     pp = res["gpt2_pp"]
     assert pp["microbatches"] == 4 and pp["model"] == "gpt2-medium"
+    # the last stage's training and held-out losses reach rank 0's record
+    assert pp["loss_last_stage"] > 0 and pp["heldout_loss"] > 0
     # the planner's choice and the transport numbers ride in the line
     assert pp["plan"]["pp"] == 4 and pp["plan"]["strategy"] == "pp" and pp["plan"]["comm_measured"]
     assert 0 < pp["bubble_fraction"] < 1 and pp["p2p_gbps"] > 0 and pp["p2p_bytes"] > 0
@@ -188,3 +236,5 @@ def test_bench_py_transformer_configs_two_ranks_cpu(model, size):
     assert res["value"] == pytest.approx(4 * 32 * 2 / (res["ms_per_step"] * 2 / 1000), rel=1e-2)
     assert c["plan"]["dp"] * c["plan"]["pp"] * c["plan"]["tp"] == 2
     assert 0 <= c["checkpointed_layers"] <= c["layers"]
+    # forward-only loss on a fresh batch, reported next to the training loss
+    assert c["heldout_loss"] is not None and c["heldout_loss"] > 0 and c["ln_vocab"] > 0
