@@ -245,7 +245,7 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
     if sync == "params" and sync_every == -1:
         sync = "manual"  # the reference's batchSize = -1 (datamodule.lua:45)
     if sync == "params" and sync_every is None:
-        sync_samples = _heuristic_period(cfg)
+        sync_samples = _heuristic_period(cfg, group, device)
     engine = DataParallel(model, space, group=group, src_rank=src_rank, sync=sync,
                           sync_every=sync_every if sync_every not in (None, -1) else 1,
                           sync_samples=sync_samples, sync_budget=cfg.sync_budget,
@@ -269,19 +269,25 @@ def _distribute_dp(model, optimizer, cfg: Config, device, group=None, src_rank: 
     return engine, optimizer
 
 
-def _heuristic_period(cfg: Config) -> int:
+def _heuristic_period(cfg: Config, group=None, device=None) -> int:
     """The reference's default period (R6, datamodule.lua:68-78) for ``sync="params"`` without
-    ``sync_every``: 1/10/50/100 SAMPLES by the size of this rank's shard -- ``cfg.local_size``,
-    else the shard ``madnn.data`` last cut on this rank.  With neither, the shard is taken to be
-    large (the heuristic's top tier, 100 samples)."""
+    ``sync_every``: 1/10/50/100 SAMPLES by the size of the shard -- ``cfg.local_size``, else the
+    shard ``madnn.data`` last cut on this rank.  With neither, the shard is taken to be large (the
+    heuristic's top tier, 100 samples).  The period is AGREED over the group (the smallest shard
+    decides): with ``remainder="last"`` shards differ in size and may fall into different tiers,
+    and ranks that averaged at different steps would pair up unrelated collectives."""
     from .data import last_local_size
 
     local = cfg.local_size if cfg.local_size is not None else last_local_size()
     if local is None:
         get_logger().warning("madnn dp: sync='params' without sync_every and no known shard size "
                              "(pass local_size=): using the heuristic's top tier, 100 samples")
-        return default_sync_period(10 ** 9)
-    return default_sync_period(int(local))
+    v = int(local) if local is not None else 10 ** 9
+    if not comm._local(group) and rt.get_world_size(group) > 1:
+        t = torch.tensor([-float(v)], dtype=torch.float64, device=device)
+        comm.all_reduce(t, "max", group=group)
+        v = int(-t.item())
+    return default_sync_period(v)
 
 
 def _after_plain_step(engine: DataParallel):

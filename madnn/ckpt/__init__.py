@@ -284,7 +284,8 @@ def _plan_meta(engine) -> dict:
     if isinstance(engine, DataParallel):
         return {"strategy": "dp", "dp": engine.world, "pp": 1, "sync": engine.sync, "sync_every": engine.sync_every,
                 "sync_samples": engine.sync_samples, "sync_calibration": engine.sync_calibration,
-                "steps": engine._steps}
+                "steps": engine._steps, "samples": engine._samples, "per_step": engine._per_step,
+                "period_origin": engine._period_origin}
     return {"strategy": "none"}
 
 
@@ -381,7 +382,17 @@ def load(path: str, engine, optimizer=None, strict: bool = True, sampler=None, t
                     g[k] = tuple(v) if isinstance(g.get(k), tuple) else v
         optimizer.load_state_dict(sd)
     if isinstance(engine, DataParallel):
-        engine._steps = int(meta.get("plan", {}).get("steps", engine._steps))
+        pm = meta.get("plan", {})
+        engine._steps = int(pm.get("steps", engine._steps))
+        # the sync="params" period resumes where it was: the sample counter, the agreed samples
+        # per step, and (sync_every="auto") the measured K instead of a fresh calibration
+        engine._samples = int(pm.get("samples") or 0)
+        engine._per_step = pm.get("per_step")
+        engine._period_origin = int(pm.get("period_origin") or 0)
+        cal = pm.get("sync_calibration")
+        if engine.sync_every == "auto" and cal and cal.get("K"):
+            engine.sync_every = int(cal["K"])
+            engine.sync_calibration = dict(cal, resumed=True)
     st = _load_resume_state(path, engine, meta)
     if st is not None:
         torch.set_rng_state(st["rng_cpu"])

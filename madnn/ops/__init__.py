@@ -662,6 +662,10 @@ def rope_qkv(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, rot_heads:
         if not (qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and qkv.size(-1) % 16 == 0
                 and cos.dtype == torch.float32 and cos.is_contiguous()):
             raise ValueError("rope_qkv: needs a contiguous bf16 qkv (D % 16 == 0) and fp32 tables")
+        if qkv.data_ptr() % 16:
+            qkv = qkv.clone()   # a slice off a 16-byte boundary: K14 moves 16 B per lane
+        if cos.data_ptr() % 16 or sin.data_ptr() % 16:
+            cos, sin = cos.clone(), sin.clone()
     return _RopeQKVFn.apply(qkv, cos, sin, rot_heads)
 
 
@@ -677,12 +681,15 @@ class _SwiGLUFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         (gu,) = ctx.saved_tensors
+        if dh.data_ptr() % 16 or not dh.is_contiguous():
+            dh = dh.contiguous().clone()   # K15 moves 16 B per lane: a fresh (aligned) buffer
         return torch.ops.madnn.swiglu_bwd(dh, gu)
 
 
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
     """``silu(g) * u`` with ``g, u = gu.chunk(2, -1)``: K15 on contiguous HIP bf16, eager otherwise."""
-    if _is_dev(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.size(-1) % 16 == 0:
+    if (_is_dev(gu) and gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.size(-1) % 16 == 0
+            and gu.data_ptr() % 16 == 0):
         _need_native("swiglu")
         return _SwiGLUFn.apply(gu)
     g, u = gu.chunk(2, dim=-1)

@@ -1314,6 +1314,12 @@ at::Tensor gelu_fwd(const at::Tensor& x, int64_t kind) {
   return y;
 }
 
+// K14 / K15 move 16 bytes per lane: every operand must start on a 16-byte boundary (a contiguous
+// slice of a larger buffer need not)
+static void check_aligned16(const at::Tensor& t, const char* op, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, op, ": ", name, " must be 16-byte aligned");
+}
+
 // K14: heads 0..rot_heads-1 of the packed bf16 QKV [B, S, NH, D] rotated (inverse: the transpose
 // rotation); in place (rope_qkv_, the backward on dQKV) or into a new packed tensor (rope_qkv, the
 // v heads copied); cos / sin fp32 [>= S][D]
@@ -1329,6 +1335,7 @@ at::Tensor rope_qkv_impl(const at::Tensor& qkv, at::Tensor out, const at::Tensor
                     t->size(0) >= S && t->size(1) == D,
                 "rope_qkv_: cos / sin must be contiguous fp32 [>= S, D] on the device");
   }
+  for (const at::Tensor* t : {&qkv, const_cast<const at::Tensor*>(&out), &cos, &sin}) check_aligned16(*t, "rope_qkv", "qkv / out / cos / sin");
   at::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   check(madnn_rope_qkv(qkv.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), qkv.size(0) * S,
                        (int)S, (int)NH, (int)rot_heads, (int)D, inverse ? 1 : 0, cur_stream(qkv)),
@@ -1354,6 +1361,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   const int64_t I = gu.size(-1) / 2, M = gu.numel() / (2 * I);
   auto shape = gu.sizes().vec();
   shape.back() = I;
+  check_aligned16(gu, "swiglu", "gu");
   at::hip::HIPGuardMasqueradingAsCUDA guard(gu.device());
   at::Tensor h = at::empty(shape, gu.options());
   check(madnn_swiglu_fwd(gu.data_ptr(), h.data_ptr(), M, (int)I, cur_stream(gu)), "swiglu_fwd");
@@ -1367,6 +1375,8 @@ at::Tensor swiglu_bwd(const at::Tensor& dh, const at::Tensor& gu) {
   const int64_t I = gu.size(-1) / 2, M = gu.numel() / (2 * I);
   at::Tensor d = dh.to(at::kBFloat16).contiguous();
   TORCH_CHECK(d.numel() == M * I, "swiglu_bwd: dh must have gu's rows and I columns");
+  check_aligned16(gu, "swiglu_bwd", "gu");
+  check_aligned16(d, "swiglu_bwd", "dh");
   at::hip::HIPGuardMasqueradingAsCUDA guard(gu.device());
   at::Tensor dgu = at::empty_like(gu);
   check(madnn_swiglu_bwd(d.data_ptr(), gu.data_ptr(), dgu.data_ptr(), M, (int)I, cur_stream(gu)), "swiglu_bwd");

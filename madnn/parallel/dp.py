@@ -128,6 +128,7 @@ class DataParallel(nn.Module):
         self.sync_calibration = None          # sync_every="auto": the measurement and the chosen K
         self._samples = 0
         self._fwd_samples = 0
+        self._per_step = None                 # agreed samples per step (sync_samples; _params_tick)
         self._calib = None
         self._period_origin = 0
         self.cast_dtype = cast_dtype
@@ -379,14 +380,29 @@ class DataParallel(nn.Module):
     def _params_tick(self):
         n, self._fwd_samples = self._fwd_samples, 0
         if self.sync_samples is not None:
+            # the averaging is a collective: every replica must reach it at the same step.  The
+            # samples a step counts are agreed once (MIN over the group at the first step) and
+            # the counter then advances by that amount on every rank, so the decision is a
+            # function of the step count alone -- a rank with a larger shard or a short last
+            # batch cannot drift off its peers
+            if self._per_step is None:
+                self._per_step = self._agree_min(max(n, 1))
             before = self._samples
-            self._samples += max(n, 1)
+            self._samples += self._per_step
             if self._samples // self.sync_samples > before // self.sync_samples:
                 self.average_parameters()
         elif self.sync_every == "auto":
             self._auto_period()
         elif (self._steps - self._period_origin) % self.sync_every == 0:
             self.average_parameters()
+
+    def _agree_min(self, v: int) -> int:
+        if comm._local(self.group) or self.world <= 1:
+            return int(v)
+        dev = self.space.buckets[0].master.device if self.space.buckets else torch.device("cpu")
+        t = torch.tensor([-int(v)], dtype=torch.float64, device=dev)
+        comm.all_reduce(t, "max", group=self.group)
+        return int(-t.item())
 
     AUTO_WARMUP = 1   # steps averaged every step before timing starts (allocator, kernel choices)
     AUTO_MEASURE = 3  # steps timed: compute since the previous average ended, then the average

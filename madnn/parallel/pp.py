@@ -1091,6 +1091,11 @@ class PipelineEngine:
         self._tune_end(tune)
         self.stats["steps"] += 1
         self.last_loss = total
+        if self.unpack_to_params:
+            # a plain torch optimizer: p.grad holds the final (reduced, tied-summed) gradients as
+            # soon as train_step returns, so anything between it and opt.step() -- gradient
+            # clipping, inspection -- sees and changes what the step will apply
+            self.finalize_grads()
         return total
 
     # -------------------------------------------------- tied parameters (N8)

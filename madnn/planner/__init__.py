@@ -198,6 +198,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
     cap = hw.hbm_gb * cfg.mem_headroom * 1e9
     L = len(spine)
     forced = cfg.strategy
+    elig = [_ckpt_eligible(spine, i) for i in range(L)]
     cands = []
     for pp in divisors(world):
         if pp > L:
@@ -205,9 +206,12 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         dp = world // pp
         if not _allowed(forced, pp, dp, world, cfg.pp_stages):
             continue
-        for ckpt_mode in ([False, True] if cfg.checkpointing == "auto" else [cfg.checkpointing == "all"]):
+        # checkpointing="auto": no recompute, every block, and the per-block choice (the fewest
+        # blocks per rank whose recompute makes it fit, _candidate) are all priced
+        modes = [False, True, "auto"] if cfg.checkpointing == "auto" else [cfg.checkpointing == "all"]
+        for ckpt_mode in modes:
             for schedule, V, M in pp_variants(pp, max(B // dp, 1), L, cfg):
-                c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode, schedule, V, M)
+                c = _candidate(costs, pp, dp, B, cfg, hw, opt, cap, ckpt_mode, schedule, V, M, elig=elig)
                 if c is not None:
                     cands.append(c)
     if (forced == "tp" or forced == "auto" and not cfg.pp_stages) and world > 1:
@@ -222,7 +226,7 @@ def plan_model(model: nn.Module, cfg: Config, world: int, example_input: Optiona
         raise RuntimeError(f"madnn planner: no feasible placement for world={world}, strategy={forced}")
     feasible = [c for c in cands if c["fits"]] or cands
     best = min(feasible, key=lambda c: (c["step_s"], c["pp"], c.get("tp", 1), c["ckpt"]))
-    ck = [best["ckpt"] and _ckpt_eligible(spine, i) for i in range(L)]
+    ck = list(best.get("ck") or [False] * L)
     plan = Plan(best["strategy"], best["dp"], best["pp"], best["bounds"], best["M"], ck, best["step_s"],
                 best["mem_list"], spine, costs, cands, B, schedule=best.get("schedule", "1f1b"),
                 virtual=best.get("V", 1), tp=best.get("tp", 1), measured=measured)
@@ -454,38 +458,90 @@ def _calibrate_chain(spine, example_input, costs, batch, dtype, cfg: Config, hw:
     return out
 
 
-def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="none", V=1, M=1):
+def _seg_act(costs, ck, idx) -> float:
+    """Saved-activation bytes per sample of the layers ``idx``: a checkpointed layer keeps only
+    its boundary tensor, and while one is recomputed its full activations live again (the
+    largest checkpointed layer's working set)."""
+    kept, work = 0.0, 0.0
+    for i in idx:
+        if ck[i]:
+            kept += costs[i].out_bytes
+            work = max(work, costs[i].act_bytes)
+        else:
+            kept += costs[i].act_bytes
+    return kept + work
+
+
+RECOMPUTE = 1.0 / 3.0   # a checkpointed layer's forward again in the backward: ~1/3 of its fwd + bwd
+
+
+def _pick_checkpoints(costs, ck, elig, idx, mb, over) -> None:
+    """Checkpoint layers of ``idx`` (eligible, not yet chosen) until ``over()`` -- the rank's memory
+    above the cap -- is no longer positive, most saved bytes per recompute second first: the
+    fewest extra forward seconds for the memory the rank must give up."""
+    def gain(i):
+        c = costs[i]
+        return (c.act_bytes - c.out_bytes) / max(RECOMPUTE * c.call_s(mb), 1e-12)
+
+    for i in sorted((i for i in idx if elig[i] and not ck[i]), key=gain, reverse=True):
+        if over() <= 0:
+            return
+        ck[i] = True
+
+
+def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="none", V=1, M=1, elig=None):
+    """One placement priced.  ``ckpt``: False (no recompute), True (every eligible layer) or
+    "auto" -- per block: on each pipeline rank that would not fit, the fewest eligible layers
+    whose recompute makes it fit (``_pick_checkpoints``); None when that equals one of the two
+    uniform choices (already priced)."""
     from ..parallel.pp import pipeline_bubble, simulate_schedule, transport_time
 
     L = len(costs)
+    elig = elig if elig is not None else [True] * L
     per_replica = max(B // dp, 1)
     if pp == 1:
         schedule, V, M = "none", 1, 1
     mb = per_replica / M
-    rfac = 1.0 + (1.0 / 3.0 if ckpt else 0.0)
+    ck = [bool(ckpt is True and elig[i]) for i in range(L)]
     nst = pp * V
-    mems = [stage_estimate(costs, i, i + 1, opt, ckpt).param_bytes + stage_estimate(costs, i, i + 1, opt, ckpt)
-            .act_bytes_per_sample * mb * (pp if pp > 1 else 1) for i in range(L)]
-    times = [c.call_s(mb) * rfac for c in costs]
+    pbytes_l = [stage_estimate(costs, i, i + 1, opt, False).param_bytes for i in range(L)]
+
+    def layer_times():
+        return [c.call_s(mb) * (1.0 + (RECOMPUTE if ck[i] else 0.0)) for i, c in enumerate(costs)]
+
+    times = layer_times()
+    mems = [pbytes_l[i] + _seg_act(costs, ck, [i]) * mb * (pp if pp > 1 else 1) for i in range(L)]
     try:
         bounds, _ = native_runtime.partition(times, nst, mems, cap / V if cap > 0 else 0.0)
     except ValueError:
         bounds, _ = native_runtime.partition(times, nst)
-    chunk_est = [stage_estimate(costs, bounds[v], bounds[v + 1], opt, ckpt) for v in range(nst)]
+    chunk_est = [stage_estimate(costs, bounds[v], bounds[v + 1], opt, False) for v in range(nst)]
     ranks = _chunk_ranks(pp, V)
-    # per-rank time of ONE microbatch through its chunks: fixed per-call cost + per-sample slope
-    rank_t = [sum(times[i] for v in vs for i in range(bounds[v], bounds[v + 1])) for vs in ranks]
     if pp > 1:
         inflight = simulate_schedule(schedule, pp, M, V)["peak_inflight"]
         if schedule == "gpipe":
             inflight = [M * V] * pp
     else:
         inflight = [1]
-    mem_list = []
-    for r, vs in enumerate(ranks):
+
+    def rank_mem(r) -> float:
+        vs = ranks[r]
         pbytes = sum(chunk_est[v].param_bytes for v in vs)
-        act_per_chunk = sum(chunk_est[v].act_bytes_per_sample for v in vs) / len(vs) * mb
-        mem_list.append((pbytes + act_per_chunk * inflight[r]) / 1e9)
+        act = sum(_seg_act(costs, ck, range(bounds[v], bounds[v + 1])) for v in vs) / len(vs) * mb
+        return pbytes + act * inflight[r]
+
+    if ckpt == "auto":
+        for r, vs in enumerate(ranks):
+            idx = [i for v in vs for i in range(bounds[v], bounds[v + 1])]
+            _pick_checkpoints(costs, ck, elig, idx, mb, lambda r=r: rank_mem(r) - cap)
+        k = sum(ck)
+        if k == 0 or k == sum(elig):
+            return None
+        times = layer_times()
+    mem_list = [rank_mem(r) / 1e9 for r in range(len(ranks))]
+    # per-rank time of ONE microbatch through its chunks: fixed per-call cost + per-sample slope
+    rank_t = [sum(times[i] for v in vs for i in range(bounds[v], bounds[v + 1])) for vs in ranks]
+    rf = [1.0 + (RECOMPUTE if ck[i] else 0.0) for i in range(L)]
     rb = _reduce_bytes(cfg)
     bucket_bytes = _bucket_bytes(cfg, costs, rb)
     rank_params = [sum(chunk_est[v].params for v in vs) for vs in ranks]
@@ -494,7 +550,7 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
     if pp == 1:
         compute = rank_t[0]
         bubble = 0.0
-        bwd = [(c.bwd_s * per_replica + c.fixed_s * 2.0 / 3.0) * rfac for c in costs]
+        bwd = [(c.bwd_s * per_replica + c.fixed_s * 2.0 / 3.0) * rf[i] for i, c in enumerate(costs)]
         comm_s = dp_exposed_s(bwd, [c.params * rb for c in costs], dp, hw, bucket_bytes)
         step = compute + comm_s + opt_s
     else:
@@ -511,14 +567,14 @@ def _candidate(costs, pp, dp, B, cfg, hw: Machine, opt, cap, ckpt, schedule="non
         if dp > 1:  # stage-local reduction overlaps the last microbatch's backward only
             for vs in ranks:
                 idx = [i for v in vs for i in range(bounds[v], bounds[v + 1])]
-                bwd = [(costs[i].bwd_s * mb + costs[i].fixed_s * 2.0 / 3.0) * rfac for i in idx]
+                bwd = [(costs[i].bwd_s * mb + costs[i].fixed_s * 2.0 / 3.0) * rf[i] for i in idx]
                 dp_s = max(dp_s, dp_exposed_s(bwd, [costs[i].params * rb for i in idx], dp, hw, bucket_bytes))
         comm_s += dp_s
         step = pipe + dp_s + opt_s
     fits = max(mem_list) * 1e9 <= cap
     strategy = "dp" if pp == 1 else ("pp" if dp == 1 else "dp_pp")
     return {"strategy": strategy, "dp": dp, "pp": pp, "tp": 1, "M": M, "V": V, "schedule": schedule,
-            "ckpt": ckpt, "bounds": bounds, "step_s": step, "compute_s": compute, "comm_s": comm_s,
+            "ckpt": sum(ck), "ck": ck, "bounds": bounds, "step_s": step, "compute_s": compute, "comm_s": comm_s,
             "bubble": bubble, "mem_gb": max(mem_list), "mem_list": mem_list, "fits": fits, "opt_s": opt_s,
             "lag": lag}
 
@@ -593,7 +649,7 @@ def _tp_candidate(spine: Spine, costs, dp, tp, B, cfg, hw: Machine, opt, cap, ex
         grad_dp = dp_exposed_s(bwd, [c.params * _reduce_bytes(cfg) / tp for c in costs], dp, hw,
                                _bucket_bytes(cfg, costs, _reduce_bytes(cfg)))
     step = compute + comm + grad_dp + optimizer_s(local_params, opt, hw)
-    return {"strategy": "tp", "dp": dp, "pp": 1, "tp": tp, "M": 1, "V": 1, "schedule": "none", "ckpt": False,
+    return {"strategy": "tp", "dp": dp, "pp": 1, "tp": tp, "M": 1, "V": 1, "schedule": "none", "ckpt": 0,
             "bounds": [0, len(costs)], "step_s": step, "compute_s": compute, "comm_s": comm + grad_dp,
             "bubble": 0.0, "mem_gb": mem, "mem_list": [mem], "fits": mem * 1e9 <= cap}
 

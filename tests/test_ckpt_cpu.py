@@ -64,6 +64,49 @@ def test_dp_save_resume_consolidate(tmp_path):
     run_dist(_w_dp_resume, 2, str(tmp_path / "ck"))
 
 
+def _w_params_period_resume(rank, world, path):
+    """sync="params" with a sample period (local_size 1200 -> 10 samples) and 4 samples a step:
+    an uninterrupted run averages at steps 3, 5, 8; a run saved after step 4 and resumed must
+    average at the same steps (the sample counter is restored, not restarted)."""
+    import madnn
+    from madnn import ckpt
+    from madnn.optim import FusedSGD
+
+    def make():
+        m = _gpt()
+        return madnn.distribute(m, FusedSGD(m.parameters(), lr=1e-2), strategy="dp", sync="params",
+                                local_size=1200)
+
+    x, y = _data()
+    xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+
+    def run(eng, opt, steps, synced):
+        real = eng.average_parameters
+        eng.average_parameters = lambda: (synced.append(eng._steps), real())
+        for _ in range(steps):
+            F.cross_entropy(eng(xs).flatten(0, 1), ys.flatten()).backward()
+            opt.step()
+        eng.average_parameters = real
+
+    eng, opt = make()
+    first = []
+    run(eng, opt, 4, first)
+    ckpt.save(path, eng, opt, step=4)
+    rest = []
+    run(eng, opt, 4, rest)
+    assert first + rest == [3, 5, 8]
+    eng2, opt2 = make()
+    ckpt.load(path, eng2, opt2)
+    assert eng2._samples == 16 and eng2._per_step == 4
+    resumed = []
+    run(eng2, opt2, 4, resumed)
+    assert resumed == rest
+
+
+def test_params_period_resumes_sample_counter(tmp_path):
+    run_dist(_w_params_period_resume, 2, str(tmp_path / "ck"))
+
+
 def _w_pp_save(rank, world, path):
     import madnn
     from madnn import ckpt

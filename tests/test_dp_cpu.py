@@ -162,6 +162,44 @@ def test_distribute_params_sync_period(mode):
     run_dist(_w_params_period, 2, mode)
 
 
+def _w_params_period_unequal_shards(rank, world):
+    """Shards of 2499 and 2500 samples (``remainder="last"``) fall into different tiers of the
+    reference heuristic (10 vs 50 samples), and the ranks train different batch sizes: the period
+    and the per-step sample count are agreed, so both ranks average at the same steps."""
+    import madnn
+    from madnn.data import shard
+    from madnn.optim import FusedSGD
+
+    x, y = _data(5, n=4999)
+    xs, ys = shard(x, remainder="last"), shard(y, remainder="last")
+    assert len(xs) == (2499 if rank == 0 else 2500)
+    model = _ref_model()
+    opt = FusedSGD(model.parameters(), lr=0.05)
+    dm, opt = madnn.distribute(model, opt, strategy="dp", sync="params")
+    assert dm.sync_samples == 10                      # the smaller shard's tier, on both ranks
+    synced = []
+    real = dm.average_parameters
+
+    def counting():
+        synced.append(dm._steps)
+        real()
+
+    dm.average_parameters = counting
+    b = 3 if rank == 0 else 4                          # 3 samples a step are agreed
+    for step in range(10):
+        F.cross_entropy(dm(xs[step * b:step * b + b]), ys[step * b:step * b + b]).backward()
+        opt.step()
+        opt.zero_grad()
+    assert synced == [4, 7, 10], synced               # crossing 10, 20, 30 at 3 samples a step
+    _check_same_across_ranks(torch.tensor(synced))
+    for p in model.parameters():
+        _check_same_across_ranks(p.detach())
+
+
+def test_params_period_agreed_with_unequal_shards():
+    run_dist(_w_params_period_unequal_shards, 2)
+
+
 def _w_no_sync(rank, world):
     import madnn
     from madnn.optim import FusedSGD

@@ -73,3 +73,31 @@ def test_llama_block_k14_k15_match_eager(cuda, monkeypatch):
     torch.testing.assert_close(loss.float(), loss2.float(), atol=2e-2, rtol=2e-2)
     for n, p in model.named_parameters():
         assert _rel(got[n], p.grad) < 5e-2, (n, _rel(got[n], p.grad))
+
+
+def test_misaligned_inputs_are_refused_or_rerouted(cuda):
+    """K14 / K15 move 16 bytes per lane: a contiguous slice that starts off a 16-byte boundary is
+    refused by the bindings (never a misaligned vector access) and handled by ``ops`` (an aligned
+    copy for RoPE, the eager path for SwiGLU) with the right result."""
+    from madnn import ops
+    from madnn.models.common import RotaryEmbedding
+
+    assert ops.load_kernels()
+    torch.manual_seed(3)
+    buf = torch.randn(1 + 64 * 32, device=cuda).bfloat16()
+    gu = buf[1:].view(64, 32)                      # 2-byte offset: misaligned, contiguous
+    assert gu.is_contiguous() and gu.data_ptr() % 16
+    with pytest.raises(RuntimeError, match="16-byte aligned"):
+        torch.ops.madnn.swiglu_fwd(gu)
+    g, u = gu.float().chunk(2, -1)
+    assert _rel(ops.swiglu(gu), F.silu(g) * u) < 1e-2
+    D, H, HKV, S = 64, 2, 1, 16
+    rope = RotaryEmbedding(D, 10000.0, 64).to(cuda)
+    qb = torch.randn(8 + 2 * S * (H + 2 * HKV) * D, device=cuda).bfloat16()
+    qkv = qb[8 * 0 + 1: 1 + 2 * S * (H + 2 * HKV) * D].view(2, S, H + 2 * HKV, D)
+    assert qkv.data_ptr() % 16
+    with pytest.raises(RuntimeError, match="16-byte aligned"):
+        torch.ops.madnn.rope_qkv(qkv, rope.cos, rope.sin, H + HKV, False)
+    ref = qkv.float().clone()
+    ref[:, :, : H + HKV] = ops._rope_rotate(ref[:, :, : H + HKV], rope.cos, rope.sin, False).float()
+    torch.testing.assert_close(ops.rope_qkv(qkv, rope.cos, rope.sin, H + HKV).float(), ref, atol=2e-2, rtol=1e-2)

@@ -293,7 +293,7 @@ def test_plan_tuning_survives_a_shape_change_mid_tuning():
     run_dist(_w_plan_tuning_with_shape_change, 4)
 
 
-def _w_pp_plain_optimizer(rank, world, dp):
+def _w_pp_plain_optimizer(rank, world, dp, clip=None):
     """A plain torch optimizer through the pipeline path (as the DP path accepts one): the engine
     fills p.grad (after the cross-stage tied-embedding sum) before optimizer.step() and re-syncs its
     flat master copy after it -- parameters track single-process AdamW."""
@@ -314,15 +314,23 @@ def _w_pp_plain_optimizer(rank, world, dp):
     xr = x[d_idx * per:(d_idx + 1) * per]
     for _ in range(3):
         eng.train_step(xr, xr)
+        if clip:   # p.grad is final when train_step returns: clipping changes what the step applies
+            torch.nn.utils.clip_grad_value_([p for p in model.parameters() if p.grad is not None], clip)
         opt.step()
         opt.zero_grad()
         model.loss_fn(ref(x), x).backward()
+        if clip:
+            torch.nn.utils.clip_grad_value_(ref.parameters(), clip)
         ropt.step()
         ropt.zero_grad()
     ref_params = dict(ref.named_parameters(remove_duplicate=False))
     for name, p in eng.state_dict().items():
         torch.testing.assert_close(p.detach(), ref_params[name].detach(), atol=1e-3, rtol=1e-3,
                                    msg=lambda m, name=name: f"{name}: {m}")
+
+
+def test_pp_plain_torch_optimizer_with_grad_clipping():
+    run_dist(_w_pp_plain_optimizer, 2, 1, 1e-3)
 
 
 @pytest.mark.parametrize("world,dp", [(2, 1), (4, 2)])

@@ -423,6 +423,31 @@ def test_planner_auto_pipeline_when_a_replica_does_not_fit():
     assert "V=" in p.table() or p.virtual == 1
 
 
+def test_planner_checkpoints_the_fewest_blocks_that_fit():
+    """Per-block activation checkpointing: Llama-3 8B at 8192 tokens x 4 sequences on one GPU does
+    not fit without recompute and does not need it on every block.  The planner prices no
+    recompute, every block, and the per-block choice, and takes the per-block plan: 0 < k < 32
+    blocks, inside the HBM cap, faster than recomputing all of them (the reference's analog is its
+    size-driven automatic knob, datamodule.lua:65-78)."""
+    from madnn.models.llama import Llama, llama_config
+    from madnn.planner import plan_model
+
+    with torch.device("meta"):
+        m = Llama(llama_config("llama3-8b"))
+    p = plan_model(m, Config.from_env(strategy="auto", checkpointing="auto"), 1,
+                   example_input=torch.zeros(1, 8192, dtype=torch.long), global_batch=4)
+    k = sum(p.checkpoint)
+    assert 0 < k < 32, p.describe()
+    assert not p.checkpoint[0] and not p.checkpoint[-1]          # embedding and head never recomputed
+    rows = {c["ckpt"]: c for c in p.candidates}
+    assert not rows[0]["fits"] and rows[32]["fits"] and rows[k]["fits"]
+    assert rows[k]["step_s"] < rows[32]["step_s"] and p.est_step_s == rows[k]["step_s"]
+    # a smaller problem fits without any recompute: the knob follows the problem size
+    p2 = plan_model(m, Config.from_env(strategy="auto", checkpointing="auto"), 1,
+                    example_input=torch.zeros(1, 1024, dtype=torch.long), global_batch=4)
+    assert sum(p2.checkpoint) == 0
+
+
 def test_measured_costs_change_the_placement():
     """The planner consumes measured layer times: with GPT-2 medium at 8 GPUs, analytic costs
     and costs that make compute 100x cheaper (comm-dominated) must not pick the same layout,
