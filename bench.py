@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--tf-batch-per-gpu", type=int, default=None,
                     help="sequences per GPU for --model bert-large (default 128 at --seq-len 512) / llama3-8b "
                          "(default 4 at --seq-len 4096)")
+    ap.add_argument("--checkpointing", default="auto", choices=["auto", "all", "none"],
+                    help="--model bert-large|llama3-8b: activation checkpointing (auto: the planner's per-block "
+                         "choice; all / none pin it, for A/Bs)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (resnet50)")
     ap.add_argument("--gpt2-batch-per-gpu", type=int, default=128,
                     help="GPT-2 sequences per GPU (global = this x N); 128: 369k tok/s vs 360k at 64 on one "
@@ -405,7 +408,8 @@ def bench_transformer(args, world, rank):
         from madnn.parallel.pp import materialize_
 
         materialize_(model, madnn.device(), getattr(model, "init_weights", None), opt)
-    engine, opt = madnn.distribute(model, opt, strategy=args.strategy, checkpointing="auto", global_batch=gbatch,
+    engine, opt = madnn.distribute(model, opt, strategy=args.strategy, checkpointing=args.checkpointing,
+                                   global_batch=gbatch,
                                    example_input=torch.zeros(1, seq, dtype=torch.long))
     plan = getattr(engine, "plan", None)
     dp = plan.dp if plan is not None else world
@@ -441,6 +445,7 @@ def bench_transformer(args, world, rank):
             "data": "synthetic (random tokens, random-init weights)",
             "config": {"model": args.tf_config or name, "global_batch": gbatch, "per_gpu_batch": per_gpu,
                        "seq_len": seq, "parallelism": _parallelism(plan, world), "optimizer": "FusedAdam",
+                       "checkpointing": args.checkpointing,
                        "checkpointed_layers": ck, "layers": nl, "peak_mem_gib": _peak_gib(),
                        "warmup_s": round(t0 - tw, 1), "loss": lv, "heldout_loss": held,
                        "ln_vocab": round(math.log(cfg.vocab_size), 4), "plan": _plan_info(plan),

@@ -1354,6 +1354,7 @@ WGRAD = os.environ.get("MADNN_WGRAD", "auto")  # weight-gradient GEMM: auto (tim
 _WGRAD_CHOICE: dict = {}
 _GELU_FWD_CHOICE: dict = {}
 _DGELU_CHOICE: dict = {}
+_DGRAD_CHOICE: dict = {}
 _TUNE = {"timed": 0, "table": None}   # run-time timings taken; the shipped table that was loaded
 _TUNE_MS: dict = {}   # (table, key) -> {implementation: ms for 3 calls} of every run-time timing (the A/B record)
 
@@ -1380,7 +1381,8 @@ def load_tuning_table(path: Optional[str] = None) -> int:
     except (OSError, ValueError):
         return 0
     n = 0
-    for name, dst in (("wgrad", _WGRAD_CHOICE), ("gelu_fwd", _GELU_FWD_CHOICE), ("dgelu", _DGELU_CHOICE)):
+    for name, dst in (("wgrad", _WGRAD_CHOICE), ("gelu_fwd", _GELU_FWD_CHOICE), ("dgelu", _DGELU_CHOICE),
+                      ("dgrad", _DGRAD_CHOICE)):
         for k, v in data.get(name, {}).items():
             dst.setdefault(ast.literal_eval(k), v)
             n += 1
@@ -1394,7 +1396,8 @@ def export_choices(path: str) -> None:
 
     data = {"arch": "gfx950", "wgrad": {repr(k): v for k, v in sorted(_WGRAD_CHOICE.items(), key=repr)},
             "gelu_fwd": {repr(k): v for k, v in sorted(_GELU_FWD_CHOICE.items(), key=repr)},
-            "dgelu": {repr(k): v for k, v in sorted(_DGELU_CHOICE.items(), key=repr)}}
+            "dgelu": {repr(k): v for k, v in sorted(_DGELU_CHOICE.items(), key=repr)},
+            "dgrad": {repr(k): v for k, v in sorted(_DGRAD_CHOICE.items(), key=repr)}}
     with open(path, "w") as f:
         json.dump(data, f, indent=1)
         f.write("\n")
@@ -1407,11 +1410,12 @@ def sync_choices(group=None, src: int = 0) -> None:
 
     if not dist.is_initialized() or dist.get_world_size(group) <= 1:
         return
-    obj = [(dict(_WGRAD_CHOICE), dict(_GELU_FWD_CHOICE), dict(_DGELU_CHOICE))]
+    obj = [(dict(_WGRAD_CHOICE), dict(_GELU_FWD_CHOICE), dict(_DGELU_CHOICE), dict(_DGRAD_CHOICE))]
     dist.broadcast_object_list(obj, src=src, group=group)
     _WGRAD_CHOICE.update(obj[0][0])
     _GELU_FWD_CHOICE.update(obj[0][1])
     _DGELU_CHOICE.update(obj[0][2])
+    _DGRAD_CHOICE.update(obj[0][3])
 
 
 def tuning_timings() -> int:
@@ -1423,7 +1427,8 @@ def tuning_measurements() -> list:
     """Every per-shape timing this process ran: [{"table", "key", "ms": {impl: ms}, "chosen"}]."""
     out = []
     for (tab, key), ms in _TUNE_MS.items():
-        chosen = {"wgrad": _WGRAD_CHOICE, "gelu_fwd": _GELU_FWD_CHOICE, "dgelu": _DGELU_CHOICE}[tab].get(key)
+        chosen = {"wgrad": _WGRAD_CHOICE, "gelu_fwd": _GELU_FWD_CHOICE, "dgelu": _DGELU_CHOICE,
+                  "dgrad": _DGRAD_CHOICE}[tab].get(key)
         out.append({"table": tab, "key": repr(key), "ms": {k: round(v, 4) for k, v in ms.items()}, "chosen": chosen})
     return out
 
@@ -1459,20 +1464,26 @@ def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.T
     if WGRAD == "lt" or not _wgrad_k12_ok(g2, x2, out):
         return lib()
     return tuned_wgrad(("linear",) + tuple(g2.shape) + (x2.shape[1],), lib,
-                       lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0))
+                       lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0),
+                       k12w=lambda: torch.ops.madnn.linear_wgrad4(g2, x2, out, False, 0))
 
 
-def tuned_wgrad(key, lib, k12, k9=None):
+def tuned_wgrad(key, lib, k12, k9=None, k12w=None):
     """Run the weight-gradient implementation that was faster for ``key``: ``lib`` (the library
-    kernel: hipBLASLt / MIOpen), ``k12`` (K12 split-K over the rows) or, for NHWC 1x1 convolutions,
-    ``k9`` (K9's split-M kernel, slabs reduced and cast in one pass) -- from the shipped table
+    kernel: hipBLASLt / MIOpen), ``k12`` (K12 split-K over the rows), ``k12w`` (K12W: the same
+    split-K GEMM at one wave per SIMD, 128 x 128 per wave) or, for NHWC 1x1 convolutions, ``k9``
+    (K9's split-M kernel, slabs reduced and cast in one pass) -- from the shipped table
     (:func:`load_tuning_table`), else timed once on first use (outside graph capture).
-    ``MADNN_WGRAD=lt`` / ``k12`` pin one."""
+    ``MADNN_WGRAD=lt`` / ``k12`` / ``k12w`` pin one."""
     if WGRAD == "lt":
         return lib()
     if WGRAD == "k12":
         return k12()
+    if WGRAD == "k12w" and k12w is not None:
+        return k12w()
     cands = {"lib": lib, "k12": k12}
+    if k12w is not None:
+        cands["k12w"] = k12w
     if k9 is not None:
         cands["k9"] = k9
     choice = _WGRAD_CHOICE.get(key)
@@ -1507,7 +1518,8 @@ def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> to
         return lib()
     k9 = (lambda: _k9_wgrad(dy, x, w)) if x.dim() == 4 and conv1x1_supported(x, w.view(w.size(0), -1)) else None
     return tuned_wgrad(("conv1x1", dr.shape[0], dr.shape[1], xr.shape[1]), lib,
-                       lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape), k9)
+                       lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape), k9,
+                       k12w=lambda: torch.ops.madnn.linear_wgrad4(dr, xr, None, False, 0).view(w.shape))
 
 
 LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)
@@ -1568,7 +1580,8 @@ def _timed_choice(table: dict, key, cands: dict, default: str) -> str:
         return default
     _TUNE["timed"] += 1
     times = {k: _time_wgrad(f) for k, f in cands.items()}
-    _TUNE_MS[("gelu_fwd" if table is _GELU_FWD_CHOICE else "dgelu", key)] = times
+    name = {id(_GELU_FWD_CHOICE): "gelu_fwd", id(_DGELU_CHOICE): "dgelu", id(_DGRAD_CHOICE): "dgrad"}[id(table)]
+    _TUNE_MS[(name, key)] = times
     choice = table[key] = min(times, key=times.get)
     return choice
 
@@ -1654,6 +1667,31 @@ def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dty
     return lt() if choice == "lt" else k12p()
 
 
+DGRAD = os.environ.get("MADNN_DGRAD", "auto")  # plain Linear data gradient: auto | lt | k12p
+
+
+def dgrad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``g2 @ weight``: a Linear's data gradient, from whichever was faster for the shape (shipped
+    table, else timed once on first use like :func:`tuned_wgrad`): ``lt`` (hipBLASLt) or ``k12p``
+    (the persistent K12P GEMM, plain epilogue).  hipBLASLt's choice at 32k-token microbatches ran
+    the GPT-2 data gradients 35 % slower per FLOP than at 131k tokens
+    (``profiles/r6_gpt2m_mb32_steady_steps.md``).  ``MADNN_DGRAD=lt`` / ``k12p`` pin one."""
+    def lt():
+        return g2 @ weight
+
+    if DGRAD == "lt" or not (g2.is_contiguous() and _k12p_ok(g2, weight, weight.shape[1], g2.shape[0], g2.shape[1],
+                                                             False)):
+        return lt()
+
+    def k12p():
+        return torch.ops.madnn.linear_dgrad_p(g2, weight, None, g2.dtype, 1)[0]
+
+    if DGRAD == "k12p":
+        return k12p()
+    key = (tuple(g2.shape), tuple(weight.shape))
+    return {"lt": lt, "k12p": k12p}[_timed_choice(_DGRAD_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")]()
+
+
 class _LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) (+ residual) with act in {identity, tanh-GELU}.
 
@@ -1720,7 +1758,7 @@ class _LinearFn(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = (g2 @ weight).view(*x.shape[:-1], weight.shape[1])
+            dx = dgrad(g2, weight).view(*x.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             sink = grad_sink(ctx.param)

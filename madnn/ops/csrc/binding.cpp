@@ -114,6 +114,8 @@ hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const vo
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
 int madnn_wgrad_splits(int64_t, int64_t, int64_t);
+hipError_t madnn_linear_wgrad4(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
+                               hipStream_t);
 hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
                               hipStream_t);
 int madnn_gemmp_supported(int64_t, int64_t, int64_t, int);
@@ -810,8 +812,8 @@ at::Tensor linear_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::op
 // dW[N, K] = dy[M, N]^T x[M, K] over the M tokens, split along M (fp32 slabs + reduce) so the few
 // output tiles of a weight gradient fill the GPU.  With `out` the result is written there (the
 // reducer's bucket slot: a grad sink), with accumulate added to its contents.  splits <= 0: auto.
-at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
-                        bool accumulate, int64_t splits) {
+at::Tensor linear_wgrad_impl(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                             bool accumulate, int64_t splits, bool four_wave) {
   gemm_check(dy, "dy");
   gemm_check(x, "x");
   const int64_t N = dy.size(-1), K = x.size(-1), M = dy.numel() / std::max<int64_t>(N, 1);
@@ -830,10 +832,22 @@ at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::op
   }
   const int sp = splits > 0 ? (int)splits : madnn_wgrad_splits(M, N, K);
   at::Tensor ws = sp > 1 ? at::empty({sp, N, K}, dy.options().dtype(at::kFloat)) : at::Tensor();
-  check(madnn_linear_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr, sp,
-                           accumulate ? 1 : 0, M, N, K, cur_stream(dy)),
+  auto fn = four_wave ? madnn_linear_wgrad4 : madnn_linear_wgrad;
+  check(fn(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr, sp, accumulate ? 1 : 0,
+           M, N, K, cur_stream(dy)),
         "linear_wgrad");
   return dw;
+}
+
+at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                        bool accumulate, int64_t splits) {
+  return linear_wgrad_impl(dy, x, out, accumulate, splits, false);
+}
+
+// K12W (gemm.hip: one wave per SIMD, 128 x 128 per wave), same contract
+at::Tensor linear_wgrad4(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                         bool accumulate, int64_t splits) {
+  return linear_wgrad_impl(dy, x, out, accumulate, splits, true);
 }
 
 int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) { return madnn_wgrad_splits(M, N, K); }
@@ -1575,6 +1589,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("linear_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? res, int act, bool save_aux) -> (Tensor, Tensor)");
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
+  m.def("linear_wgrad4(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
   m.def("wgrad_splits(int M, int N, int K) -> int", &wgrad_splits);
   m.def("gemmp_supported(int I, int J, int K, bool has_bias) -> bool", &gemmp_supported);
   m.def("linear_fwd_p(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
@@ -1655,6 +1670,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_fwd", linear_fwd);
   m.impl("linear_dgrad", linear_dgrad);
   m.impl("linear_wgrad", linear_wgrad);
+  m.impl("linear_wgrad4", linear_wgrad4);
   m.impl("linear_fwd_p", linear_fwd_p);
   m.impl("linear_dgrad_p", linear_dgrad_p);
   m.impl("conv3x3_fwd", conv3x3_fwd);

@@ -51,6 +51,8 @@
 // [256 j][256 i] (XOR-swizzled 16-B chunks) and stored as full 512-B rows; in that row pass:
 // aux = pre-activation store, tanh-GELU, residual add (fp32 add of two bf16, one rounding:
 // the same two roundings as the unfused PyTorch graph).
+#include <type_traits>
+
 #include "k12.h"
 
 namespace madnn {
@@ -353,6 +355,237 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K12W: the weight-gradient GEMM (both operands k-major: "col" images) at ONE wave per SIMD.
+//
+// Why (profiles/r5_gemm_pmc.md): K12's 8 waves own 128 x 64 blocks, so every bf16 fragment read
+// from LDS feeds 4 (A) or 8 (B) MFMAs and each phase's reads must land inside the partner group's
+// 256-cycle MFMA segment; the matrix cores idle ~12 points in its main loop.  Here 4 waves each own
+// a 128 x 128 block -- 4 x 4 v_mfma_f32_32x32x16_bf16 accumulators, 256 registers: the
+// accumulation registers of a lone wave (the 16x16x32 form's 64 four-register tuples made hipcc
+// shuffle them between register files every iteration) -- every fragment feeds 4 MFMAs of 32
+// cycles, and a wave issues the NEXT phase's fragment reads between its own MFMAs (software
+// pipelining inside the wave instead of across two wave groups).
+//
+// K tile (64 deep) = 4 phases, one per 16-deep k step ks: 4 A + 4 B fragments, 16 MFMAs; the
+// fragments of phase ks + 1 are read during phase ks.
+// LDS: the [64 k][128 x] swz<128> half-tile images of K12, laid out half-tile-major
+// [A0 s0, A0 s1, A1 s0, A1 s1, B0 s0, ...] so that a wave's two stages of one operand sit within the
+// 16-bit ds_read immediate of one address: every fragment read is one of 8 per-lane address
+// registers per operand (4 x blocks x 2 row quads: the XOR swizzle is per lane) + an immediate.
+// Each half-tile is split by k half (rows 0..31 = part K0: k steps 0, 1; rows 32..63 = part K1:
+// k steps 2, 3; 8 of its 16 1-KiB DMA pieces each); wave w streams half-tile w (A0, A1, B0, B1).
+//   reads: P3(t-1) -> ks 0 of tile t (K0); P0(t) -> ks 1 (K0); P1(t) -> ks 2 (K1); P2(t) -> ks 3 (K1).
+//   P1(t): RAW for K1(t) + WAR for K0(t) (last read in P0): counted vmcnt + lgkmcnt(0) + barrier,
+//          then K0(t + 2) is issued into the same stage.
+//   P3(t): RAW for K0(t + 1) + WAR for K1(t) (last read in P2), then K1(t + 2).
+//   vmcnt(16) at both: a wave's pieces retire in issue order and two parts (16 pieces) were issued
+//   after the one waited for.  Latency cover: 6 phases per part (1.5 K tiles).
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 1) void gemm4_kernel(const Args p) {
+  static_assert(A_COL && B_COL, "K12W: weight gradient (both operands k-major)");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  int wid = blockIdx.x;
+  {
+    const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
+    wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
+  }
+  const int ntile = p.i_tiles * p.j_tiles;
+  const int split = wid / ntile;
+  wid -= split * ntile;
+  const int it = wid % p.i_tiles, jt = wid / p.i_tiles;
+  const int64_t i0 = (int64_t)it * kT, j0 = (int64_t)jt * kT;
+  const int64_t kbeg = (int64_t)split * p.kper;
+  const int64_t klen = p.K - kbeg < p.kper ? p.K - kbeg : p.kper;
+  const int nk = (int)(klen / kBK);
+
+  // this wave's DMA half-tile (0, 1: A halves; 2, 3: B halves) and its 8 per-lane piece offsets
+  // (rows 4e .. 4e + 3 of part K0; part K1 is 32 rows further)
+  const bool isA = wave < 2;
+  const uint16_t* const op = isA ? p.a : p.b;
+  const int64_t ld = isA ? p.lda : p.ldb;
+  const int64_t x0 = isA ? i0 + 128 * wave : j0 + 128 * (wave - 2);
+  int off[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) off[e] = (int)dma_offset<true>(e, lane, ld, x0, isA ? p.I : p.J);
+  // half-tile h of stage st at (2h + st) * kHalf
+  auto issue = [&](int t, int st, int part) {
+    const uint16_t* src = op + (kbeg + (int64_t)t * kBK + 32 * part) * ld + x0;
+    uint16_t* dst = smem + (2 * wave + st) * kHalf + 8 * part * 512;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) glds16((const void*)(src + off[e]), (lds_void*)(dst + e * 512));
+  };
+
+  f32x16 ac[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) ac[a][b] = zero16();
+
+  // per-lane LDS byte addresses of the 32x32x16 operand reads (mf::lds_col<128>: two
+  // ds_read_b64_tr_b16, row quads hq = 0 / 1) of x block xb (32 columns):
+  //   byte(st, ks, xb, hq) = st * 16 KiB + ks * 4 KiB + lanepart(hq) + 64 * (xb ^ (f(hq) >> 2))
+  const int g = lane >> 4, i = lane & 15;
+  unsigned adA[4][2], adB[4][2];
+  {
+    const unsigned baseA = (unsigned)(size_t)(smem + 2 * wr * kHalf);
+    const unsigned baseB = (unsigned)(size_t)(smem + 2 * (2 + wc) * kHalf);
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {
+      const int row = 8 * (g >> 1) + (i >> 2) + 4 * hq;
+      const int f = ((row & 3) << 2) | ((row >> 2) & 3);
+      const int cl = 2 * (g & 1) + ((i & 3) >> 1);
+      const unsigned lanepart = (unsigned)(row * 256 + 16 * (cl ^ (f & 3)) + 8 * (i & 1));
+#pragma unroll
+      for (int xb = 0; xb < 4; ++xb) {
+        const unsigned o = lanepart + 64u * (unsigned)(xb ^ (f >> 2));
+        adA[xb][hq] = baseA + o;
+        adB[xb][hq] = baseB + o;
+      }
+    }
+  }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto frag = [&](const unsigned (&ad)[2], auto st_c, auto ks_c) {
+    constexpr int imm = decltype(st_c)::value * kHalf * 2 + decltype(ks_c)::value * 4096;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(ad[0] + imm));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(ad[1] + imm));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  using C2 = std::integral_constant<int, 2>;
+  using C3 = std::integral_constant<int, 3>;
+
+  bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+  auto rd = [&](bf16x8 (&fa)[4], bf16x8 (&fb)[4], auto st_c, auto ks_c) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      fa[x] = frag(adA[x], st_c, ks_c);
+      fb[x] = frag(adB[x], st_c, ks_c);
+    }
+  };
+  auto mma = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4], int a_lo, int a_hi) {
+#pragma unroll
+    for (int a = a_lo; a < a_hi; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) ac[a][b] = mf::mfma(fa[a], fb[b], ac[a][b]);
+  };
+
+  // The loop has no branch but its own: every K tile issues the parts of tile t + 2 (clamped to
+  // the last tile: a harmless reload into the stage nobody reads again) and reads the first
+  // fragments of tile t + 1 (unused after the last tile), so every wait count is a constant and
+  // the accumulators stay in place.
+  // (a split whose share of the reduction is empty -- possible for the last splits when the
+  // split count does not divide the K tiles -- issues nothing and contributes zeros)
+  if (nk > 0) {
+  issue(0, 0, 0);
+  issue(0, 0, 1);
+  issue(nk > 1 ? 1 : 0, 1, 0);
+  issue(nk > 1 ? 1 : 0, 1, 1);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  barrier();
+  rd(fa0, fb0, C0{}, C0{});
+  // K tile t in stage ST (compile-time: the loop runs tiles in pairs).  Each phase: the first 4
+  // MFMAs (they consume fragments whose reads are long done), the next phase's 16 reads, the
+  // other 12 MFMAs.
+  auto ktile = [&](int t, auto st_c) {
+    using ST = decltype(st_c);
+    using NST = std::integral_constant<int, 1 - ST::value>;
+    const int t2 = t + 2 < nk ? t + 2 : nk - 1;
+    // ---- P0 (ks 0)
+    mma(fa0, fb0, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(fa1, fb1, ST{}, C1{});
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(fa0, fb0, 1, 4);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P1 (ks 1): RAW K1(t), WAR K0(t); then K0(t + 2)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    issue(t2, ST::value, 0);
+    mma(fa1, fb1, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(fa0, fb0, ST{}, C2{});
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(fa1, fb1, 1, 4);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P2 (ks 2)
+    mma(fa0, fb0, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(fa1, fb1, ST{}, C3{});
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(fa0, fb0, 1, 4);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- P3 (ks 3): RAW K0(t + 1), WAR K1(t); then K1(t + 2)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+    issue(t2, ST::value, 1);
+    mma(fa1, fb1, 0, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(fa0, fb0, NST{}, C0{});
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mma(fa1, fb1, 1, 4);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(t, C0{});
+    ktile(t + 1, C1{});
+  }
+  if (t < nk) ktile(t, C0{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped reloads
+  }
+
+  // accumulator (a, b) register r of lane half h: i row wr*128 + 32a + acc_row(r, h), j col
+  // wc*128 + 32b + (lane & 31); a lane's registers 4m..4m+3 are 4 consecutive i
+  const int h = lane >> 5, l32 = lane & 31;
+  auto for_each_group = [&](auto&& fn) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          fn(wr * 128 + 32 * a + 8 * m + 4 * h, wc * 128 + 32 * b + l32,
+             f32x4{ac[a][b][4 * m], ac[a][b][4 * m + 1], ac[a][b][4 * m + 2], ac[a][b][4 * m + 3]});
+  };
+  if (p.ws != nullptr) {
+    float* slab = p.ws + (int64_t)split * p.J * p.I;
+    for_each_group([&](int il, int jl, const f32x4& v) {
+      const int64_t ig = i0 + il, jg = j0 + jl;
+      if (ig < p.I && jg < p.J) *reinterpret_cast<f32x4*>(slab + jg * p.I + ig) = v;
+    });
+    return;
+  }
+  for_each_group([&](int il, int jl, const f32x4& v) {
+    const int64_t ig = i0 + il, jg = j0 + jl;
+    if (ig < p.I && jg < p.J) {
+      float w[4] = {v[0], v[1], v[2], v[3]};
+      if (p.res != nullptr) {
+        const u32x2 r = *reinterpret_cast<const u32x2*>(p.res + jg * p.ldr + ig);
+        w[0] += bf16_to_f32((unsigned short)(r[0] & 0xffffu));
+        w[1] += bf16_to_f32((unsigned short)(r[0] >> 16));
+        w[2] += bf16_to_f32((unsigned short)(r[1] & 0xffffu));
+        w[3] += bf16_to_f32((unsigned short)(r[1] >> 16));
+      }
+      const unsigned lo = (unsigned)f32_to_bf16(w[0]) | ((unsigned)f32_to_bf16(w[1]) << 16);
+      const unsigned hi = (unsigned)f32_to_bf16(w[2]) | ((unsigned)f32_to_bf16(w[3]) << 16);
+      *reinterpret_cast<u32x2*>(p.out + jg * p.ldo + ig) = u32x2{lo, hi};
+    }
+  });
+}
+
 template <bool A_COL, bool B_COL>
 hipError_t launch(Args& p, hipStream_t s) {
   p.i_tiles = (int)((p.I + kT - 1) / kT);
@@ -476,4 +709,41 @@ hipError_t madnn_linear_wgrad(const void* dy, const void* x, void* dw, float* ws
   return hipGetLastError();
 }
 
+// K12W weight gradient (same contract as madnn_linear_wgrad; the split count from madnn_wgrad_splits)
+hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
+                               int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  if (M % kBK || !madnn_gemm_supported(K, N, M, K, N)) return hipErrorInvalidValue;
+  if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
+  Args p{};
+  p.a = static_cast<const uint16_t*>(x);
+  p.lda = K;
+  p.b = static_cast<const uint16_t*>(dy);
+  p.ldb = N;
+  p.out = static_cast<uint16_t*>(dw);
+  p.ldo = K;
+  p.res = accumulate && splits <= 1 ? static_cast<const uint16_t*>(dw) : nullptr;
+  p.ldr = K;
+  p.I = K;
+  p.J = N;
+  p.K = M;
+  p.splits = splits > 1 ? splits : 1;
+  const int64_t nk = M / kBK;
+  p.kper = ((nk + p.splits - 1) / p.splits) * kBK;
+  p.ws = p.splits > 1 ? ws : nullptr;
+  p.i_tiles = (int)((p.I + kT - 1) / kT);
+  p.j_tiles = (int)((p.J + kT - 1) / kT);
+  const int64_t grid = (int64_t)p.i_tiles * p.j_tiles * p.splits;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm4_kernel<true, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || p.splits == 1) return e;
+  const int64_t n = N * K;
+  int64_t blocks = (n / 8 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, static_cast<uint16_t*>(dw),
+                     p.splits, n, accumulate);
+  return hipGetLastError();
+}
+
 }  // extern "C"
+

@@ -113,3 +113,31 @@ extern "C" hipError_t madnn_hwq_spin(int64_t spin_us, hipStream_t s) {
   hipLaunchKernelGGL(hwq_spin_kernel, dim3(1), dim3(madnn::kWave), 0, s, static_cast<long long>(spin_us) * 100);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// Attention-backward dQ floor probe: the f32 atomic traffic a ONE-pass backward (dQ accumulated
+// inside the dK / dV kernel, cdna_hip_programming.md 'Attention backward') must issue, with no
+// other work.  Workgroup (bh, key block) adds one value to every dQ[bh][q][d] with q >= the block's
+// first key (causal) -- one global_atomic_add_f32 (no return) per dQ element per key block, 16 B
+// apart per lane quad, exactly the fused design's add pattern.  Its time is a floor for that
+// design; compare it with the separate dQ kernel it would replace (bench/attn_dq_floor.py).
+namespace {
+
+__global__ __launch_bounds__(256) void dq_atomic_floor_kernel(float* __restrict__ dq, int S, int D, int kblock,
+                                                              int nkb, int causal, float v) {
+  const int bh = blockIdx.x / nkb, kb = blockIdx.x % nkb;
+  const int q0 = causal ? kb * kblock : 0;
+  float* base = dq + (int64_t)bh * S * D;
+  const int64_t n = (int64_t)(S - q0) * D;
+  for (int64_t e = threadIdx.x; e < n; e += 256) unsafeAtomicAdd(base + (int64_t)q0 * D + e, v);
+}
+
+}  // namespace
+
+extern "C" hipError_t madnn_dq_atomic_floor(float* dq, int BH, int S, int D, int kblock, int causal, hipStream_t s) {
+  if (BH <= 0 || S <= 0 || D <= 0 || kblock <= 0) return hipErrorInvalidValue;
+  const int nkb = (S + kblock - 1) / kblock;
+  hipLaunchKernelGGL(dq_atomic_floor_kernel, dim3((unsigned)(BH * nkb)), dim3(256), 0, s, dq, S, D, kblock, nkb,
+                     causal, 1.0e-3f);
+  return hipGetLastError();
+}

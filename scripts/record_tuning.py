@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--gpt2-batches", default="128,64,32,16,8,4")
     ap.add_argument("--bert-batches", default="128")
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--keep-table", action="store_true",
+                    help="start from the shipped choice table (time only the shapes it lacks) instead of an empty one")
+    ap.add_argument("--retime", default="",
+                    help="with --keep-table: comma list of table:kind entries to drop and time afresh, e.g. "
+                         "wgrad:linear (every Linear weight gradient, with K12W as a candidate)")
     args = ap.parse_args()
     out = Path(args.out)
     db = out / "miopen"
@@ -43,7 +48,8 @@ def main():
         if f.is_file():
             shutil.copy2(f, db / f.name)
     os.environ["MIOPEN_USER_DB_PATH"] = str(db)
-    os.environ["MADNN_TUNE_TABLE"] = "0"      # decide every shape afresh
+    if not args.keep_table:
+        os.environ["MADNN_TUNE_TABLE"] = "0"      # decide every shape afresh
 
     import torch
     import torch.nn.functional as F
@@ -52,6 +58,14 @@ def main():
     import madnn.ops as ops
 
     madnn.init()
+    if args.keep_table:
+        ops.load_kernels()
+        tables = {"wgrad": ops._WGRAD_CHOICE, "gelu_fwd": ops._GELU_FWD_CHOICE, "dgelu": ops._DGELU_CHOICE,
+                  "dgrad": ops._DGRAD_CHOICE}
+        for item in [v for v in args.retime.split(",") if v]:
+            tab, kind = item.split(":")
+            for k in [k for k in tables[tab] if k and k[0] == kind]:
+                del tables[tab][k]
     dev = madnn.device()
     rec = []
 
@@ -127,7 +141,8 @@ def main():
     (out / "record.json").write_text(json.dumps(rec, indent=1) + "\n")
     # the per-shape A/B behind every choice (ms for 3 calls of each implementation)
     (out / "measurements.json").write_text(json.dumps(ops.tuning_measurements(), indent=1) + "\n")
-    print(json.dumps({"choices": len(ops._WGRAD_CHOICE) + len(ops._GELU_FWD_CHOICE) + len(ops._DGELU_CHOICE),
+    print(json.dumps({"choices": len(ops._WGRAD_CHOICE) + len(ops._GELU_FWD_CHOICE) + len(ops._DGELU_CHOICE)
+                      + len(ops._DGRAD_CHOICE),
                       "miopen_db": sorted(p.name for p in db.iterdir())}), flush=True)
 
 

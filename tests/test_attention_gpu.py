@@ -55,6 +55,35 @@ def test_attention_fwd_bwd(cuda, B, S, H, HKV, D, causal):
         assert _rel(g, gr) < 2e-2, name
 
 
+@pytest.mark.parametrize("B,S,H,HKV,D", [(1, 4096, 32, 8, 128), (2, 2048, 16, 16, 64)])
+def test_attention_bench_shapes_causal(cuda, B, S, H, HKV, D):
+    """The shapes the benches time: Llama-3 8B's (S = 4096, D = 128, GQA 32 / 8) and a long
+    D = 64 case, causal, forward and all three gradients against fp32 SDPA (the reference runs
+    one query-head group at a time to bound its memory)."""
+    torch.manual_seed(4)
+    q = torch.randn(B, S, H, D, device=cuda).bfloat16().requires_grad_(True)
+    k = torch.randn(B, S, HKV, D, device=cuda).bfloat16().requires_grad_(True)
+    v = torch.randn(B, S, HKV, D, device=cuda).bfloat16().requires_grad_(True)
+    o = ops.attention(q, k, v, causal=True)
+    do = torch.randn_like(o)
+    gq, gk, gv = torch.autograd.grad(o, (q, k, v), do)
+    g = H // HKV
+    rq, rk, rv = torch.zeros_like(gq, dtype=torch.float32), torch.zeros_like(gk, dtype=torch.float32), \
+        torch.zeros_like(gv, dtype=torch.float32)
+    orf = torch.empty_like(o, dtype=torch.float32)
+    for j in range(HKV):   # kv head j and its g query heads
+        qs = slice(j * g, (j + 1) * g)
+        qr = q[:, :, qs].detach().float().requires_grad_(True)
+        kr = k[:, :, j:j + 1].detach().float().requires_grad_(True)
+        vr = v[:, :, j:j + 1].detach().float().requires_grad_(True)
+        oj = _ref(qr, kr, vr, True, D ** -0.5)
+        a, b, c = torch.autograd.grad(oj, (qr, kr, vr), do[:, :, qs].float())
+        orf[:, :, qs], rq[:, :, qs], rk[:, :, j:j + 1], rv[:, :, j:j + 1] = oj.detach(), a, b, c
+    assert _rel(o, orf) < 1e-2, _rel(o, orf)
+    for got, ref, name in ((gq, rq, "dq"), (gk, rk, "dk"), (gv, rv, "dv")):
+        assert _rel(got, ref) < 2e-2, (name, _rel(got, ref))
+
+
 @pytest.mark.parametrize("H,HKV,D", [(4, 4, 64), (8, 2, 128)])
 def test_attention_qkvpacked_inplace_grad(cuda, H, HKV, D):
     torch.manual_seed(1)

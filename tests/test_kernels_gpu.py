@@ -410,9 +410,9 @@ def test_lt_linear_epilogues_match_fp32(cuda, gelu, res, bias, M, K, N):
     w = (torch.randn(N, K, device=cuda, dtype=torch.bfloat16) * K ** -0.5).requires_grad_()
     b = (torch.randn(N, device=cuda, dtype=torch.bfloat16) * 0.1).requires_grad_() if bias else None
     r = torch.randn(M, N, device=cuda, dtype=torch.bfloat16, requires_grad=True) if res else None
+    # where hipBLASLt refuses this epilogue kind on the box (ops._LT_FAILED), ops.linear took its
+    # fallback path: that path is what the comparisons below then verify, never skipped
     y = madnn.ops.linear(x, w, b, gelu=gelu, residual=r)
-    if (gelu, res) in madnn.ops._LT_FAILED:
-        pytest.skip(f"hipBLASLt offers no epilogue for this kind on this box: {madnn.ops._LT_FAILED[(gelu, res)]}")
     xf, wf = x.detach().float().requires_grad_(), w.detach().float().requires_grad_()
     bf = b.detach().float().requires_grad_() if bias else None
     rf = r.detach().float().requires_grad_() if res else None
