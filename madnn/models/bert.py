@@ -137,5 +137,5 @@ class BertForPreTraining(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]
 
-    def loss_fn(self, logits, targets):
-        return mlm_loss(logits, targets, vocab=self.config.vocab_size)
+    def loss_fn(self, logits, targets, scale: float = 1.0):
+        return mlm_loss(logits, targets, vocab=self.config.vocab_size, scale=scale)

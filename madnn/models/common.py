@@ -21,18 +21,19 @@ from torch import nn
 from .. import ops
 
 
-def causal_lm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None) -> torch.Tensor:
+def causal_lm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None, scale: float = 1.0) -> torch.Tensor:
     """Next-token cross entropy (shifted), fp32 math; on the GPU one fused K6 kernel
-    each way over the bf16 logits (no fp32 copy, no slicing copies)."""
+    each way over the bf16 logits (no fp32 copy, no slicing copies).  ``scale``: a microbatched
+    step's 1 / M (``ops.scaled_loss``)."""
     from .. import ops
 
-    return ops.cross_entropy(logits, targets, shift=True, vocab=vocab)
+    return ops.cross_entropy(logits, targets, shift=True, vocab=vocab, scale=scale)
 
 
-def mlm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None) -> torch.Tensor:
+def mlm_loss(logits: torch.Tensor, targets: torch.Tensor, vocab: int = None, scale: float = 1.0) -> torch.Tensor:
     from .. import ops
 
-    return ops.cross_entropy(logits, targets, shift=False, vocab=vocab, ignore_index=-100)
+    return ops.cross_entropy(logits, targets, shift=False, vocab=vocab, ignore_index=-100, scale=scale)
 
 
 def linear(mod: nn.Module, x: torch.Tensor, gelu: bool = False, residual: torch.Tensor = None) -> torch.Tensor:

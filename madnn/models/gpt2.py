@@ -140,8 +140,8 @@ class GPT2(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.h, self.head]
 
-    def loss_fn(self, logits, targets):
-        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size)
+    def loss_fn(self, logits, targets, scale: float = 1.0):
+        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size, scale=scale)
 
     def flops_per_token(self) -> float:
         c = self.config

@@ -116,5 +116,5 @@ class Llama(nn.Module):
     def pipeline_layers(self):
         return [self.embed, *self.layers, self.head]
 
-    def loss_fn(self, logits, targets):
-        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size)
+    def loss_fn(self, logits, targets, scale: float = 1.0):
+        return causal_lm_loss(logits, targets, vocab=self.config.vocab_size, scale=scale)

@@ -475,11 +475,15 @@ def max_pool2d(x: torch.Tensor, kernel_size, stride=None, padding=0, dilation=1,
 # ---------------------------------------------------------------------- K6
 class _XentFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, targets, shift, vocab, ignore_index):
+    def forward(ctx, logits, targets, shift, vocab, ignore_index, scale):
         lg = logits.contiguous()
         tg = targets.contiguous()
         used = tg[:, 1:] if shift else tg
-        cnt = ((used != ignore_index) & (used >= 0) & (used < vocab)).sum().clamp(min=1).to(torch.float32)
+        # the loss is ``scale`` x the mean: a microbatch's 1 / M folded in here reaches the fused
+        # gradient at forward time, so its backward sees an upstream gradient of exactly 1 and the
+        # rescale pass over the logit gradient exits at once (at 32 x 1024 tokens per microbatch that
+        # pass was 1.3 ms of GPT-2 medium's LM head, profiles/r6_gpt2m_mb32_steady_steps.md)
+        cnt = ((used != ignore_index) & (used >= 0) & (used < vocab)).sum().clamp(min=1).to(torch.float32) / scale
         ctx.grad = None
         ctx.fused = bool(ctx.needs_input_grad[0] and XENT_FUSED and _xent_fused_ok(lg))
         if ctx.fused:
@@ -501,11 +505,11 @@ class _XentFn(torch.autograd.Function):
                 raise RuntimeError("madnn cross_entropy: the fused (K6f) gradient was already consumed by an "
                                    "earlier backward; set MADNN_XENT_FUSED=0 to backward through it twice")
             torch.ops.madnn.xent_rescale(grad, g.to(torch.float32).reshape(1))
-            return grad, None, None, None, None
+            return grad, None, None, None, None, None
         lg, tg, lse, cnt = ctx.saved_tensors
         gscale = (g.to(torch.float32) / cnt).reshape(1)
         grad = torch.ops.madnn.xent_bwd(lg, tg, lse, ctx.shift, ctx.vocab, ctx.ignore_index, gscale)
-        return grad, None, None, None, None
+        return grad, None, None, None, None, None
 
 
 XENT_FUSED = os.environ.get("MADNN_XENT_FUSED", "1") != "0"  # A/B switch
@@ -520,8 +524,9 @@ def _xent_fused_ok(lg: torch.Tensor) -> bool:
 
 
 def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, *, shift: bool = False, vocab: Optional[int] = None,
-                  ignore_index: int = -100) -> torch.Tensor:
-    """Mean token cross entropy of ``logits[..., :vocab]`` (fp32 math, one fused kernel each way).
+                  ignore_index: int = -100, scale: float = 1.0) -> torch.Tensor:
+    """Mean token cross entropy of ``logits[..., :vocab]`` (fp32 math, one fused kernel each way),
+    times ``scale`` (a microbatched step's 1 / M, applied inside the kernels: see _XentFn).
 
     ``shift=True`` is the causal-LM form: logits[:, t] predicts targets[:, t+1] and the
     last position carries no loss — no slicing copies of the logit matrix are made.
@@ -529,8 +534,24 @@ def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, *, shift: bool = 
     v = vocab or logits.size(-1)
     if _is_dev(logits) and logits.dtype in (torch.bfloat16, torch.float32, torch.float16):
         _need_native("cross_entropy")
-        return _XentFn.apply(logits, targets, shift, v, ignore_index)
-    return reference.cross_entropy(logits, targets, shift=shift, vocab=v, ignore_index=ignore_index)
+        return _XentFn.apply(logits, targets, shift, v, ignore_index, float(scale))
+    out = reference.cross_entropy(logits, targets, shift=shift, vocab=v, ignore_index=ignore_index)
+    return out * scale if scale != 1.0 else out
+
+
+def scaled_loss(fn, out, targets, scale: float):
+    """``fn(out, targets) * scale`` -- with the scale passed INTO ``fn`` when it takes one (madnn's
+    model losses: the cross entropy folds it into its fused gradient), else applied after."""
+    import inspect
+
+    try:
+        takes = "scale" in inspect.signature(fn).parameters
+    except (TypeError, ValueError):
+        takes = False
+    if takes and scale != 1.0:
+        return fn(out, targets, scale=scale)
+    loss = fn(out, targets)
+    return loss * scale if scale != 1.0 else loss
 
 
 # ---------------------------------------------------------------------- K8

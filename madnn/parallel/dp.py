@@ -537,6 +537,8 @@ class DataParallel(nn.Module):
     def train_step(self, inputs, targets=None, loss_fn=None, microbatches: int = 1):
         """Forward + backward of one (optionally micro-batched) step; same protocol as
         ``PipelineEngine.train_step`` so scripts can switch strategy without changes."""
+        from ..ops import scaled_loss
+
         fn = loss_fn or getattr(self, "loss_fn", None)
         if fn is None:
             raise ValueError("train_step needs loss_fn= (or model.loss_fn)")
@@ -546,7 +548,7 @@ class DataParallel(nn.Module):
         for i, (x, t) in enumerate(zip(xs, ts)):
             ctx = self.no_sync() if i < len(xs) - 1 else contextlib.nullcontext()
             with ctx:
-                loss = fn(self(x), t) / len(xs)
+                loss = scaled_loss(fn, self(x), t, 1.0 / len(xs))
                 loss.backward()
             total = loss.detach() if total is None else total + loss.detach()
         return total

@@ -46,7 +46,7 @@ from torch.utils.checkpoint import checkpoint
 from .. import comm
 from .. import runtime as rt
 from ..config import Config
-from ..ops import native_runtime
+from ..ops import native_runtime, scaled_loss
 from ..utils.logging import get_logger
 from .dp import DataParallel, _cast_inputs
 
@@ -1064,7 +1064,7 @@ class PipelineEngine:
                 acts_in[(c, m)] = x
                 y = self.chunks[c](x)
                 if vs == SV - 1:
-                    loss = self.loss_fn(y, ts[m]) / M
+                    loss = scaled_loss(self.loss_fn, y, ts[m], 1.0 / M)
                     losses[(c, m)] = loss
                     total.add_(loss.detach().float())
                 else:

@@ -283,6 +283,26 @@ def test_fused_cross_entropy(cuda, V, ld, shift, dt):
         assert logits.grad[..., V:].abs().max() == 0
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_cross_entropy_scale_is_folded_into_the_gradient(cuda, fused, monkeypatch):
+    """``cross_entropy(..., scale=s)`` (a microbatched step's 1 / M, ops.scaled_loss) equals
+    ``s * cross_entropy(...)`` in value and logit gradient, for the one-pass (K6f) and two-pass
+    kernels -- and the one-pass gradient is finished at forward time (upstream gradient 1)."""
+    monkeypatch.setattr(ops, "XENT_FUSED", fused)
+    torch.manual_seed(4)
+    V = 50257
+    base = (torch.randn(2, 33, 50304, device=cuda) * 3).bfloat16()
+    tg = torch.randint(0, V, (2, 33), device=cuda)
+    a = base.clone().requires_grad_(True)
+    la = ops.cross_entropy(a, tg, shift=True, vocab=V, scale=0.25)
+    la.backward()
+    b = base.clone().requires_grad_(True)
+    lb = ops.cross_entropy(b, tg, shift=True, vocab=V)
+    (lb * 0.25).backward()
+    torch.testing.assert_close(la.float(), 0.25 * lb.detach().float(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=1e-6, rtol=1e-2)
+
+
 @pytest.mark.parametrize("V,ld", [(50257, 50304), (128256, 128256), (130, 136)])
 def test_one_pass_cross_entropy_matches_two_pass(cuda, V, ld, monkeypatch):
     """K6f (loss + finished gradient in one pass over the logits, backward only rescales) against the

@@ -963,3 +963,33 @@ def test_linear_tee_sums_the_residual_gradient_in_the_data_gradient():
     y, _ = ops._LinearTeeFn.apply(x, w, b)
     (y * gy).sum().backward()
     torch.testing.assert_close(x.grad, gy.reshape(-1, 24).mm(w.detach()).view_as(x), atol=1e-5, rtol=1e-5)
+
+
+def test_scaled_loss_passes_the_scale_into_scale_aware_losses():
+    """ops.scaled_loss: a loss function that takes ``scale`` receives it (madnn's model losses fold
+    a microbatch's 1 / M into the fused cross entropy); any other is multiplied afterwards."""
+    from madnn import ops
+
+    seen = []
+
+    def aware(out, t, scale=1.0):
+        seen.append(scale)
+        return (out - t).square().mean() * scale
+
+    def plain(out, t):
+        return (out - t).square().mean()
+
+    out, t = torch.randn(4, 3), torch.randn(4, 3)
+    ref = (out - t).square().mean() * 0.25
+    torch.testing.assert_close(ops.scaled_loss(aware, out, t, 0.25), ref)
+    torch.testing.assert_close(ops.scaled_loss(plain, out, t, 0.25), ref)
+    torch.testing.assert_close(ops.scaled_loss(plain, out, t, 1.0), (out - t).square().mean())
+    assert seen == [0.25]
+    # the zoo's losses take it (CPU reference path)
+    from madnn.models.gpt2 import GPT2, gpt2_config
+
+    torch.manual_seed(0)
+    m = GPT2(gpt2_config("gpt2-tiny"))
+    ids = torch.randint(0, 512, (2, 16))
+    logits = m(ids)
+    torch.testing.assert_close(ops.scaled_loss(m.loss_fn, logits, ids, 0.5), 0.5 * m.loss_fn(logits, ids))
