@@ -27,7 +27,7 @@ from torch import nn
 from ..nn.conv import FusedConv2d
 from ..nn.norm import FusedBatchNorm2d as BN
 from ..nn.norm import FusedGlobalAvgPool2d, FusedMaxPool2d
-from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_epi_supported, bn_relu_conv1x1_supported,
+from ..ops import (batch_norm_add_bn_relu, bn_relu_conv1x1, bn_relu_conv1x1_epi_supported,
                    bn_relu_conv3x3, conv1x1_route,
                    bn_relu_conv3x3_supported, bn_relu_maxpool, bn_relu_maxpool_supported)
 
@@ -127,13 +127,10 @@ class Bottleneck(nn.Module):
         return self.conv2(out, stats=True)
 
     def _bn2_conv3(self, y, st):
-        """conv3(relu(bn2(y))): on K9 the bn2 apply + ReLU run in conv3's operand prologue
-        (forward and weight grad), so relu(bn2(y)) is never written to HBM."""
+        """conv3(relu(bn2(y))): when conv3's data grad runs on K9, bn2's backward reduction is taken
+        in that kernel's epilogue."""
         if isinstance(y, torch.Tensor) and isinstance(self.bn2, BN) and isinstance(self.conv3, FusedConv2d) \
-                and self.conv3._k9(y) \
-                and (bn_relu_conv1x1_supported(y, self.bn2, self.conv3.weight)
-                     or bn_relu_conv1x1_epi_supported(y, self.bn2, self.conv3.weight)):
-            # K9 BN prologue (opt-in) or bn2's backward reduction in conv3's K9 data-grad epilogue
+                and self.conv3._k9(y) and bn_relu_conv1x1_epi_supported(y, self.bn2, self.conv3.weight):
             return bn_relu_conv1x1(y, self.bn2, self.conv3.weight, stats_in=st, stats=True)
         out = self.bn2(y, relu=True, stats=st)
         return self.conv3(out, stats=True)

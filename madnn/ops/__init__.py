@@ -294,10 +294,6 @@ class _BNFn(torch.autograd.Function):
         # mask instead of writing the masked copy of dy (one activation-sized write less)
         ctx.defer = (DEFER_RES_MASK and relu and residual is not None and mask.numel() > 0
                      and getattr(residual, "_madnn_defer_mask", False))
-        if BN_SUM_IN_DGRAD and training and relu and residual is not None and mask.numel() > 0 and x.dtype == torch.bfloat16:
-            # a consumer whose data grad runs on K9 (the next identity block's conv1) may take this BN's
-            # backward sums in that kernel's epilogue: it needs the BN input and the ReLU bit mask
-            y._madnn_bnsrc = (x, mask)
         return y
 
     @staticmethod
@@ -305,14 +301,8 @@ class _BNFn(torch.autograd.Function):
         x, mask, weight, mean, invstd, scale, shift = ctx.saved_tensors
         need_w = ctx.has_w and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         defer = ctx.defer and dy.dtype == x.dtype and dy.stride() == x.stride()
-        part = _attached(dy, "_madnn_bnpart")
-        if part is not None and ctx.has_res and dy.dtype == x.dtype and dy.stride() == x.stride():
-            # the reduction came from the K9 data grad that produced dy (_Conv1x1Fn, conv1x1_dgrad_bnres)
-            dx, dw, db, dres = torch.ops.madnn.bn_bwd_ext_res(dy, x, weight, mean, invstd, scale, shift, part,
-                                                              mask, not defer)
-        else:
-            dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
-                                                      mean, invstd, scale, shift, ctx.relu, need_w, not defer)
+        dx, dw, db, dres = torch.ops.madnn.bn_bwd(dy, x, mask if mask.numel() else None, ctx.has_res, weight,
+                                                  mean, invstd, scale, shift, ctx.relu, need_w, not defer)
         if defer:
             dres = dy.view_as(dy)
             _attach(dres, "_madnn_resmask", mask)
@@ -321,8 +311,6 @@ class _BNFn(torch.autograd.Function):
 
 
 DEFER_RES_MASK = os.environ.get("MADNN_DEFER_RES_MASK", "1") != "0"  # A/B switch (see _BNFn.forward)
-SUB_IN_DGRAD = os.environ.get("MADNN_SUB_IN_DGRAD", "0") == "1"  # off: A/B -0.28 % (docs/PERF.md)
-BN_SUM_IN_DGRAD = os.environ.get("MADNN_BN_SUM_IN_DGRAD", "0") == "1"  # off: A/B -0.23 % (docs/PERF.md)
 
 
 def _apply_bit_mask(t: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
@@ -771,9 +759,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         else:
             y = torch.nn.functional.conv2d(x, w) if x.dim() == 4 else torch.mm(x, w.reshape(w.size(0), -1).t())
             part = x.new_empty((0, 2, w.size(0)), dtype=torch.float32)
-        src = getattr(x, "_madnn_bnsrc", None) if (BN_SUM_IN_DGRAD and fork == 1 and dgrad == "k9") else None
-        ctx.bnsum = src is not None and src[0].shape == x.shape and src[0].stride() == x.stride()
-        ctx.save_for_backward(x, w, *(src if ctx.bnsum else ()))
+        ctx.save_for_backward(x, w)
         ctx.route = (dgrad, wgrad)
         ctx.fork = fork
         ctx.mark_non_differentiable(part)
@@ -785,7 +771,7 @@ class _Conv1x1Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dpart, dfork=None):
-        x, w = ctx.saved_tensors[:2]
+        x, w = ctx.saved_tensors
         dgrad, wgrad = ctx.route
         dy = _nhwc(dy.to(x.dtype))
         sub = None
@@ -798,17 +784,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             res, resmask = _apply_bit_mask(res, resmask), None
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if dgrad == "k9" and ctx.bnsum:
-                # x = relu(bn(y) + r) of the previous block (_BNFn): that BN's backward sums come out of
-                # this epilogue, over the gradient it writes (no reduction pass over dx and y)
-                bny, bnmask = ctx.saved_tensors[2:]
-                dx, part = torch.ops.madnn.conv1x1_dgrad_bnres(dy, w, res, resmask, bny, bnmask)
-                _attach(dx, "_madnn_bnpart", part)
-            elif dgrad == "k9" and sub is not None and res is None and SUB_IN_DGRAD and x.dim() == 4:
-                # the downsample path's compact gradient is added at the even pixels in the epilogue
-                dx = torch.ops.madnn.conv1x1_dgrad(dy, w, _nhwc(sub.to(x.dtype)), None, True)
-                sub = None
-            elif dgrad == "k9":
+            if dgrad == "k9":
                 dx = torch.ops.madnn.conv1x1_dgrad(dy, w, res, resmask)
             else:
                 w2 = w.reshape(w.size(0), -1)
@@ -867,38 +843,6 @@ def conv1x1(x: torch.Tensor, w: torch.Tensor, *, stats: bool = False, fork: bool
     return ret[0] if len(ret) == 1 else tuple(ret)
 
 
-class _BNReluConv1x1Fn(torch.autograd.Function):
-    """``conv1x1(relu(bn(y)), w)`` in training with the BatchNorm apply + ReLU inside K9's operand
-    prologue (forward and weight grad): ``relu(bn(y))`` never exists in HBM.  Backward: the data
-    grad (K9 / hipBLASLt per :func:`conv1x1_route`) gives d relu(bn(y)), then one K5 backward
-    (ReLU mask recomputed from y) gives dy and the BN parameter gradients."""
-
-    @staticmethod
-    def forward(ctx, y, w, bn_w, bn_b, bn, stats_in, want_stats):
-        mean, invstd, scale, shift = torch.ops.madnn.bn_coef(y, bn_w, bn_b, bn.running_mean, bn.running_var,
-                                                             bn.num_batches_tracked, float(bn.momentum),
-                                                             float(bn.eps), stats_in)
-        out, part = torch.ops.madnn.conv1x1_fwd(y, w, bool(want_stats), scale, shift)
-        ctx.save_for_backward(y, w, bn_w, mean, invstd, scale, shift)
-        ctx.dgrad = conv1x1_route(y.size(1), w.size(0))[1]
-        ctx.mark_non_differentiable(part)
-        return out, part
-
-    @staticmethod
-    def backward(ctx, dout, _dpart):
-        y, w, bn_w, mean, invstd, scale, shift = ctx.saved_tensors
-        dout = _nhwc(dout.to(y.dtype))
-        if ctx.dgrad == "k9":
-            da = torch.ops.madnn.conv1x1_dgrad(dout, w, None)
-        else:
-            da = torch.empty_like(y)
-            torch.mm(_rows(dout), w.reshape(w.size(0), -1), out=_rows(da))
-        dw = _k9_wgrad(dout, y, w, scale, shift)
-        need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        dy, dbw, dbb, _ = torch.ops.madnn.bn_bwd(da, y, None, False, bn_w, mean, invstd, scale, shift, True, need_bn)
-        return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
-
-
 class _BNReluConv1x1EpiFn(torch.autograd.Function):
     """``conv1x1(relu(bn(y)), w)`` in training with bn's backward reduction taken in the K9 data
     grad's epilogue (the conv3 shapes whose data grad runs on K9): forward = K5 apply + K9 with the
@@ -935,24 +879,13 @@ class _BNReluConv1x1EpiFn(torch.autograd.Function):
         return dy, dw, dbw if need_bn else None, dbb if need_bn else None, None, None, None
 
 
-def bn_relu_conv1x1_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
-    """Whether :func:`bn_relu_conv1x1` runs fused: training-mode BN with running statistics and an
-    fp32 affine, bf16 NHWC input, K9-shaped weight."""
-    return (_BN_PROLOGUE and isinstance(y, torch.Tensor) and bn.training and bn.track_running_stats and bn.affine and bn.momentum is not None
-            and bn.weight.dtype == torch.float32 and conv1x1_supported(y, w) and bn_supported(y, bn.weight))
-
-
 def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[torch.Tensor] = None,
                     stats: bool = False):
-    """``conv1x1(relu(bn(y)), w)`` (ResNet's bn2 -> conv3): with ``MADNN_BN_PROLOGUE=1`` the
-    BatchNorm's apply pass is fused into the convolution's operand load; otherwise, when the data
-    grad runs on K9, bn's backward reduction is taken in that kernel's epilogue.  ``stats_in``:
-    ``y``'s partial statistics from its producer; ``stats``: also return the output's partial
-    statistics (None if not computed)."""
-    if bn_relu_conv1x1_supported(y, bn, w):
-        _need_native("bn_relu_conv1x1")
-        out, part = _BNReluConv1x1Fn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
-        return (out, part if part.numel() else None) if stats else out
+    """``conv1x1(relu(bn(y)), w)`` (ResNet's bn2 -> conv3): when the data grad runs on K9, bn's
+    backward reduction is taken in that kernel's epilogue.  ``stats_in``: ``y``'s partial
+    statistics from its producer; ``stats``: also return the output's partial statistics (None if
+    not computed).  (A BatchNorm-apply prologue inside K9's operand load lost its A/B --
+    profiles/r2_ab_bn_prologue.json -- and was removed in round 6.)"""
     if bn_relu_conv1x1_epi_supported(y, bn, w):
         _need_native("bn_relu_conv1x1")
         out, part = _BNReluConv1x1EpiFn.apply(y, w, bn.weight, bn.bias, bn, stats_in, stats)
@@ -963,13 +896,6 @@ def bn_relu_conv1x1(y: torch.Tensor, bn, w: torch.Tensor, *, stats_in: Optional[
     out = torch.nn.functional.conv2d(a, w.view(w.size(0), -1, 1, 1)) if a.dim() == 4 else torch.mm(
         a, w.reshape(w.size(0), -1).t())
     return (out, None) if stats else out
-
-
-# Off by default: same-process A/B at batch 1536 (profiles/r2_ab_bn_prologue.json): 121.8 -> 122.2
-# ms/step.  The fused forward costs +0.8 ms/step over the plain K9 forward (its prologue VALU work sits
-# on the LDS-store path of a one-k-step-per-tile, write-bound GEMM) and K9's weight grad is 1.1 ms/step
-# slower than MIOpen's on the conv3 shapes; together they eat the 1.5 ms/step bn2 apply pass saved.
-_BN_PROLOGUE = os.environ.get("MADNN_BN_PROLOGUE", "0") != "0"
 
 
 def bn_relu_conv1x1_epi_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
@@ -1032,18 +958,14 @@ _POOL_BN = os.environ.get("MADNN_POOL_BN", "1") != "0"
 
 # ---------------------------------------------------------------------- K13
 _K13 = os.environ.get("MADNN_CONV3X3", "1") != "0"
-_K13_DGRAD = os.environ.get("MADNN_CONV3X3_DGRAD", "k13")  # "k13" | "miopen" (A/B runs)
 # weight grad: "auto" = K13 or MIOpen per shape, timed once (_conv3x3_wgrad); "k13" | "miopen" force one
 _K13_WGRAD = os.environ.get("MADNN_CONV3X3_WGRAD", "auto")
-
-
-_K13_CH = 64 if os.environ.get("MADNN_K13_CH", "32") == "64" else 32  # input channels per LDS stage (A/B knob)
 
 
 def _k13_halo_ok(W: int) -> bool:
     # conv3.hip conv3x3_lds: halo pixels (rounded to whole 1-KiB DMA pieces) x 2*CH bytes + zero row +
     # two weight slots, at least the 32 KiB epilogue tile, must leave two workgroups per CU
-    rb = 2 * _K13_CH
+    rb = 2 * 32   # 32 input channels per LDS stage (conv3.hip k13_ch)
     rpi = 1024 // rb
     cap = ((255 // W) * W + 4 * W + rpi - 1) // rpi * rpi
     return max(cap * rb + rb + 2 * 64 * rb, 32 * 1024) <= 80 * 1024
@@ -1105,12 +1027,8 @@ class _Conv3x3Fn(torch.autograd.Function):
         dy = _nhwc(dy.to(x.dtype))
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if _K13_DGRAD == "k13":
-                wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-                dx = torch.ops.madnn.conv3x3_fwd(dy, wt, False)[0]
-            else:
-                dx = torch.ops.aten.convolution_backward(dy, x, w, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
-                                                         (True, False, False))[0]
+            wt = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            dx = torch.ops.madnn.conv3x3_fwd(dy, wt, False)[0]
         if ctx.needs_input_grad[1]:
             dw = _conv3x3_wgrad(dy, x, w)
         return dx, dw, None
@@ -1147,7 +1065,7 @@ class _BNReluConv3x3Fn(torch.autograd.Function):
 def bn_relu_conv3x3_supported(y: torch.Tensor, bn, w: torch.Tensor) -> bool:
     """Whether :func:`bn_relu_conv3x3` runs fused: training-mode BN with running statistics and an
     fp32 affine in front of a K13-shaped convolution whose data grad runs on K13."""
-    return (_BN_DGRAD_EPI and isinstance(y, torch.Tensor) and _K13_DGRAD == "k13" and bn.training
+    return (_BN_DGRAD_EPI and isinstance(y, torch.Tensor) and bn.training
             and bn.track_running_stats and bn.affine and bn.momentum is not None
             and bn.weight.dtype == torch.float32 and conv3x3_supported(y, w) and y.size(1) == w.size(1)
             and bn_supported(y, bn.weight))
@@ -1299,7 +1217,7 @@ __all__ = [
     "bucket_pack", "bucket_unpack", "flat_scale_cast", "sgd_step", "adam_step", "grad_norm", "layer_norm",
     "rms_norm", "batch_norm_act", "bn_supported", "cross_entropy", "attention", "attention_qkvpacked", "attention_supported",
     "max_pool2d", "max_pool_supported", "conv1x1", "conv1x1_route", "batch_norm_add_bn_relu",
-    "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_conv1x1_supported", "bn_relu_maxpool",
+    "batch_norm_dual_supported", "bn_relu_conv1x1", "bn_relu_maxpool",
     "bn_relu_maxpool_supported", "bn_relu_conv3x3", "bn_relu_conv3x3_supported",
     "bn_relu_conv1x1_epi_supported", "conv1x1_supported", "stem_conv", "stem_supported", "native_available", "load_kernels", "kernels_path", "hidden_supported", "reference",
 ]
@@ -1518,9 +1436,9 @@ def tuned_wgrad(key, lib, k12, k9=None, k12w=None):
     return cands[choice]()
 
 
-def _k9_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, scale=None, shift=None) -> torch.Tensor:
+def _k9_wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """K9's weight gradient in ``w``'s dtype (the split reduction writes it: no cast pass)."""
-    return torch.ops.madnn.conv1x1_wgrad(dy, x, scale, shift, w.dtype == torch.bfloat16).to(w.dtype).view(w.shape)
+    return torch.ops.madnn.conv1x1_wgrad(dy, x, w.dtype == torch.bfloat16).to(w.dtype).view(w.shape)
 
 
 def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -1765,6 +1683,7 @@ class _LinearFn(torch.autograd.Function):
         else:
             (x, weight), pre = ctx.saved_tensors, None
         db = None
+        g_out = g   # the residual's gradient: the upstream gradient itself, not the GELU-scaled one
         if ctx.gelu:
             db, g = bias_grad(g, pre, ctx.bias_dtype or g.dtype)
             if ctx.bias_dtype is None:
@@ -1790,7 +1709,7 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = (g2.t() @ x2).to(weight.dtype)
         ctx.param = None
-        return dx, dw, db, None, (g if ctx.has_res else None)
+        return dx, dw, db, None, (g_out if ctx.has_res else None)
 
 
 def _linear_residual_fwd(a: torch.Tensor, weight, bias, residual):

@@ -79,15 +79,12 @@ hipError_t madnn_bn_bwd_dual(const void*, const void*, const void*, const unsign
                              float*, float*, float*, float*, float*, float*, hipStream_t);
 int madnn_conv1x1_supported(int64_t, int64_t);
 int madnn_conv1x1_stat_rows(int64_t, int64_t, int64_t);
-hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, const float*,
-                             const float*, hipStream_t);
+hipError_t madnn_conv1x1_fwd(const void*, const void*, void*, float*, int64_t, int64_t, int64_t, hipStream_t);
 hipError_t madnn_conv1x1_dgrad(const void*, const void*, void*, const void*, int64_t, int64_t, int64_t, const void*,
-                               const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr,
-                               const unsigned char* = nullptr, int = 0, int = 0);
+                               const float*, const float*, float*, hipStream_t, const unsigned char* = nullptr);
 int madnn_conv1x1_dgrad_rows(int64_t, int64_t, int64_t);
 int64_t madnn_conv1x1_wgrad_ws(int64_t, int64_t, int64_t);
-hipError_t madnn_conv1x1_wgrad(const void*, const void*, void*, int, float*, int64_t, int64_t, int64_t, const float*, const float*,
-                               hipStream_t);
+hipError_t madnn_conv1x1_wgrad(const void*, const void*, void*, int, float*, int64_t, int64_t, int64_t, hipStream_t);
 hipError_t madnn_bn_coef(const void*, int64_t, int, float, float, const float*, const float*, float*, float*, int64_t*,
                          float*, float*, float*, float*, float*, const float*, int, hipStream_t);
 int madnn_stem_supported(int, int);
@@ -107,7 +104,7 @@ hipError_t madnn_conv3x3_fwd_bnb(const void*, const void*, void*, float*, const 
                                  int, int, int, int, hipStream_t);
 hipError_t madnn_bn_bwd_ext(const void*, const void*, void*, int64_t, int, int, const float*, const float*,
                             const float*, const float*, const float*, float*, float*, float*, const float*, int, float*,
-                            hipStream_t, const unsigned char* = nullptr, void* = nullptr);
+                            hipStream_t);
 int madnn_bn_prereduce_floats(int);
 hipError_t madnn_conv3x3_wgrad(const void*, const void*, float*, void*, int, int, int, int, int, int, hipStream_t);
 hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const void*, void*, void*, int, int64_t,
@@ -605,54 +602,31 @@ void conv_check_w(const at::Tensor& w, int64_t cout, int64_t cin) {
 }
 
 // y = conv(x, w); with stats: partial [rows, 2, Cout] per-channel (sum, sum of squares) of y
-// optional BatchNorm prologue: x is convolved as relu(x * scale + shift) (fp32 [cin] each)
-const float* pro_ptr(const c10::optional<at::Tensor>& t, int64_t C, const char* name) {
-  if (!t.has_value() || !t->defined()) return nullptr;
-  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, "conv1x1: ", name,
-              " must be fp32 [Cin]");
-  return t->data_ptr<float>();
-}
-
-std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, bool stats,
-                                               const c10::optional<at::Tensor>& scale,
-                                               const c10::optional<at::Tensor>& shift) {
+std::tuple<at::Tensor, at::Tensor> conv1x1_fwd(const at::Tensor& x, const at::Tensor& w, bool stats) {
   const int64_t cin = x.size(1), cout = w.size(0);
   const int64_t M = conv_rows(x, cin, "x");
   conv_check_w(w, cout, cin);
-  const float* sc = pro_ptr(scale, cin, "scale");
-  const float* sh = pro_ptr(shift, cin, "shift");
-  TORCH_CHECK((sc == nullptr) == (sh == nullptr), "conv1x1: scale and shift go together");
   at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   at::Tensor y = conv_out_like(x, cout);
   const int64_t rows = stats ? madnn_conv1x1_stat_rows(M, cin, cout) : 0;
   at::Tensor part = at::empty({rows, 2, cout}, x.options().dtype(at::kFloat));
   check(madnn_conv1x1_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, M, cin,
-                          cout, sc, sh, cur_stream(x)),
+                          cout, cur_stream(x)),
         "conv1x1_fwd");
   return {y, part};
 }
 
 // dx = dy (*) w^T, plus `res` (a gradient of x's layout accumulated from another path) if given;
 // resmask: a ReLU bit mask over res's elements (8 per byte) -- res counts only where it is set
-// sub (with res, no resmask): res is the gradient of x[:, :, ::2, ::2] (compact NHWC), added at dx's even
-// pixels
 at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::optional<at::Tensor>& res,
-                         const c10::optional<at::Tensor>& resmask, bool sub) {
+                         const c10::optional<at::Tensor>& resmask) {
   const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
   const int64_t M = conv_rows(dy, cout, "dy");
   conv_check_w(w, cout, cin);
   at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   at::Tensor dx = conv_out_like(dy, cin);
   const bool has_res = res.has_value() && res->defined();
-  int sub_h = 0, sub_w = 0;
-  if (sub) {
-    TORCH_CHECK(has_res && dy.dim() == 4 && res->dim() == 4 && res->size(0) == dy.size(0) && res->size(1) == cin &&
-                    res->size(2) == (dy.size(2) + 1) / 2 && res->size(3) == (dy.size(3) + 1) / 2 &&
-                    conv_rows(*res, cin, "res") == res->numel() / cin,
-                "conv1x1_dgrad: sub residual must be the NHWC gradient of x[:, :, ::2, ::2]");
-    sub_h = (int)dy.size(2);
-    sub_w = (int)dy.size(3);
-  } else if (has_res) {
+  if (has_res) {
     TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad: residual layout");
   }
   const bool has_mask = resmask.has_value() && resmask->defined();
@@ -660,10 +634,9 @@ at::Tensor conv1x1_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::o
     TORCH_CHECK(has_res && resmask->scalar_type() == at::kByte && resmask->is_contiguous() &&
                     resmask->numel() == M * cin / 8, "conv1x1_dgrad: resmask must be a uint8 bit mask over res");
   }
-  TORCH_CHECK(!(sub && has_mask), "conv1x1_dgrad: a sub residual takes no mask");
   check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
                             cout, nullptr, nullptr, nullptr, nullptr, cur_stream(dy),
-                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr, nullptr, sub_h, sub_w),
+                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr),
         "conv1x1_dgrad");
   return dx;
 }
@@ -688,45 +661,9 @@ std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnb(const at::Tensor& dy, const
   return {dx, part};
 }
 
-// conv1x1_dgrad whose dx is the incoming gradient of relu(bn(bny) + r) with that ReLU's bit mask
-// bnmask: also returns bn's backward sums (sum g, sum g*bny), g = dx * mask, from the epilogue
-// -> (dx, partial [rows, 2, Cin]); res / resmask as in conv1x1_dgrad
-std::tuple<at::Tensor, at::Tensor> conv1x1_dgrad_bnres(const at::Tensor& dy, const at::Tensor& w,
-                                                       const c10::optional<at::Tensor>& res,
-                                                       const c10::optional<at::Tensor>& resmask, const at::Tensor& bny,
-                                                       const at::Tensor& bnmask) {
-  const int64_t cout = dy.size(1), cin = w.numel() / std::max<int64_t>(cout, 1);
-  const int64_t M = conv_rows(dy, cout, "dy");
-  conv_check_w(w, cout, cin);
-  TORCH_CHECK(conv_rows(bny, cin, "bny") == M && bny.dim() == dy.dim(), "conv1x1_dgrad_bnres: bny layout");
-  TORCH_CHECK(bnmask.scalar_type() == at::kByte && bnmask.is_contiguous() && bnmask.numel() == M * cin / 8,
-              "conv1x1_dgrad_bnres: bnmask must be a uint8 bit mask over bny");
-  const bool has_res = res.has_value() && res->defined();
-  if (has_res) {
-    TORCH_CHECK(conv_rows(*res, cin, "res") == M && res->dim() == dy.dim(), "conv1x1_dgrad_bnres: residual layout");
-  }
-  const bool has_mask = resmask.has_value() && resmask->defined();
-  if (has_mask) {
-    TORCH_CHECK(has_res && resmask->scalar_type() == at::kByte && resmask->is_contiguous() &&
-                    resmask->numel() == M * cin / 8, "conv1x1_dgrad_bnres: resmask must be a uint8 bit mask over res");
-  }
-  at::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
-  at::Tensor dx = conv_out_like(dy, cin);
-  at::Tensor part = at::empty({madnn_conv1x1_dgrad_rows(M, cin, cout), 2, cin}, dy.options().dtype(at::kFloat));
-  check(madnn_conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), has_res ? res->data_ptr() : nullptr, M, cin,
-                            cout, bny.data_ptr(), nullptr, nullptr, part.data_ptr<float>(), cur_stream(dy),
-                            has_mask ? resmask->data_ptr<uint8_t>() : nullptr, bnmask.data_ptr<uint8_t>()),
-        "conv1x1_dgrad_bnres");
-  return {dx, part};
-}
-
 // [Cout, Cin] weight gradient, fp32 (or bf16 with out_bf16: the split reduction casts)
-at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& scale,
-                         const c10::optional<at::Tensor>& shift, bool out_bf16) {
+at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, bool out_bf16) {
   const int64_t cout = dy.size(1), cin = x.size(1);
-  const float* sc = pro_ptr(scale, cin, "scale");
-  const float* sh = pro_ptr(shift, cin, "shift");
-  TORCH_CHECK((sc == nullptr) == (sh == nullptr), "conv1x1: scale and shift go together");
   const int64_t M = conv_rows(x, cin, "x");
   TORCH_CHECK(conv_rows(dy, cout, "dy") == M && dy.dim() == x.dim(), "conv1x1_wgrad: dy / x pixel mismatch");
   TORCH_CHECK(madnn_conv1x1_supported(cin, cout), "conv1x1: channels must be multiples of 64");
@@ -734,7 +671,7 @@ at::Tensor conv1x1_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::o
   at::Tensor dw = at::empty({cout, cin}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
   at::Tensor ws = at::empty({madnn_conv1x1_wgrad_ws(M, cin, cout)}, x.options().dtype(at::kFloat));
   check(madnn_conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), out_bf16 ? 1 : 0, ws.data_ptr<float>(), M, cin,
-                            cout, sc, sh, cur_stream(x)),
+                            cout, cur_stream(x)),
         "conv1x1_wgrad");
   return dw;
 }
@@ -1019,36 +956,6 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_bwd_ext(const at::Tensor& dy, 
                          partial.data_ptr<float>(), (int)partial.size(0), ws.data_ptr<float>(), cur_stream(x)),
         "bn_bwd_ext");
   return {dx, dw, db};
-}
-
-// bn_bwd_ext for relu(bn(x) + r) with the ReLU bit mask (ResNet identity blocks' bn3, reduction from
-// conv1x1_dgrad_bnres): -> (dx, dw, db, dres); dres = dy * mask is written only with write_dres
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd_ext_res(
-    const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& w, const at::Tensor& save_mean,
-    const at::Tensor& save_invstd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& partial,
-    const at::Tensor& mask, bool write_dres) {
-  check_dev(x, "x");
-  const int64_t C = x.size(1);
-  const int64_t M = bn_rows(x, C);
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && dy.strides() == x.strides(),
-              "bn_bwd_ext_res: bf16 dy / x of one layout");
-  TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.is_contiguous() && partial.dim() == 3 &&
-                  partial.size(1) == 2 && partial.size(2) == C,
-              "bn_bwd_ext_res: partial must be fp32 [rows, 2, C]");
-  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.is_contiguous() && mask.numel() * 8 == M * C,
-              "bn_bwd_ext_res: uint8 bit mask over x");
-  at::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  auto fo = x.options().dtype(at::kFloat);
-  at::Tensor dx = at::empty_like(x), dw = at::empty({C}, fo), db = at::empty({C}, fo), coef = at::empty({3 * C}, fo);
-  at::Tensor dres = write_dres ? at::empty_like(x) : at::empty({0}, x.options());
-  at::Tensor ws = at::empty({(int64_t)madnn_bn_prereduce_floats((int)C)}, fo);
-  check(madnn_bn_bwd_ext(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), M, (int)C, 1, optf(w), save_mean.data_ptr<float>(),
-                         save_invstd.data_ptr<float>(), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                         dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), partial.data_ptr<float>(),
-                         (int)partial.size(0), ws.data_ptr<float>(), cur_stream(x), mask.data_ptr<uint8_t>(),
-                         write_dres ? dres.data_ptr() : nullptr),
-        "bn_bwd_ext_res");
-  return {dx, dw, db, dres};
 }
 
 // dW [Co, Ci, 3, 3] (channels_last) of y = conv3x3(x, w): dy [N, Co, H, W], x [N, Ci, H, W], both NHWC bf16
@@ -1567,21 +1474,15 @@ TORCH_LIBRARY(madnn, m) {
   m.def(
       "attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
       "Tensor(c!) dv, bool causal, float scale, Tensor(d!)? colsum=None) -> ()");
-  m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats, Tensor? scale=None, Tensor? shift=None) -> (Tensor, Tensor)");
-  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None, bool sub=False) -> Tensor");
+  m.def("conv1x1_fwd(Tensor x, Tensor w, bool stats) -> (Tensor, Tensor)");
+  m.def("conv1x1_dgrad(Tensor dy, Tensor w, Tensor? res=None, Tensor? resmask=None) -> Tensor");
   m.def("conv1x1_dgrad_bnb(Tensor dy, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
-  m.def(
-      "conv1x1_dgrad_bnres(Tensor dy, Tensor w, Tensor? res, Tensor? resmask, Tensor bny, Tensor bnmask) -> "
-      "(Tensor, Tensor)");
-  m.def(
-      "bn_bwd_ext_res(Tensor dy, Tensor x, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, "
-      "Tensor shift, Tensor partial, Tensor mask, bool write_dres) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "conv3x3_fwd_bnb(Tensor x, Tensor w, Tensor bny, Tensor scale, Tensor shift) -> (Tensor, Tensor)");
   m.def(
       "bn_bwd_ext(Tensor dy, Tensor x, Tensor? w, Tensor save_mean, Tensor save_invstd, Tensor scale, Tensor shift, "
       "Tensor partial, bool relu) -> (Tensor, Tensor, Tensor)");
-  m.def("conv1x1_wgrad(Tensor dy, Tensor x, Tensor? scale=None, Tensor? shift=None, bool out_bf16=False) -> Tensor");
+  m.def("conv1x1_wgrad(Tensor dy, Tensor x, bool out_bf16=False) -> Tensor");
   m.def(
       "bn_coef(Tensor x, Tensor? w, Tensor? b, Tensor(a!)? run_mean, Tensor(b!)? run_var, Tensor(c!)? nbt, "
       "float momentum, float eps, Tensor? partial=None) -> Tensor[]");
@@ -1642,8 +1543,6 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("bn_coef", bn_coef);
   m.impl("conv3x3_fwd_bnb", conv3x3_fwd_bnb);
   m.impl("conv1x1_dgrad_bnb", conv1x1_dgrad_bnb);
-  m.impl("conv1x1_dgrad_bnres", conv1x1_dgrad_bnres);
-  m.impl("bn_bwd_ext_res", bn_bwd_ext_res);
   m.impl("bn_bwd_ext", bn_bwd_ext);
   m.impl("bn_bwd_dual", bn_bwd_dual);
   m.impl("xent_fwd", xent_fwd);

@@ -784,13 +784,11 @@ hipError_t madnn_bn_bwd_finalize(const float* partial, int G, int C, int pstride
 
 // BatchNorm(+ReLU) backward whose reduction came from the producer of dy (K13's / K9's data-grad
 // epilogue: partial [G][2][C] = (sum g, sum g*x)): finalize + apply only.  coef: 3 * C floats.
-// mask (relu only): the ReLU followed a residual add -- its bit mask gates dy, and dres (if not null)
-// receives the masked dy for the residual path.
 // scratch: madnn_bn_prereduce_floats(C) floats
 hipError_t madnn_bn_bwd_ext(const void* dy, const void* x, void* dx, int64_t M, int C, int relu, const float* w,
                             const float* save_mean, const float* save_invstd, const float* scale, const float* shift,
                             float* dw, float* db, float* coef, const float* partial, int G, float* scratch,
-                            hipStream_t stream, const unsigned char* mask, void* dres) {
+                            hipStream_t stream) {
   using namespace madnn;
   if (!madnn_bn_supported(C) || partial == nullptr || G <= 0) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
@@ -802,10 +800,7 @@ hipError_t madnn_bn_bwd_ext(const void* dy, const void* x, void* dx, int64_t M, 
   MADNN_HIP_CHECK(hipGetLastError());
   const int64_t total = M * C;
   const int grid = stream_grid(total, 256 * 8, bn_tune().wg_per_cu * kNumCU);
-  if (relu && mask != nullptr) {  // relu(bn(x) + r): the ReLU is the stored bit mask; dres = dy * mask if asked
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, true, true>), dim3(grid), dim3(256), 0, stream, dy, x, mask,
-                       scale, shift, coef, coef + C, coef + 2 * C, dx, dres, total, C, bn_walk_flags());
-  } else if (relu) {
+  if (relu) {
     hipLaunchKernelGGL((bn_bwd_apply_kernel<kBF16, true, false>), dim3(grid), dim3(256), 0, stream, dy, x, nullptr,
                        scale, shift, coef, coef + C, coef + 2 * C, dx, nullptr, total, C, bn_walk_flags());
   } else {

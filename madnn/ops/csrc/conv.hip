@@ -36,12 +36,9 @@
 // all its tiles, and writes one [2][Cout] partial row.  That slab is the input format of
 // bn.hip's finalize kernel, so the BatchNorm forward skips its statistics pass over Y.
 //
-// Fused BatchNorm apply + ReLU prologue (forward and weight grad, operand X): when X is the
-// raw output of the previous convolution, x = relu(y * scale[c] + shift[c]) is computed on the
-// register-staged chunk (8 channels) between its global load and its LDS store, so the
-// normalised activation is never written to or read from HBM (ResNet's bn2 -> conv3).  The
-// channel of a thread's chunk is the same for all of its chunks of a k step (row memory: k0 +
-// 8 (tid & 7); column memory: x0 + 8 (tid % (R/8))), so scale/shift are loaded once per step.
+// (A BatchNorm apply + ReLU prologue on the X operand, a BN-reduction epilogue over a residual
+// ReLU's bit mask and a stride-2 residual epilogue were measured, lost their A/Bs and were removed
+// in round 6: docs/PERF.md.)
 #include "mfma.h"
 
 namespace madnn {
@@ -74,61 +71,25 @@ struct GemmArgs {
   const unsigned char* resmask;  // with res: res element e counts only where bit e of resmask is set
                                  // (a ReLU bit mask over the same [J][I] elements, 8 per byte), or null
   float* stats;
-  const float* bsc;  // B-operand BatchNorm prologue: relu(b * bsc[c] + bsh[c]) (PRO kernels)
-  const float* bsh;
   const uint16_t* bny;  // BNB epilogue (data grad): BN input y [J][I] whose backward sums are taken,
   const float* bnsc;    //   with its forward scale / shift (ReLU mask = y * sc + sh > 0)
   const float* bnsh;
-  const unsigned char* bnmask;  // BNB with a stored ReLU bit mask over [J][I] (8 per byte) instead of
-                                // y * sc + sh > 0: the BN's ReLU follows a residual add (bnsc unused)
   int64_t lda, ldb, ldo;
   int64_t I, J, K;                       // D is I x J, reduction length K
   int i_tiles, j_tiles, j_groups, k_chunk;
   int xcd;  // 1: remap workgroup ids so consecutive logical ids share an XCD (and its L2)
-  int sub_h, sub_w;  // > 0: res is the compact stride-2 subsample [N][ceil(H/2)][ceil(W/2)][I] of the
-                     // output's [N][H][W] pixel grid, added at the even (h, w) rows only
 };
 
 // One operand's 64-deep slice, register-staged: R rows of "row" memory ([x][ld], k
 // contiguous) or 64 k-rows of "column" memory ([k][ld], R contiguous x).  Rows past the
 // end load a valid row and are zeroed by a mask (no per-load branch).
-// relu(v * sc + sh) on 8 packed bf16 (fp32 math, one rounding: bn_apply_kernel's arithmetic)
-__device__ __forceinline__ u32x4 bn_relu8(u32x4 v, const float4 s0, const float4 s1, const float4 h0,
-                                          const float4 h1) {
-  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-  u32x4 o;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float lo = bf16_to_f32((unsigned short)(v[e] & 0xffffu)) * sc[2 * e] + sh[2 * e];
-    float hi = bf16_to_f32((unsigned short)(v[e] >> 16)) * sc[2 * e + 1] + sh[2 * e + 1];
-    lo = lo > 0.f ? lo : 0.f;
-    hi = hi > 0.f ? hi : 0.f;
-    o[e] = (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
-  }
-  return o;
-}
-
 template <bool COL, int R>
 struct Stage {
   static constexpr int PER = R / 32;  // 16-B chunks per thread
   u32x4 r[PER];
-  float4 ps0, ps1, ph0, ph1;  // PRO: this thread's 8 channels of scale / shift
 
-  // PRO: also fetch scale/shift of the chunk's channels (ch = the chunk's first channel = col);
-  // the transform itself waits until store(), so the global loads stay in flight across the
-  // MFMAs of the current step like the plain path's
-  template <bool PRO = false>
   __device__ __forceinline__ void load(const uint16_t* __restrict__ base, int64_t ld, int64_t x0, int64_t xlim,
-                                       int64_t k0, int64_t klim, int tid, const float* __restrict__ sc = nullptr,
-                                       const float* __restrict__ sh = nullptr) {
-    if constexpr (PRO) {  // chunk channel is thread-invariant across i (kThreads is a multiple of R / 8 and 8)
-      const int64_t ch = COL ? x0 + (tid % (R / 8)) * 8 : k0 + (tid & 7) * 8;
-      ps0 = *reinterpret_cast<const float4*>(sc + ch);
-      ps1 = *reinterpret_cast<const float4*>(sc + ch + 4);
-      ph0 = *reinterpret_cast<const float4*>(sh + ch);
-      ph1 = *reinterpret_cast<const float4*>(sh + ch + 4);
-    }
+                                       int64_t k0, int64_t klim, int tid) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + kThreads * i;
@@ -149,9 +110,6 @@ struct Stage {
     }
   }
 
-  // PRO: masked-off rows become relu(shift), which is harmless: forward B rows past J only feed
-  // output columns that are never stored, and weight-grad k rows past K meet a zeroed A row
-  template <bool PRO = false>
   __device__ __forceinline__ void store(uint16_t* tile, int tid) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -162,9 +120,7 @@ struct Stage {
       } else {
         boff = swz<64>(c >> 3, c & 7);
       }
-      u32x4 v = r[i];
-      if constexpr (PRO) v = bn_relu8(v, ps0, ps1, ph0, ph1);
-      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(tile) + boff) = v;
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(tile) + boff) = r[i];
     }
   }
 
@@ -181,7 +137,7 @@ struct Stage {
 // BNB (store mode): besides the output D, accumulate per output channel the BatchNorm backward sums
 // sum g and sum g*y, g = D * [y * sc + sh > 0], into the same [groups][2][I] partial rows STATS writes
 // (the data grad of conv3 whose input was relu(bn2(y)): bn2's backward skips its reduction pass).
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false, bool BNB = false>
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool BNB = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   static_assert(!(STATS && BNB), "one statistics epilogue per launch");
   constexpr int NI = (BI == 64 && BJ == 64) ? 1 : 2;  // 32-row i blocks per wave
@@ -236,7 +192,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   }
   if constexpr (BNB) {  // this thread's 8 output channels (chunk tid % CPR of the i tile) are fixed
     const int cc = tid % (BI / 8);
-    if (p.bnmask == nullptr)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bs[e] = p.bnsc[i0 + 8 * cc + e];
@@ -250,9 +205,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   };
 
   sta.load(p.a, p.lda, i0, p.I, (int64_t)kbeg * kBK, p.K, tid);
-  stb.template load<PRO>(p.b, p.ldb, (int64_t)jt * BJ, p.J, (int64_t)kbeg * kBK, p.K, tid, p.bsc, p.bsh);
+  stb.load(p.b, p.ldb, (int64_t)jt * BJ, p.J, (int64_t)kbeg * kBK, p.K, tid);
   sta.store(smem, tid);
-  stb.template store<PRO>(smem + AE, tid);
+  stb.store(smem + AE, tid);
   __syncthreads();
   int cur = 0, ks = kbeg;
   for (;;) {
@@ -264,7 +219,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
     const bool more = njt < p.j_tiles;
     if (more) {
       sta.load(p.a, p.lda, i0, p.I, (int64_t)nks * kBK, p.K, tid);
-      stb.template load<PRO>(p.b, p.ldb, (int64_t)njt * BJ, p.J, (int64_t)nks * kBK, p.K, tid, p.bsc, p.bsh);
+      stb.load(p.b, p.ldb, (int64_t)njt * BJ, p.J, (int64_t)nks * kBK, p.K, tid);
     }
     uint16_t* buf = smem + cur * SE;
 #pragma unroll
@@ -281,7 +236,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
     }
     if (more) {  // the other buffer was last read before the previous barrier
       sta.store(smem + (cur ^ 1) * SE, tid);
-      stb.template store<PRO>(smem + (cur ^ 1) * SE + AE, tid);
+      stb.store(smem + (cur ^ 1) * SE + AE, tid);
     }
     if (ks == kend - 1) {  // tile done: epilogue
       if constexpr (MODE == kStoreT) {
@@ -312,13 +267,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
           const int64_t j = (int64_t)jt * BJ + r;
           if (j < p.J) {
             u32x4 v = *reinterpret_cast<const u32x4*>(ot + out_off(r, c));
-            int64_t rj = j;  // residual row of output row j (-1: none)
-            if (p.sub_h > 0) {
-              const int64_t wq = j % p.sub_w, t = j / p.sub_w, hq = t % p.sub_h, nq = t / p.sub_h;
-              rj = ((hq | wq) & 1) ? -1 : (nq * ((p.sub_h + 1) / 2) + hq / 2) * ((p.sub_w + 1) / 2) + wq / 2;
-            }
-            if (p.res != nullptr && rj >= 0) {  // fused residual-gradient accumulation (fp32 add, one rounding)
-              u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + rj * p.ldo + i0 + 8 * c);
+            if (p.res != nullptr) {  // fused residual-gradient accumulation (fp32 add, one rounding)
+              u32x4 rv = *reinterpret_cast<const u32x4*>(p.res + j * p.ldo + i0 + 8 * c);
               if (p.resmask != nullptr) {
                 const unsigned bits = p.resmask[(j * p.ldo + i0 + 8 * c) >> 3];
 #pragma unroll
@@ -336,7 +286,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
             *reinterpret_cast<u32x4*>(out + j * p.ldo + i0 + 8 * c) = v;
             if constexpr (BNB) {
               const u32x4 yv = *reinterpret_cast<const u32x4*>(p.bny + j * p.ldo + i0 + 8 * c);
-              const unsigned mb = p.bnmask != nullptr ? p.bnmask[(j * p.ldo + i0 + 8 * c) >> 3] : 0u;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
 #pragma unroll
@@ -344,7 +293,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
                   const int k = 2 * e + hf;
                   const float g = bf16_to_f32((unsigned short)(hf ? v[e] >> 16 : v[e] & 0xffffu));
                   const float yy = bf16_to_f32((unsigned short)(hf ? yv[e] >> 16 : yv[e] & 0xffffu));
-                  const bool on = p.bnmask != nullptr ? ((mb >> k) & 1u) != 0u : yy * bs[k] + bh[k] > 0.f;
+                  const bool on = yy * bs[k] + bh[k] > 0.f;
                   const float gm = on ? g : 0.f;
                   ssum[k] += gm;
                   ssq[k] += gm * yy;
@@ -409,9 +358,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(const GemmArgs p) {
   }
 }
 
-template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool PRO = false, bool BNB = false>
+template <bool A_COL, bool B_COL, int BI, int BJ, int MODE, bool STATS, bool BNB = false>
 hipError_t launch(const GemmArgs& p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS, PRO, BNB>), dim3(grid), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL((gemm_kernel<A_COL, B_COL, BI, BJ, MODE, STATS, BNB>), dim3(grid), dim3(kThreads), 0, s, p);
   return hipGetLastError();
 }
 
@@ -487,7 +436,6 @@ int madnn_conv1x1_stat_rows(int64_t M, int64_t cin, int64_t cout) {
   return p.j_groups;
 }
 
-// bsc/bsh (optional, [cin] fp32): x is a raw BatchNorm input, convolved as relu(x * bsc + bsh)
 // partial rows the BNB data grad writes ([rows][2][cin] fp32)
 int madnn_conv1x1_dgrad_rows(int64_t M, int64_t cin, int64_t cout) {
   if (!madnn_conv1x1_supported(cin, cout) || M <= 0) return 0;
@@ -497,7 +445,7 @@ int madnn_conv1x1_dgrad_rows(int64_t M, int64_t cin, int64_t cout) {
 }
 
 hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats, int64_t M, int64_t cin,
-                             int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
+                             int64_t cout, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -508,8 +456,6 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
   p.out = y;
   p.ldo = cout;
   p.stats = stats;
-  p.bsc = bsc;
-  p.bsh = bsh;
   p.xcd = tune().xcd;
   p.I = cout;
   p.J = M;
@@ -517,15 +463,6 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
   const bool wide = cout % 128 == 0;
   plan_persistent(p, M, wide ? 128 : 64, cout, cin);
   const int grid = p.i_tiles * p.j_groups;
-  if ((bsc == nullptr) != (bsh == nullptr)) return hipErrorInvalidValue;
-  if (bsc != nullptr) {
-    if (wide) {
-      return stats ? launch<false, false, 128, 128, kStoreT, true, true>(p, grid, s)
-                   : launch<false, false, 128, 128, kStoreT, false, true>(p, grid, s);
-    }
-    return stats ? launch<false, false, 64, 128, kStoreT, true, true>(p, grid, s)
-                 : launch<false, false, 64, 128, kStoreT, false, true>(p, grid, s);
-  }
   if (wide) {
     return stats ? launch<false, false, 128, 128, kStoreT, true>(p, grid, s)
                  : launch<false, false, 128, 128, kStoreT, false>(p, grid, s);
@@ -537,14 +474,10 @@ hipError_t madnn_conv1x1_fwd(const void* x, const void* w, void* y, float* stats
 // dx = dY W (+ res: an accumulated gradient of the same layout, added in the epilogue)
 // bny/bnsc/bnsh/partial (optional, all or none): dx is d relu(bn(bny)); the epilogue also writes bn's
 // backward sums as partial [madnn_conv1x1_dgrad_rows][2][cin] (see BNB)
-// bny/bnmask/partial (with or without res): the same sums for relu(bn(bny) + r), whose ReLU is the
-// stored bit mask (a ResNet identity block's bn3, whose output x is: dx feeds that bn's backward)
-// sub_h / sub_w (> 0, no resmask): res is the compact x[:, :, ::2, ::2] gradient of a [M / (H W)][H][W]
-// pixel grid, added at the even pixels (a ResNet downsample path's input gradient)
+// resmask (with res): res counts only where its ReLU bit is set
 hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const void* res, int64_t M, int64_t cin,
                                int64_t cout, const void* bny, const float* bnsc, const float* bnsh, float* partial,
-                               hipStream_t s, const unsigned char* resmask, const unsigned char* bnmask, int sub_h,
-                               int sub_w) {
+                               hipStream_t s, const unsigned char* resmask) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipSuccess;
   GemmArgs p{};
@@ -555,12 +488,6 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   p.out = dx;
   p.res = static_cast<const uint16_t*>(res);
   p.resmask = res != nullptr ? resmask : nullptr;
-  if (sub_h > 0 || sub_w > 0) {
-    if (res == nullptr || resmask != nullptr || sub_h <= 0 || sub_w <= 0 || M % ((int64_t)sub_h * sub_w))
-      return hipErrorInvalidValue;
-    p.sub_h = sub_h;
-    p.sub_w = sub_w;
-  }
   p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cin;
@@ -570,15 +497,13 @@ hipError_t madnn_conv1x1_dgrad(const void* dy, const void* w, void* dx, const vo
   plan_persistent(p, M, wide ? 128 : 64, cin, cout);
   const int grid = p.i_tiles * p.j_groups;
   if (bny != nullptr) {
-    if (partial == nullptr) return hipErrorInvalidValue;
-    if (bnmask == nullptr && (bnsc == nullptr || bnsh == nullptr || res != nullptr)) return hipErrorInvalidValue;
-    p.bnmask = bnmask;
+    if (partial == nullptr || bnsc == nullptr || bnsh == nullptr || res != nullptr) return hipErrorInvalidValue;
     p.bny = static_cast<const uint16_t*>(bny);
     p.bnsc = bnsc;
     p.bnsh = bnsh;
     p.stats = partial;
-    return wide ? launch<true, false, 128, 128, kStoreT, false, false, true>(p, grid, s)
-                : launch<true, false, 64, 128, kStoreT, false, false, true>(p, grid, s);
+    return wide ? launch<true, false, 128, 128, kStoreT, false, true>(p, grid, s)
+                : launch<true, false, 64, 128, kStoreT, false, true>(p, grid, s);
   }
   return wide ? launch<true, false, 128, 128, kStoreT, false>(p, grid, s)
               : launch<true, false, 64, 128, kStoreT, false>(p, grid, s);
@@ -593,10 +518,9 @@ int64_t madnn_conv1x1_wgrad_ws(int64_t M, int64_t cin, int64_t cout) {
 }
 
 // dw: [cout][cin] fp32 or (dw_bf16) bf16; ws: madnn_conv1x1_wgrad_ws floats (the per-split partial
-// slabs, summed in split order into dw -- one pass that also casts).  bsc/bsh (optional): x is
-// convolved as relu(x * bsc + bsh), as in madnn_conv1x1_fwd
+// slabs, summed in split order into dw -- one pass that also casts)
 hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, void* dw, int dw_bf16, float* ws, int64_t M, int64_t cin,
-                               int64_t cout, const float* bsc, const float* bsh, hipStream_t s) {
+                               int64_t cout, hipStream_t s) {
   if (!madnn_conv1x1_supported(cin, cout)) return hipErrorInvalidValue;
   if (M <= 0) return hipMemsetAsync(dw, 0, (size_t)(cin * cout) * (dw_bf16 ? 2 : 4), s);
   GemmArgs p{};
@@ -604,8 +528,6 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, void* dw, int dw_b
   p.lda = cout;
   p.b = static_cast<const uint16_t*>(x);  // B[k = m][j = ci] = X[m][ci]: column memory
   p.ldb = cin;
-  p.bsc = bsc;
-  p.bsh = bsh;
   p.xcd = tune().xcd;
   p.ldo = cin;
   p.I = cout;
@@ -620,19 +542,11 @@ hipError_t madnn_conv1x1_wgrad(const void* dy, const void* x, void* dw, int dw_b
   p.j_tiles = (int)(cin / bj);
   const int grid = (int)(tiles * splits);
   p.j_groups = 0;
-  if ((bsc == nullptr) != (bsh == nullptr)) return hipErrorInvalidValue;
   hipError_t e;
-  if (bsc != nullptr) {
-    if (bi == 128 && bj == 128) e = launch<true, true, 128, 128, kSplit, false, true>(p, grid, s);
-    else if (bi == 128) e = launch<true, true, 128, 64, kSplit, false, true>(p, grid, s);
-    else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false, true>(p, grid, s);
-    else e = launch<true, true, 64, 64, kSplit, false, true>(p, grid, s);
-  } else {
-    if (bi == 128 && bj == 128) e = launch<true, true, 128, 128, kSplit, false>(p, grid, s);
-    else if (bi == 128) e = launch<true, true, 128, 64, kSplit, false>(p, grid, s);
-    else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false>(p, grid, s);
-    else e = launch<true, true, 64, 64, kSplit, false>(p, grid, s);
-  }
+  if (bi == 128 && bj == 128) e = launch<true, true, 128, 128, kSplit, false>(p, grid, s);
+  else if (bi == 128) e = launch<true, true, 128, 64, kSplit, false>(p, grid, s);
+  else if (bj == 128) e = launch<true, true, 64, 128, kSplit, false>(p, grid, s);
+  else e = launch<true, true, 64, 64, kSplit, false>(p, grid, s);
   if (e != hipSuccess) return e;
   const int64_t n = cin * cout;
   const int64_t blocks = (n / 4 + 255) / 256;

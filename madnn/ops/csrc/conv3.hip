@@ -482,11 +482,9 @@ using namespace madnn::conv3;
 
 extern "C" {
 
-// chunk width: 32 channels (LDS ~37 KiB at W = 56: four workgroups per CU) unless MADNN_K13_CH=64
-static int k13_ch(int Ci) {
-  static const int want = getenv("MADNN_K13_CH") ? atoi(getenv("MADNN_K13_CH")) : 32;
-  return (want == 64 && Ci % 64 == 0) ? 64 : 32;
-}
+// chunk width: 32 input channels per LDS stage (LDS ~37 KiB at W = 56: four workgroups per CU; the
+// 64-channel variant measured slower and was removed in round 6)
+static int k13_ch(int) { return 32; }
 
 int madnn_conv3x3_supported(int H, int W, int Ci, int Co) {
   if (H < 1 || W < 1 || Ci % 64 || Co % 64 || Ci < 64 || Co < 64 || Ci > 8192) return 0;
@@ -521,13 +519,8 @@ hipError_t madnn_conv3x3_fwd(const void* x, const void* w, void* y, float* stats
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const size_t lds = conv3x3_lds(W, CH);
   const dim3 g((unsigned)grid), b(kThreads);
-  if (CH == 32) {
-    if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true>), g, b, lds, s, p);
-    else hipLaunchKernelGGL((conv3x3_kernel<32, false>), g, b, lds, s, p);
-  } else {
-    if (stats) hipLaunchKernelGGL((conv3x3_kernel<64, true>), g, b, lds, s, p);
-    else hipLaunchKernelGGL((conv3x3_kernel<64, false>), g, b, lds, s, p);
-  }
+  if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true>), g, b, lds, s, p);
+  else hipLaunchKernelGGL((conv3x3_kernel<32, false>), g, b, lds, s, p);
   return hipGetLastError();
 }
 
@@ -564,13 +557,8 @@ hipError_t madnn_conv3x3_fwd_s2(const void* x, const void* w, void* y, float* st
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const size_t lds = conv3x3_lds(W, CH, 2);
   const dim3 g((unsigned)grid), b(kThreads);
-  if (CH == 32) {
-    if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true, false, 2>), g, b, lds, s, p);
-    else hipLaunchKernelGGL((conv3x3_kernel<32, false, false, 2>), g, b, lds, s, p);
-  } else {
-    if (stats) hipLaunchKernelGGL((conv3x3_kernel<64, true, false, 2>), g, b, lds, s, p);
-    else hipLaunchKernelGGL((conv3x3_kernel<64, false, false, 2>), g, b, lds, s, p);
-  }
+  if (stats) hipLaunchKernelGGL((conv3x3_kernel<32, true, false, 2>), g, b, lds, s, p);
+  else hipLaunchKernelGGL((conv3x3_kernel<32, false, false, 2>), g, b, lds, s, p);
   return hipGetLastError();
 }
 
@@ -604,8 +592,7 @@ hipError_t madnn_conv3x3_fwd_bnb(const void* x, const void* w, void* y, float* p
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const size_t lds = conv3x3_lds(W, CH);
   const dim3 g((unsigned)grid), b(kThreads);
-  if (CH == 32) hipLaunchKernelGGL((conv3x3_kernel<32, false, true>), g, b, lds, s, p);
-  else hipLaunchKernelGGL((conv3x3_kernel<64, false, true>), g, b, lds, s, p);
+  hipLaunchKernelGGL((conv3x3_kernel<32, false, true>), g, b, lds, s, p);
   return hipGetLastError();
 }
 

@@ -172,49 +172,8 @@ def test_identity_block_deferred_relu_mask_matches(cuda, monkeypatch):
     assert ((res[0][3] - res[1][3]).norm() / res[1][3].norm()).item() < 1e-2
 
 
-def test_identity_bn3_sums_from_next_conv1_dgrad(cuda, monkeypatch):
-    """Two chained stride-1 Bottlenecks: the first block's bn3 (relu(bn3(y) + x), bit-mask ReLU) takes
-    its backward sums from the second block's conv1 K9 data-grad epilogue (conv1x1_dgrad_bnres +
-    bn_bwd_ext_res) instead of its own reduction pass -- same forward bitwise, gradients to fp32
-    summation-order tolerance against the unfused path."""
-    import madnn.ops as O
-    from madnn.models.resnet import Bottleneck
-
-    torch.manual_seed(12)
-    blks = torch.nn.Sequential(Bottleneck(256, 64), Bottleneck(256, 64))
-    for m in blks.modules():
-        if isinstance(m, torch.nn.BatchNorm2d):
-            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
-            torch.nn.init.uniform_(m.bias, -0.2, 0.2)
-    blks = blks.to(cuda).to(memory_format=torch.channels_last)
-    for p in blks.parameters():
-        if p.dim() == 4:
-            p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
-    x0 = _rand((4, 256, 14, 14), cuda)
-    g = torch.randn(4, 256, 14, 14, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
-    calls = []
-    real = torch.ops.madnn.bn_bwd_ext_res
-    monkeypatch.setattr(torch.ops.madnn, "bn_bwd_ext_res", lambda *a: calls.append(1) or real(*a))
-    res = []
-    for fused in (True, False):
-        monkeypatch.setattr(O, "BN_SUM_IN_DGRAD", fused)
-        blks.zero_grad(set_to_none=True)
-        x = x0.clone().requires_grad_(True)
-        y = blks(x)
-        y.backward(g)
-        b0 = blks[0]
-        res.append((y.float(), x.grad.float(), b0.bn3.weight.grad.float(), b0.bn3.bias.grad.float(),
-                    b0.conv3.weight.grad.float()))
-        assert len(calls) == (1 if fused else 0)
-        calls.clear()
-    torch.testing.assert_close(res[0][0], res[1][0], atol=0, rtol=0)
-    for a, b in zip(res[0][1:], res[1][1:]):
-        assert ((a - b).norm() / b.norm()).item() < 1e-2
-
-
-@pytest.mark.parametrize("in_dgrad", [True, False])
 @pytest.mark.parametrize("inplanes,planes,hw", [(256, 128, 28), (512, 256, 14), (1024, 512, 8), (256, 64, 7)])
-def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw, in_dgrad):
+def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes, planes, hw):
     """A stride-2 downsample Bottleneck: the downsample 1x1 run as a stride-1 K9 conv on conv1's
     compact x[:, :, ::2, ::2] (gradient added into conv1's data grad at the even pixels) vs the
     stride-2 library convolution on the full input (same bf16 block: tight), and vs fp32 eager."""
@@ -240,10 +199,7 @@ def test_downsample_block_compact_subsample_matches(cuda, monkeypatch, inplanes,
             p.data = p.data.bfloat16().contiguous(memory_format=torch.channels_last)
     x0 = _rand((4, inplanes, hw, hw), cuda)
     g = torch.randn(4, planes * 4, (hw + 1) // 2, (hw + 1) // 2, device=cuda)
-    # in_dgrad: the compact gradient is added at the even pixels inside conv1's K9 data-grad epilogue
     # (odd hw: the last row / column is even, x[:, :, ::2, ::2] keeps it)
-    import madnn.ops as O
-    monkeypatch.setattr(O, "SUB_IN_DGRAD", in_dgrad)
     res = []
     for sub in (True, False):
         monkeypatch.setattr(R, "_DS_SUB", sub)
@@ -285,96 +241,6 @@ def test_conv1x1_fork_accumulates_residual_grad(cuda, cin, cout):
     _close(wt.grad.float(), wr.grad, 3e-2)
     if ops.conv1x1_route(cin, cout)[0] == "k9":
         assert st is not None and st.size(2) == cout
-
-
-@pytest.mark.parametrize("shape", [(2, 64, 256, 7, 7), (3, 128, 64, 5, 9), (1, 512, 2048, 3, 3),
-                                   (2, 192, 320, 11, 13)])
-@pytest.mark.parametrize("with_stats", [False, True])
-def test_bn_relu_conv1x1_prologue_matches_fp32(cuda, shape, with_stats, monkeypatch):
-    """K9 BatchNorm prologue: conv1x1(relu(bn(y))) with bn's apply inside the operand load vs
-    fp32 eager BN + ReLU + conv: output, output statistics, running stats and every gradient."""
-    from madnn.nn.norm import FusedBatchNorm2d
-
-    n, cin, cout, h, w = shape
-    torch.manual_seed(1)
-    y = (_rand((n, cin, h, w), cuda).float() * 1.3 + 0.2).bfloat16().contiguous(memory_format=torch.channels_last)
-    y.requires_grad_(True)
-    wt = _rand((cout, cin, 1, 1), cuda, cin ** -0.5).contiguous(memory_format=torch.channels_last)
-    wt.requires_grad_(True)
-    bn = FusedBatchNorm2d(cin).to(cuda)
-    with torch.no_grad():
-        bn.weight.uniform_(0.5, 1.5)
-        bn.bias.normal_(0, 0.2)
-    ref = torch.nn.BatchNorm2d(cin).to(cuda)
-    ref.load_state_dict(bn.state_dict())
-    st = None
-    if with_stats:
-        v = y.detach().float().permute(0, 2, 3, 1).reshape(1, -1, cin)
-        st = torch.stack([v.sum(1), (v * v).sum(1)], 1).contiguous()
-    monkeypatch.setattr(ops, "_BN_PROLOGUE", True)   # opt-in path (off by default: docs/PERF.md)
-    assert ops.bn_relu_conv1x1_supported(y, bn, wt)
-    out, part = ops.bn_relu_conv1x1(y, bn, wt, stats_in=st, stats=True)
-    dout = _rand(tuple(out.shape), cuda)
-    out.backward(dout)
-    yr = y.detach().float().requires_grad_(True)
-    wr = wt.detach().float().requires_grad_(True)
-    a = torch.relu(ref(yr))
-    outr = F.conv2d(a, wr)
-    outr.backward(dout.float())
-    _close(out.float(), outr, 3e-2)
-    of = out.double().permute(0, 2, 3, 1).reshape(-1, cout)
-    torch.testing.assert_close(part.double().sum(0)[0], of.sum(0), atol=1e-2 * of.abs().sum(0).max().item(),
-                               rtol=1e-3)
-    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-4)
-    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-3, rtol=1e-3)
-    assert int(bn.num_batches_tracked) == 1
-    _close(wt.grad.float(), wr.grad, 3e-2)
-    _close(y.grad.float(), yr.grad, 6e-2)
-    _close(bn.weight.grad, ref.weight.grad, 6e-2)
-    _close(bn.bias.grad, ref.bias.grad, 6e-2)
-
-
-def test_bottleneck_bn_prologue_matches_unfused(cuda, monkeypatch):
-    """A ResNet-50 bottleneck with bn2 fused into conv3's prologue vs the same block unfused."""
-    import copy
-
-    import madnn.ops as O
-    from madnn.models.resnet import Bottleneck
-
-    torch.manual_seed(2)
-    blk = Bottleneck(256, 64).to(cuda).bfloat16()
-    for m in blk.modules():
-        if isinstance(m, torch.nn.BatchNorm2d):
-            m.float()
-            torch.nn.init.uniform_(m.weight, 0.5, 1.5)
-    blk2 = copy.deepcopy(blk)
-    monkeypatch.setattr(O, "_BN_PROLOGUE", True)
-    x = _rand((4, 256, 14, 14), cuda)
-    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
-    y1 = blk(x1)
-    old = O._BN_PROLOGUE
-    O._BN_PROLOGUE = False
-    try:
-        y2 = blk2(x2)
-    finally:
-        O._BN_PROLOGUE = old
-    blk3 = copy.deepcopy(blk2).float()   # fp32 oracle: eager convolutions, composed BNs
-    x3 = x.float().requires_grad_(True)
-    y3 = blk3(x3)
-    dy = _rand(tuple(y1.shape), cuda)
-    y1.backward(dy)
-    y2.backward(dy)
-    y3.backward(dy.float())
-
-    def rel(a, b):
-        return ((a.float() - b).norm() / b.norm()).item()
-
-    # each bf16 path against fp32 (element-wise comparison of two bf16 paths trips on ReLU-mask flips)
-    assert rel(y1, y3) <= 1.5 * rel(y2, y3) + 1e-3
-    assert rel(x1.grad, x3.grad) <= 1.5 * rel(x2.grad, x3.grad) + 1e-3
-    assert rel(x1.grad, x3.grad) < 0.1   # bf16 end to end through a whole block: ~0.06
-    for (n, p1), p2, p3 in zip(blk.named_parameters(), blk2.parameters(), blk3.parameters()):
-        assert rel(p1.grad, p3.grad) <= 1.5 * rel(p2.grad, p3.grad) + 2e-3, n
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56), (3, 128, 128, 28, 28), (2, 256, 256, 14, 14),
@@ -437,7 +303,7 @@ def test_bn_relu_conv1x1_dgrad_epilogue_matches_fp32(cuda, shape):
         bn.bias.normal_(0, 0.2)
     ref = torch.nn.BatchNorm2d(cin).to(cuda)
     ref.load_state_dict(bn.state_dict())
-    assert not ops.bn_relu_conv1x1_supported(y, bn, wt) and ops.bn_relu_conv1x1_epi_supported(y, bn, wt)
+    assert ops.bn_relu_conv1x1_epi_supported(y, bn, wt)
     out, part = ops.bn_relu_conv1x1(y, bn, wt, stats=True)
     dout = _rand(tuple(out.shape), cuda)
     out.backward(dout)

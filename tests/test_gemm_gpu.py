@@ -106,20 +106,24 @@ WGRAD_SHAPES = [(256, 256, 64, 1), (4096, 1024, 1024, 0), (2048, 3072, 1024, 5),
                 (8192, 1032, 4096, 0), (64, 64, 64, 1)]
 
 
-@pytest.mark.parametrize("M,N,K,splits", WGRAD_SHAPES)
-def test_linear_wgrad_split_k(M, N, K, splits):
+@pytest.mark.parametrize("kernel", ["linear_wgrad", "linear_wgrad4"])   # K12 (8 waves), K12W (4 waves)
+@pytest.mark.parametrize("M,N,K,splits", WGRAD_SHAPES + [(64 * 37, 136, 1000, 7), (64 * 20, 520, 264, 40)])
+def test_linear_wgrad_split_k(M, N, K, splits, kernel):
+    """Both weight-gradient kernels against fp32, with ragged N / K tiles, odd K-tile counts (K12W
+    runs its K loop in pairs) and more splits than K tiles per split (empty splits write zeros)."""
     m = _ops()
+    wgrad = getattr(m, kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
     dy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    dw = m.linear_wgrad(dy, x, None, False, splits)
+    dw = wgrad(dy, x, None, False, splits)
     ref = dy.float().t() @ x.float()
     assert dw.shape == (N, K) and dw.dtype == torch.bfloat16
     assert _rel(dw, ref) < 6e-3, (M, N, K, splits)
     # accumulate into an existing gradient (a second backward before the optimizer step)
     base = torch.randn(N, K, device="cuda", generator=g).bfloat16()
     out = base.clone()
-    m.linear_wgrad(dy, x, out, True, splits)
+    wgrad(dy, x, out, True, splits)
     assert _rel(out, ref + base.float()) < 6e-3
 
 
