@@ -1606,29 +1606,42 @@ def dgrad_dgelu(g2: torch.Tensor, w2: torch.Tensor, pre2: torch.Tensor, bias_dty
     return lt() if choice == "lt" else k12p()
 
 
-DGRAD = os.environ.get("MADNN_DGRAD", "auto")  # plain Linear data gradient: auto | lt | k12p
+DGRAD = os.environ.get("MADNN_DGRAD", "auto")  # plain Linear data gradient: auto | lt | ltk | k12p
 
 
 def dgrad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """``g2 @ weight``: a Linear's data gradient, from whichever was faster for the shape (shipped
-    table, else timed once on first use like :func:`tuned_wgrad`): ``lt`` (hipBLASLt) or ``k12p``
-    (the persistent K12P GEMM, plain epilogue).  hipBLASLt's choice at 32k-token microbatches ran
-    the GPT-2 data gradients 35 % slower per FLOP than at 131k tokens
-    (``profiles/r6_gpt2m_mb32_steady_steps.md``).  ``MADNN_DGRAD=lt`` / ``k12p`` pin one."""
+    table, else timed once on first use like :func:`tuned_wgrad`):
+
+    * ``lt``: PyTorch's matmul (hipBLASLt through PyTorch's own plan);
+    * ``ltk``: madnn's hipBLASLt plan for the same product (``lt_linear(..., w_kn=True)``: the weight
+      taken as [K, N] without a transposed copy) -- the same library, but its plan picks a different
+      kernel on some shapes: the GPT-2 qkv data gradient runs 713 us there against 838 us through
+      PyTorch (``profiles/r6_lt_algo_sweep.jsonl``);
+    * ``k12p``: the persistent K12P GEMM, plain epilogue (hipBLASLt's choice at 32k-token microbatches
+      ran the GPT-2 data gradients 35 % slower per FLOP than at 131k tokens,
+      ``profiles/r6_gpt2m_mb32_steady_steps.md``).
+
+    ``MADNN_DGRAD=lt`` / ``ltk`` / ``k12p`` pin one."""
     def lt():
         return g2 @ weight
 
-    if DGRAD == "lt" or not (g2.is_contiguous() and _k12p_ok(g2, weight, weight.shape[1], g2.shape[0], g2.shape[1],
-                                                             False)):
+    if DGRAD == "lt" or not (g2.is_contiguous() and weight.is_contiguous() and _is_dev(g2)
+                             and g2.dtype == weight.dtype == torch.bfloat16):
         return lt()
 
-    def k12p():
-        return torch.ops.madnn.linear_dgrad_p(g2, weight, None, g2.dtype, 1)[0]
+    def ltk():
+        return _need_native("lt_linear").lt_linear(g2, weight, None, None, False, False, True)[0]
 
-    if DGRAD == "k12p":
-        return k12p()
+    cands = {"lt": lt, "ltk": ltk}
+    if _k12p_ok(g2, weight, weight.shape[1], g2.shape[0], g2.shape[1], False):
+        def k12p():
+            return torch.ops.madnn.linear_dgrad_p(g2, weight, None, g2.dtype, 1)[0]
+        cands["k12p"] = k12p
+    if DGRAD in cands:
+        return cands[DGRAD]()
     key = (tuple(g2.shape), tuple(weight.shape))
-    return {"lt": lt, "k12p": k12p}[_timed_choice(_DGRAD_CHOICE, key, {"lt": lt, "k12p": k12p}, "lt")]()
+    return cands[_timed_choice(_DGRAD_CHOICE, key, cands, "lt")]()
 
 
 class _LinearFn(torch.autograd.Function):

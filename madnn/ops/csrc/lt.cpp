@@ -55,19 +55,24 @@ struct Plan {
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
   hipblasLtMatmulAlgo_t algo;
   size_t ws = 0;
+  int n = 0;  // candidates the heuristic returned
 };
 
-using Key = std::tuple<int64_t, int64_t, int64_t, int, int, int, int, int, size_t>;  // [7]: w given [K, N]
+using Key = std::tuple<int64_t, int64_t, int64_t, int, int, int, int, int, size_t, int>;  // [7]: w given [K, N], [9]: algo
+constexpr int kMaxAlgos = 16;
 std::map<Key, Plan> g_plans;
 std::mutex g_mu;
 
 Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEpilogue_t epi, hipDataType dt,
                hipDataType bias_dt, bool has_c, size_t ws_cap, const void* bias_ptr, void* aux_ptr,
-               bool w_kn = false) {
-  Key key{M, N, K, (int)epi, (int)dt, (int)bias_dt, (int)has_c, w_kn ? 1 : 0, ws_cap};
+               bool w_kn = false, int algo = 0, int* n_algos = nullptr) {
+  Key key{M, N, K, (int)epi, (int)dt, (int)bias_dt, (int)has_c, w_kn ? 1 : 0, ws_cap, algo};
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_plans.find(key);
-  if (it != g_plans.end()) return it->second;
+  if (it != g_plans.end()) {
+    if (n_algos != nullptr) *n_algos = it->second.n;
+    return it->second;
+  }
   Plan p;
   LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   hipblasOperation_t ta = w_kn ? HIPBLAS_OP_N : HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
@@ -99,13 +104,21 @@ Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEp
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t cap = ws_cap;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &cap, sizeof(cap)));
-  hipblasLtMatmulHeuristicResult_t res[1];
+  // the heuristic's ranked candidates: `algo` picks one (0 = its first choice; a per-shape timed index
+  // from the tuning table can name a faster one, madnn.ops.lt_algo)
+  hipblasLtMatmulHeuristicResult_t res[kMaxAlgos];
   int n = 0;
-  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.a, p.b, p.c, p.d, pref, 1, res, &n));
+  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.a, p.b, p.c, p.d, pref, algo > 0 ? kMaxAlgos : 1, res, &n));
   hipblasLtMatmulPreferenceDestroy(pref);
   TORCH_CHECK(n > 0, "lt_linear: hipBLASLt has no algorithm for M=", M, " N=", N, " K=", K, " epilogue=", (int)epi);
-  p.algo = res[0].algo;
-  p.ws = res[0].workspaceSize;
+  if (n_algos != nullptr) {  // lt_algo_count's query: the count, and the last candidate as the plan
+    *n_algos = n;
+    algo = algo < n ? algo : n - 1;
+  }
+  TORCH_CHECK(algo < n, "lt_linear: algorithm index ", algo, " of ", n);
+  p.n = n;
+  p.algo = res[algo].algo;
+  p.ws = res[algo].workspaceSize;
   (void)has_c;
   return g_plans.emplace(key, p).first->second;
 }
@@ -116,7 +129,8 @@ Plan& get_plan(hipblasLtHandle_t h, int64_t M, int64_t N, int64_t K, hipblasLtEp
 std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tensor& w,
                                              const c10::optional<at::Tensor>& bias,
                                              const c10::optional<at::Tensor>& residual, bool gelu, bool want_pre,
-                                             bool w_kn) {
+                                             bool w_kn, int64_t algo) {
+  TORCH_CHECK(algo >= 0 && algo < kMaxAlgos, "lt_linear: algo in [0, ", kMaxAlgos, ")");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 2 && w.dim() == 2, "lt_linear: 2-D HIP tensors");
   TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "lt_linear: contiguous x and w");
   TORCH_CHECK(x.scalar_type() == w.scalar_type(), "lt_linear: x and w dtypes differ");
@@ -145,7 +159,7 @@ std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tens
   at::Tensor pre;
   if (gelu && want_pre) pre = at::empty({M, N}, x.options());
   Plan& p = get_plan(h, M, N, K, epi, dt, bdt, has_res, ws_cap, has_bias ? bias->data_ptr() : nullptr,
-                     pre.defined() ? pre.data_ptr() : nullptr, w_kn);
+                     pre.defined() ? pre.data_ptr() : nullptr, w_kn, (int)algo);
   if (has_bias) {
     const void* bp = bias->data_ptr();
     LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)));
@@ -160,6 +174,21 @@ std::tuple<at::Tensor, at::Tensor> lt_linear(const at::Tensor& x, const at::Tens
   LT_CHECK(hipblasLtMatmul(h, p.desc, &alpha, w.data_ptr(), p.a, x.data_ptr(), p.b, &beta, cptr, p.c, y.data_ptr(),
                            p.d, &p.algo, ws, p.ws, stream));
   return {y, pre.defined() ? pre : at::empty({0}, x.options())};
+}
+
+// How many ranked candidates the heuristic offers for lt_linear's problem (bias / no bias, no GELU, no
+// residual) -- the range of lt_linear's `algo`
+int64_t lt_algo_count(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, bool w_kn) {
+  const int64_t M = x.size(0), K = x.size(1), N = w_kn ? w.size(1) : w.size(0);
+  const bool has_bias = bias.has_value() && bias->defined();
+  const hipDataType dt = lt_type(x.scalar_type());
+  const hipDataType bdt = has_bias ? lt_type(bias->scalar_type()) : dt;
+  const at::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
+  int n = 0;
+  get_plan(h, M, N, K, has_bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT, dt, bdt, false,
+           at::cuda::getCUDABlasLtWorkspaceSize(), has_bias ? bias->data_ptr() : nullptr, nullptr, w_kn, kMaxAlgos - 1, &n);
+  return n;
 }
 
 // How many algorithms hipBLASLt's heuristic offers for an epilogue / type combination
@@ -214,7 +243,8 @@ int64_t lt_probe(int64_t M, int64_t N, int64_t K, int64_t epi, int64_t bias_code
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(madnn, m) {
-  m.def("lt_linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu, bool want_pre, bool w_kn=False) -> (Tensor, Tensor)");
+  m.def("lt_linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu, bool want_pre, bool w_kn=False, int algo=0) -> (Tensor, Tensor)");
+  m.def("lt_algo_count(Tensor x, Tensor w, Tensor? bias, bool w_kn=False) -> int");
   // no tensor arguments -> nothing to dispatch on: a catch-all kernel
   m.def("lt_probe(int M, int N, int K, int epi, int bias_code, int aux_code, bool has_c, int dummy_ptr) -> int",
         TORCH_FN(lt_probe));
@@ -222,4 +252,5 @@ TORCH_LIBRARY_FRAGMENT(madnn, m) {
 
 TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("lt_linear", lt_linear);
+  m.impl("lt_algo_count", lt_algo_count);
 }

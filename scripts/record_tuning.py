@@ -39,7 +39,7 @@ def main():
                     help="start from the shipped choice table (time only the shapes it lacks) instead of an empty one")
     ap.add_argument("--retime", default="",
                     help="with --keep-table: comma list of table:kind entries to drop and time afresh, e.g. "
-                         "wgrad:linear (every Linear weight gradient, with K12W as a candidate)")
+                         "wgrad:linear (every Linear weight gradient, with K12W as a candidate); table:* drops a whole table")
     args = ap.parse_args()
     out = Path(args.out)
     db = out / "miopen"
@@ -64,7 +64,7 @@ def main():
                   "dgrad": ops._DGRAD_CHOICE}
         for item in [v for v in args.retime.split(",") if v]:
             tab, kind = item.split(":")
-            for k in [k for k in tables[tab] if k and k[0] == kind]:
+            for k in [k for k in tables[tab] if k and (kind == "*" or k[0] == kind)]:
                 del tables[tab][k]
     dev = madnn.device()
     rec = []
