@@ -386,10 +386,14 @@ def _fit_measurements(distinct, mine) -> dict:
         fwd_ps, bwd_ps, fixed = f1 / n1, k1 / n1, 0.0
         if len(res) > 1:
             (n2, f2, k2) = res[1]
-            # t(n) = fixed + n * slope through the two points (slope from the large batch when
-            # the small one is not slower per call, i.e. launch-bound noise)
-            slope_f = max((f1 - f2) / (n1 - n2), 0.0) if n1 != n2 else f1 / n1
-            slope_b = max((k1 - k2) / (n1 - n2), 0.0) if n1 != n2 else k1 / n1
+            # t(n) = fixed + n * slope through the two points; a component whose time did not grow
+            # with the batch (launch-bound noise at the small size, or a small part of the layer,
+            # e.g. a loss node whose gradient the forward already formed) keeps the large batch's
+            # per-sample rate instead of a zero slope: no layer is free per sample
+            slope_f = (f1 - f2) / (n1 - n2) if n1 != n2 else 0.0
+            slope_b = (k1 - k2) / (n1 - n2) if n1 != n2 else 0.0
+            slope_f = slope_f if slope_f > 0 else f1 / n1
+            slope_b = slope_b if slope_b > 0 else k1 / n1
             if slope_f + slope_b > 0:
                 fixed = max((f1 + k1) - n1 * (slope_f + slope_b), 0.0)
                 fwd_ps, bwd_ps = slope_f, slope_b

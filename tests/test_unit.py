@@ -994,3 +994,20 @@ def test_scaled_loss_passes_the_scale_into_scale_aware_losses():
     ids = torch.randint(0, 512, (2, 16))
     logits = m(ids)
     torch.testing.assert_close(ops.scaled_loss(m.loss_fn, logits, ids, 0.5), 0.5 * m.loss_fn(logits, ids))
+
+
+def test_layer_fit_never_prices_a_component_at_zero_per_sample():
+    """Two-point layer fit (planner.cost._fit_measurements): a forward or backward whose time did not
+    grow from the quarter batch to the full batch keeps the full batch's per-sample rate (the GPU
+    tier's planner test requires fwd_s, bwd_s > 0 for every layer)."""
+    from madnn.planner.cost import _fit_measurements
+
+    # (n, fwd ms, bwd ms): forward grows 4x, backward flat (0.30 ms at 64 and 0.31 ms at 16)
+    fit = _fit_measurements(["a"], [[(64, 4.0, 0.30), (16, 1.0, 0.31)]])
+    f, b, fixed = fit["a"]
+    assert f > 0 and b > 0 and fixed >= 0
+    assert abs(b - 0.30 / 64 / 1e3) < 1e-12          # the large batch's per-sample rate
+    # both grow: the ordinary fixed + slope fit through the two points
+    f, b, fixed = _fit_measurements(["a"], [[(64, 4.2, 8.2), (16, 1.2, 2.2)]])["a"]
+    assert abs(f - 3.0 / 48 / 1e3) < 1e-12 and abs(b - 6.0 / 48 / 1e3) < 1e-12
+    assert abs(fixed - (12.4 - 64 * 9.0 / 48) / 1e3) < 1e-12
