@@ -82,9 +82,16 @@ def main():
             w0 = w12(dy, x, None, False, 0)
             w1 = w12w(dy, x, None, False, 0)
             diff = float((w0.float() - w1.float()).norm() / w0.float().norm())
-            for rnd in range(2):          # interleaved: K12, K12W, hipBLASLt, twice
+            if M % 128 == 0:   # K12W16 against K12
+                w2 = torch.ops.madnn.linear_wgrad4h(dy, x, None, False, 0)
+                diff16 = float((w0.float() - w2.float()).norm() / w0.float().norm())
+                assert diff16 < 1e-2, (name, diff16)
+            for rnd in range(2):          # interleaved: K12, K12W, K12W16, hipBLASLt, twice
                 t.setdefault("k12", []).append(timed(lambda: w12(dy, x, out, False, 0), args.reps))
                 t.setdefault("k12w", []).append(timed(lambda: w12w(dy, x, out, False, 0), args.reps))
+                if M % 128 == 0:
+                    t.setdefault("k12wh", []).append(
+                        timed(lambda: torch.ops.madnn.linear_wgrad4h(dy, x, out, False, 0), args.reps))
                 t.setdefault("lt", []).append(timed(lambda: torch.mm(dy.t(), x, out=out), args.reps))
             best = {k: min(v) for k, v in t.items()}
             row = {"shape": name, "M": M, "N": N, "K": K, "splits": sp, "k12w_vs_k12_rel": float(f"{diff:.3g}")}

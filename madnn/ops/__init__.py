@@ -1404,25 +1404,32 @@ def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor) -> torch.T
         return lib()
     return tuned_wgrad(("linear",) + tuple(g2.shape) + (x2.shape[1],), lib,
                        lambda: torch.ops.madnn.linear_wgrad(g2, x2, out, False, 0),
-                       k12w=lambda: torch.ops.madnn.linear_wgrad4(g2, x2, out, False, 0))
+                       k12w=lambda: torch.ops.madnn.linear_wgrad4(g2, x2, out, False, 0),
+                       k12wh=(lambda: torch.ops.madnn.linear_wgrad4h(g2, x2, out, False, 0))
+                       if g2.shape[0] % 128 == 0 else None)
 
 
-def tuned_wgrad(key, lib, k12, k9=None, k12w=None):
+def tuned_wgrad(key, lib, k12, k9=None, k12w=None, k12wh=None):
     """Run the weight-gradient implementation that was faster for ``key``: ``lib`` (the library
     kernel: hipBLASLt / MIOpen), ``k12`` (K12 split-K over the rows), ``k12w`` (K12W: the same
-    split-K GEMM at one wave per SIMD, 128 x 128 per wave) or, for NHWC 1x1 convolutions, ``k9``
-    (K9's split-M kernel, slabs reduced and cast in one pass) -- from the shipped table
-    (:func:`load_tuning_table`), else timed once on first use (outside graph capture).
-    ``MADNN_WGRAD=lt`` / ``k12`` / ``k12w`` pin one."""
+    split-K GEMM at one wave per SIMD, 128 x 128 per wave, on ``v_mfma_f32_32x32x16_bf16``), ``k12wh``
+    (K12W16: its ``v_mfma_f32_16x16x32_bf16`` form, rows a multiple of 128) or, for NHWC 1x1
+    convolutions, ``k9`` (K9's split-M kernel, slabs reduced and cast in one pass) -- from the shipped
+    table (:func:`load_tuning_table`), else timed once on first use (outside graph capture).
+    ``MADNN_WGRAD=lt`` / ``k12`` / ``k12w`` / ``k12wh`` pin one."""
     if WGRAD == "lt":
         return lib()
     if WGRAD == "k12":
         return k12()
     if WGRAD == "k12w" and k12w is not None:
         return k12w()
+    if WGRAD == "k12wh" and k12wh is not None:
+        return k12wh()
     cands = {"lib": lib, "k12": k12}
     if k12w is not None:
         cands["k12w"] = k12w
+    if k12wh is not None:
+        cands["k12wh"] = k12wh
     if k9 is not None:
         cands["k9"] = k9
     choice = _WGRAD_CHOICE.get(key)
@@ -1458,7 +1465,9 @@ def _conv1x1_wgrad_lib(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> to
     k9 = (lambda: _k9_wgrad(dy, x, w)) if x.dim() == 4 and conv1x1_supported(x, w.view(w.size(0), -1)) else None
     return tuned_wgrad(("conv1x1", dr.shape[0], dr.shape[1], xr.shape[1]), lib,
                        lambda: torch.ops.madnn.linear_wgrad(dr, xr, None, False, 0).view(w.shape), k9,
-                       k12w=lambda: torch.ops.madnn.linear_wgrad4(dr, xr, None, False, 0).view(w.shape))
+                       k12w=lambda: torch.ops.madnn.linear_wgrad4(dr, xr, None, False, 0).view(w.shape),
+                       k12wh=(lambda: torch.ops.madnn.linear_wgrad4h(dr, xr, None, False, 0).view(w.shape))
+                       if dr.shape[0] % 128 == 0 else None)
 
 
 LT_EPILOGUE = os.environ.get("MADNN_LT_EPILOGUE", "1") != "0"  # hipBLASLt GELU/residual epilogues (A/B switch)

@@ -111,6 +111,8 @@ hipError_t madnn_linear_fwd(const void*, const void*, const void*, int, const vo
                             int64_t, int64_t, hipStream_t);
 hipError_t madnn_linear_dgrad(const void*, const void*, const void*, void*, int64_t, int64_t, int64_t, hipStream_t);
 int madnn_wgrad_splits(int64_t, int64_t, int64_t);
+hipError_t madnn_linear_wgrad4h(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
+                                hipStream_t);
 hipError_t madnn_linear_wgrad4(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
                                hipStream_t);
 hipError_t madnn_linear_wgrad(const void*, const void*, void*, float*, int, int, int64_t, int64_t, int64_t,
@@ -750,7 +752,7 @@ at::Tensor linear_dgrad(const at::Tensor& dy, const at::Tensor& w, const c10::op
 // output tiles of a weight gradient fill the GPU.  With `out` the result is written there (the
 // reducer's bucket slot: a grad sink), with accumulate added to its contents.  splits <= 0: auto.
 at::Tensor linear_wgrad_impl(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
-                             bool accumulate, int64_t splits, bool four_wave) {
+                             bool accumulate, int64_t splits, int kind) {
   gemm_check(dy, "dy");
   gemm_check(x, "x");
   const int64_t N = dy.size(-1), K = x.size(-1), M = dy.numel() / std::max<int64_t>(N, 1);
@@ -769,7 +771,8 @@ at::Tensor linear_wgrad_impl(const at::Tensor& dy, const at::Tensor& x, const c1
   }
   const int sp = splits > 0 ? (int)splits : madnn_wgrad_splits(M, N, K);
   at::Tensor ws = sp > 1 ? at::empty({sp, N, K}, dy.options().dtype(at::kFloat)) : at::Tensor();
-  auto fn = four_wave ? madnn_linear_wgrad4 : madnn_linear_wgrad;
+  if (kind == 2) TORCH_CHECK(M % 128 == 0, "linear_wgrad4h: tokens must be a multiple of 128");
+  auto fn = kind == 2 ? madnn_linear_wgrad4h : kind == 1 ? madnn_linear_wgrad4 : madnn_linear_wgrad;
   check(fn(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), sp > 1 ? ws.data_ptr<float>() : nullptr, sp, accumulate ? 1 : 0,
            M, N, K, cur_stream(dy)),
         "linear_wgrad");
@@ -778,13 +781,19 @@ at::Tensor linear_wgrad_impl(const at::Tensor& dy, const at::Tensor& x, const c1
 
 at::Tensor linear_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
                         bool accumulate, int64_t splits) {
-  return linear_wgrad_impl(dy, x, out, accumulate, splits, false);
+  return linear_wgrad_impl(dy, x, out, accumulate, splits, 0);
 }
 
 // K12W (gemm.hip: one wave per SIMD, 128 x 128 per wave), same contract
 at::Tensor linear_wgrad4(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
                          bool accumulate, int64_t splits) {
-  return linear_wgrad_impl(dy, x, out, accumulate, splits, true);
+  return linear_wgrad_impl(dy, x, out, accumulate, splits, 1);
+}
+
+// K12W16 (gemm.hip gemm4h_kernel: the v_mfma_f32_16x16x32_bf16 form), same contract, tokens % 128 == 0
+at::Tensor linear_wgrad4h(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& out,
+                          bool accumulate, int64_t splits) {
+  return linear_wgrad_impl(dy, x, out, accumulate, splits, 2);
 }
 
 int64_t wgrad_splits(int64_t M, int64_t N, int64_t K) { return madnn_wgrad_splits(M, N, K); }
@@ -1491,6 +1500,7 @@ TORCH_LIBRARY(madnn, m) {
   m.def("linear_dgrad(Tensor dy, Tensor w, Tensor? res, bool accumulate) -> Tensor");
   m.def("linear_wgrad(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
   m.def("linear_wgrad4(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
+  m.def("linear_wgrad4h(Tensor dy, Tensor x, Tensor? out, bool accumulate, int splits) -> Tensor");
   m.def("wgrad_splits(int M, int N, int K) -> int", &wgrad_splits);
   m.def("gemmp_supported(int I, int J, int K, bool has_bias) -> bool", &gemmp_supported);
   m.def("linear_fwd_p(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
@@ -1570,6 +1580,7 @@ TORCH_LIBRARY_IMPL(madnn, CUDA, m) {
   m.impl("linear_dgrad", linear_dgrad);
   m.impl("linear_wgrad", linear_wgrad);
   m.impl("linear_wgrad4", linear_wgrad4);
+  m.impl("linear_wgrad4h", linear_wgrad4h);
   m.impl("linear_fwd_p", linear_fwd_p);
   m.impl("linear_dgrad_p", linear_dgrad_p);
   m.impl("conv3x3_fwd", conv3x3_fwd);

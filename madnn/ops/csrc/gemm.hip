@@ -52,6 +52,7 @@
 // aux = pre-activation store, tanh-GELU, residual add (fp32 add of two bf16, one rounding:
 // the same two roundings as the unfused PyTorch graph).
 #include <type_traits>
+#include <utility>
 
 #include "k12.h"
 
@@ -635,6 +636,214 @@ __global__ __launch_bounds__(256, 1) void gemm4_kernel(const Args p) {
   });
 }
 
+// f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>): a compile-time loop (a 64-step
+// `#pragma unroll` body this large stays a runtime loop, and its register arrays go to scratch)
+template <class F, int... Q>
+__device__ __forceinline__ void seq_impl(F&& f, std::integer_sequence<int, Q...>) {
+  (f(std::integral_constant<int, Q>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void for_seq(F&& f) {
+  seq_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// K12W on v_mfma_f32_16x16x32_bf16 (K12W16, madnn_linear_wgrad4h): the same 256x256 tile, one wave
+// per SIMD owning 128 x 128 as 8 x 8 blocks of 16 x 16 (64 f32x4 accumulators, 256 AGPRs), the same
+// LDS images / DMA pieces / counted waits; a K tile is 2 phases of one 32-deep k step each (64 MFMAs of
+// 16 cycles), both behind a barrier (RAW for the part read during the phase, WAR for the part the
+// phase's DMA refills).  Why: on random data the chip holds a higher clock on this shape at equal cycles
+// per FLOP (MI355X_MICROARCH.md, DVFS give-back 7).
+//   gap q of a phase: q == 2 wait + barrier; q = 3, 7, .., 31 one DMA piece; q = 4, 6, .., 34 the
+//   next phase's fragment 0..15 (A0, B0..B7, A1..A7: the order its MFMAs consume them).
+// v_mfma_f32_16x16x32_bf16 with the accumulator pinned to AGPRs: hipcc spreads 64 f32x4 accumulator
+// tuples over both register files and shuffles them every iteration (v_accvgpr_read / write around the
+// MFMAs); as an asm operand ("+a") every tuple stays in its AGPRs.  hipcc sees no MFMA here, so its
+// result is read only after mfma_drain() (wait states for the last MFMAs' writes).
+__device__ __forceinline__ void mfma16a(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_drain() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+}
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 1) void gemm4h_kernel(const Args p) {
+  static_assert(A_COL && B_COL, "K12W: weight gradient (both operands k-major)");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kLds];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+
+  int wid = blockIdx.x;
+  {
+    const int n = gridDim.x, x = wid % 8, q8 = n / 8, r8 = n % 8;
+    wid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + wid / 8;
+  }
+  const int ntile = p.i_tiles * p.j_tiles;
+  const int split = wid / ntile;
+  wid -= split * ntile;
+  const int it = wid % p.i_tiles, jt = wid / p.i_tiles;
+  const int64_t i0 = (int64_t)it * kT, j0 = (int64_t)jt * kT;
+  const int64_t kbeg = (int64_t)split * p.kper;
+  const int64_t klen = p.K - kbeg < p.kper ? p.K - kbeg : p.kper;
+  const int nk = (int)(klen / kBK);
+
+  const bool isA = wave < 2;
+  const uint16_t* const op = isA ? p.a : p.b;
+  const int64_t ld = isA ? p.lda : p.ldb;
+  const int64_t x0 = isA ? i0 + 128 * wave : j0 + 128 * (wave - 2);
+  unsigned voff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) voff[e] = (unsigned)(2 * (x0 + dma_offset<true>(e, lane, ld, x0, isA ? p.I : p.J)));
+  const char* const gbase = reinterpret_cast<const char*>(op + kbeg * ld);
+  const int64_t tbytes = (int64_t)kBK * ld * 2, pbytes = (int64_t)32 * ld * 2;
+  const unsigned ldsw = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(smem + 2 * wave * kHalf));
+  auto dma1 = [&](const char* tb, auto st_c, auto part_c, auto e_c) {
+    constexpr unsigned o = decltype(st_c)::value * kHalf * 2 + decltype(part_c)::value * 8192 + decltype(e_c)::value * 1024;
+    glds16_one<o>(tb + decltype(part_c)::value * pbytes, ldsw, voff[decltype(e_c)::value]);
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  auto dma_part = [&](const char* tb, auto st_c, auto part_c) {
+    dma1(tb, st_c, part_c, std::integral_constant<int, 0>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 1>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 2>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 3>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 4>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 5>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 6>{});
+    dma1(tb, st_c, part_c, std::integral_constant<int, 7>{});
+  };
+
+  f32x4 ac[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) ac[a][b] = zero4();
+
+  // per-lane LDS byte addresses of k12::frag16<true> reads of 16-column block x (of 8) of this wave's
+  // A / B half-tile, row quad hq (lo / hi): byte(st, s, x, hq) = st * 16 KiB + s * 8 KiB + ad[x][hq]
+  const int g = lane >> 4, i = lane & 15;
+  unsigned adA[8][2], adB[8][2];
+  {
+    const unsigned baseA = (unsigned)(size_t)(smem + 2 * wr * kHalf);
+    const unsigned baseB = (unsigned)(size_t)(smem + 2 * (2 + wc) * kHalf);
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {
+      const int row = 8 * g + (i >> 2) + 4 * hq;
+      const int f = ((row & 3) << 2) | ((row >> 2) & 3);
+#pragma unroll
+      for (int xb = 0; xb < 8; ++xb) {
+        const int ch = 2 * xb + ((i & 3) >> 1);
+        const unsigned o = (unsigned)(row * 256 + 16 * (ch ^ f) + 8 * (i & 1));
+        adA[xb][hq] = baseA + o;
+        adB[xb][hq] = baseB + o;
+      }
+    }
+  }
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto frag = [&](const unsigned (&ad)[2], auto st_c, auto s_c) {
+    constexpr int imm = decltype(st_c)::value * kHalf * 2 + decltype(s_c)::value * 8192;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(ad[0] + imm));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(ad[1] + imm));
+    const s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  };
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+
+  if (nk > 0) {
+  const char* const tb1 = gbase + (int64_t)(nk > 1 ? 1 : 0) * tbytes;
+  dma_part(gbase, C0{}, C0{});
+  dma_part(gbase, C0{}, C1{});
+  dma_part(tb1, C1{}, C0{});
+  dma_part(tb1, C1{}, C1{});
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");   // K0(0)
+  barrier();
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    fa0[x] = frag(adA[x], C0{}, C0{});
+    fb0[x] = frag(adB[x], C0{}, C0{});
+  }
+
+  // one phase: 64 MFMAs on (fc, gc) in A-block-major order (all 16 fragments read in the previous
+  // phase: the DMA of this phase refills the part they came from); after MFMA 2 the wait + barrier;
+  // part `part` of the K tile at tb into stage ST; the next phase's fragments (stage NS, k step NSS)
+  // into (fn, gn): A0, B0..B7, A1..A7, the order its MFMAs consume them
+  auto phase = [&](const bf16x8 (&fc)[8], const bf16x8 (&gc)[8], bf16x8 (&fn)[8], bf16x8 (&gn)[8], auto ns_c,
+                   auto nss_c, const char* tb, auto st_c, auto part_c) {
+    for_seq<64>([&](auto q_c) {
+      constexpr int q = decltype(q_c)::value;
+      mfma16a(ac[q >> 3][q & 7], fc[q >> 3], gc[q & 7]);
+      if constexpr (q == 2) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier();
+      }
+      if constexpr (q >= 3 && q <= 31 && (q - 3) % 4 == 0)
+        dma1(tb, st_c, part_c, std::integral_constant<int, (q - 3) / 4>{});
+      if constexpr (q >= 4 && q <= 34 && (q & 1) == 0) {
+        constexpr int f = (q - 4) >> 1;
+        if constexpr (f == 0) fn[0] = frag(adA[0], ns_c, nss_c);
+        else if constexpr (f <= 8) gn[f - 1] = frag(adB[f - 1], ns_c, nss_c);
+        else fn[f - 8] = frag(adA[f - 8], ns_c, nss_c);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  auto ktile = [&](int t, auto st_c) {
+    using ST = decltype(st_c);
+    using NST = std::integral_constant<int, 1 - ST::value>;
+    const int t2 = t + 2 < nk ? t + 2 : nk - 1;
+    const char* tb = gbase + (int64_t)t2 * tbytes;
+    __builtin_amdgcn_sched_barrier(0);
+    phase(fa0, fb0, fa1, fb1, ST{}, C1{}, tb, ST{}, C0{});    // P0: k step 0 (K0(t)); RAW K1(t), refill K0(t + 2)
+    phase(fa1, fb1, fa0, fb0, NST{}, C0{}, tb, ST{}, C1{});   // P1: k step 1 (K1(t)); RAW K0(t + 1), refill K1(t + 2)
+  };
+  // nk is even (the host gives every split an even number of K tiles): no odd tail block, around
+  // which hipcc would copy accumulators out of the AGPRs while the asm MFMAs are still writing them
+  for (int t = 0; t < nk; t += 2) {
+    ktile(t, C0{});
+    ktile(t + 1, C1{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped reloads
+  mfma_drain();   // inside the branch: the join block after it may already copy accumulators
+  }
+
+  // accumulator (a, b) register r: i row wr*128 + 16a + 4(lane >> 4) + r, j col wc*128 + 16b + (lane & 15)
+  const int ig4 = 4 * (lane >> 4), l16 = lane & 15;
+  if (p.ws != nullptr) {
+    float* slab = p.ws + (int64_t)split * p.J * p.I;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int64_t ig = i0 + wr * 128 + 16 * a + ig4, jg = j0 + wc * 128 + 16 * b + l16;
+        if (ig < p.I && jg < p.J) *reinterpret_cast<f32x4*>(slab + jg * p.I + ig) = ac[a][b];
+      }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const int64_t ig = i0 + wr * 128 + 16 * a + ig4, jg = j0 + wc * 128 + 16 * b + l16;
+      if (ig < p.I && jg < p.J) {
+        const f32x4 v = ac[a][b];
+        float w[4] = {v[0], v[1], v[2], v[3]};
+        if (p.res != nullptr) {
+          const u32x2 r = *reinterpret_cast<const u32x2*>(p.res + jg * p.ldr + ig);
+          w[0] += bf16_to_f32((unsigned short)(r[0] & 0xffffu));
+          w[1] += bf16_to_f32((unsigned short)(r[0] >> 16));
+          w[2] += bf16_to_f32((unsigned short)(r[1] & 0xffffu));
+          w[3] += bf16_to_f32((unsigned short)(r[1] >> 16));
+        }
+        const unsigned lo = (unsigned)f32_to_bf16(w[0]) | ((unsigned)f32_to_bf16(w[1]) << 16);
+        const unsigned hi = (unsigned)f32_to_bf16(w[2]) | ((unsigned)f32_to_bf16(w[3]) << 16);
+        *reinterpret_cast<u32x2*>(p.out + jg * p.ldo + ig) = u32x2{lo, hi};
+      }
+    }
+}
+
 template <bool A_COL, bool B_COL>
 hipError_t launch(Args& p, hipStream_t s) {
   p.i_tiles = (int)((p.I + kT - 1) / kT);
@@ -758,10 +967,13 @@ hipError_t madnn_linear_wgrad(const void* dy, const void* x, void* dw, float* ws
   return hipGetLastError();
 }
 
-// K12W weight gradient (same contract as madnn_linear_wgrad; the split count from madnn_wgrad_splits)
-hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
-                               int64_t M, int64_t N, int64_t K, hipStream_t s) {
+// K12W weight gradient (same contract as madnn_linear_wgrad; the split count from madnn_wgrad_splits).
+// mfma16: the v_mfma_f32_16x16x32_bf16 form (gemm4h_kernel), which needs an even number of K tiles per
+// split (M a multiple of 128; every split gets an even share).
+static hipError_t linear_wgrad4_launch(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
+                                       int64_t M, int64_t N, int64_t K, hipStream_t s, bool mfma16) {
   if (M % kBK || !madnn_gemm_supported(K, N, M, K, N)) return hipErrorInvalidValue;
+  if (mfma16 && M % (2 * kBK)) return hipErrorInvalidValue;
   if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
   Args p{};
   p.a = static_cast<const uint16_t*>(x);
@@ -776,8 +988,13 @@ hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* w
   p.J = N;
   p.K = M;
   p.splits = splits > 1 ? splits : 1;
-  const int64_t nk = M / kBK;
-  p.kper = ((nk + p.splits - 1) / p.splits) * kBK;
+  if (mfma16) {
+    const int64_t pairs = M / (2 * kBK);
+    p.kper = ((pairs + p.splits - 1) / p.splits) * 2 * kBK;
+  } else {
+    const int64_t nk = M / kBK;
+    p.kper = ((nk + p.splits - 1) / p.splits) * kBK;
+  }
   p.ws = p.splits > 1 ? ws : nullptr;
   p.i_tiles = (int)((p.I + kT - 1) / kT);
   p.j_tiles = (int)((p.J + kT - 1) / kT);
@@ -785,7 +1002,10 @@ hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* w
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   // saddr DMA: per-lane 32-bit byte offsets (31 rows + a column) within a 32-row part
   if ((p.lda > p.ldb ? p.lda : p.ldb) >= ((int64_t)1 << 25) || p.I > p.lda || p.J > p.ldb) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm4_kernel<true, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  if (mfma16)
+    hipLaunchKernelGGL((gemm4h_kernel<true, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm4_kernel<true, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || p.splits == 1) return e;
   const int64_t n = N * K;
@@ -794,6 +1014,16 @@ hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* w
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, ws, static_cast<uint16_t*>(dw),
                      p.splits, n, accumulate);
   return hipGetLastError();
+}
+
+hipError_t madnn_linear_wgrad4(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
+                               int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  return linear_wgrad4_launch(dy, x, dw, ws, splits, accumulate, M, N, K, s, false);
+}
+
+hipError_t madnn_linear_wgrad4h(const void* dy, const void* x, void* dw, float* ws, int splits, int accumulate,
+                                int64_t M, int64_t N, int64_t K, hipStream_t s) {
+  return linear_wgrad4_launch(dy, x, dw, ws, splits, accumulate, M, N, K, s, true);
 }
 
 }  // extern "C"

@@ -106,11 +106,16 @@ WGRAD_SHAPES = [(256, 256, 64, 1), (4096, 1024, 1024, 0), (2048, 3072, 1024, 5),
                 (8192, 1032, 4096, 0), (64, 64, 64, 1)]
 
 
-@pytest.mark.parametrize("kernel", ["linear_wgrad", "linear_wgrad4"])   # K12 (8 waves), K12W (4 waves)
-@pytest.mark.parametrize("M,N,K,splits", WGRAD_SHAPES + [(64 * 37, 136, 1000, 7), (64 * 20, 520, 264, 40)])
+# K12 (8 waves), K12W (4 waves, 32x32x16), K12W16 (4 waves, 16x16x32: tokens a multiple of 128)
+@pytest.mark.parametrize("kernel", ["linear_wgrad", "linear_wgrad4", "linear_wgrad4h"])
+@pytest.mark.parametrize("M,N,K,splits", WGRAD_SHAPES + [(64 * 37, 136, 1000, 7), (64 * 20, 520, 264, 40),
+                                         (128 * 37, 136, 1000, 7)])
 def test_linear_wgrad_split_k(M, N, K, splits, kernel):
-    """Both weight-gradient kernels against fp32, with ragged N / K tiles, odd K-tile counts (K12W
-    runs its K loop in pairs) and more splits than K tiles per split (empty splits write zeros)."""
+    """The weight-gradient kernels against fp32, with ragged N / K tiles, odd K-tile counts (K12W
+    runs its K loop in pairs; K12W16 gives every split an even count) and more splits than K tiles
+    per split (empty splits write zeros)."""
+    if kernel == "linear_wgrad4h" and M % 128:
+        pytest.skip("K12W16 takes token counts that are multiples of 128 (the binding refuses others)")
     m = _ops()
     wgrad = getattr(m, kernel)
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K)
@@ -125,6 +130,14 @@ def test_linear_wgrad_split_k(M, N, K, splits, kernel):
     out = base.clone()
     wgrad(dy, x, out, True, splits)
     assert _rel(out, ref + base.float()) < 6e-3
+
+
+def test_linear_wgrad4h_refuses_odd_token_tiles():
+    m = _ops()
+    dy = torch.randn(64 * 3, 256, device="cuda").bfloat16()
+    x = torch.randn(64 * 3, 256, device="cuda").bfloat16()
+    with pytest.raises(RuntimeError, match="multiple of 128"):
+        m.linear_wgrad4h(dy, x, None, False, 0)
 
 
 def test_linear_wgrad_splits_heuristic_fills_the_gpu():
