@@ -569,19 +569,20 @@ def test_fault_injection_parse():
         del os.environ["MADNN_FAULT"]
 
 
-def test_kernel_library_built_for_gfx950():
-    """build() output exists and carries a gfx950 code object (checked without a GPU)."""
+def test_kernel_library_built_for_gfx950(tmp_path):
+    """build() output exists and carries a gfx950 code object (checked without a GPU; the bundles are
+    extracted next to a copy in tmp_path, never beside the in-tree library)."""
+    import shutil
     import subprocess
 
     so = ops.kernels_path()
     if not so.exists():
         pytest.skip("kernel library not built")
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(so)], capture_output=True,
-                         text=True, cwd="/tmp")
+    local = tmp_path / so.name
+    shutil.copy(so, local)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(local)], capture_output=True,
+                         text=True)
     assert "gfx950" in out.stdout + out.stderr
-    for f in os.listdir("/tmp"):
-        if f.startswith(so.name + "."):
-            os.remove(os.path.join("/tmp", f))
 
 
 def test_miopen_find_db_seeding(tmp_path, monkeypatch):
@@ -1011,3 +1012,37 @@ def test_layer_fit_never_prices_a_component_at_zero_per_sample():
     f, b, fixed = _fit_measurements(["a"], [[(64, 4.2, 8.2), (16, 1.2, 2.2)]])["a"]
     assert abs(f - 3.0 / 48 / 1e3) < 1e-12 and abs(b - 6.0 / 48 / 1e3) < 1e-12
     assert abs(fixed - (12.4 - 64 * 9.0 / 48) / 1e3) < 1e-12
+
+
+def test_k12w16_asm_mfma_accumulators_are_never_copied_in_flight(tmp_path):
+    """K12W16 (gemm.hip gemm4h_kernel) issues its MFMAs as asm statements, so hipcc does not know their
+    AGPR results land several cycles later: the built ISA must not copy, spill or read an accumulator
+    (v_accvgpr_read / write / mov, scratch traffic) between the first MFMA and the drain (s_nop 7 run)
+    after the last one (checked on the gfx950 code object, no GPU needed)."""
+    import shutil
+    import subprocess
+
+    so = ops.kernels_path()
+    if not so.exists():
+        pytest.skip("kernel library not built")
+    tool = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    local = tmp_path / so.name
+    shutil.copy(so, local)        # --offloading extracts next to its input
+    subprocess.run([tool, "--offloading", str(local)], capture_output=True, text=True, check=True)
+    body = None
+    for obj in sorted(tmp_path.glob(so.name + ".*gfx950")):
+        dis = subprocess.run([tool, "-d", "--mcpu=gfx950", str(obj)], capture_output=True, text=True).stdout
+        start = dis.find("gemm4h_kernel")
+        while start >= 0 and not dis[start:dis.find("\n", start)].endswith(">:"):
+            start = dis.find("gemm4h_kernel", start + 1)
+        if start >= 0:
+            body = dis[start:dis.find("s_endpgm", start)]
+            break
+    assert body is not None, "gemm4h_kernel not in the gfx950 code object"
+    ins = [ln.split("//")[0].strip() for ln in body.splitlines()[1:] if ln.strip()]
+    mfma = [i for i, s in enumerate(ins) if s.startswith("v_mfma_f32_16x16x32_bf16")]
+    assert len(mfma) >= 128
+    drain = next(i for i in range(mfma[-1], len(ins)) if ins[i].startswith("s_nop 7"))
+    bad = [s for s in ins[mfma[0]:drain]
+           if s.startswith(("v_accvgpr_read", "v_accvgpr_write", "v_accvgpr_mov", "scratch_"))]
+    assert not bad, bad[:5]
