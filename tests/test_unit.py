@@ -737,7 +737,8 @@ def test_shipped_tuning_table_covers_bench_shapes(monkeypatch):
     called = []
     key = ("conv1x1", 2048 * 56 * 56, 256, 64)
     ops.tuned_wgrad(key, lambda: called.append("lib"), lambda: called.append("k12"),
-                    k9=lambda: called.append("k9"), k12w=lambda: called.append("k12w"))
+                    k9=lambda: called.append("k9"), k12w=lambda: called.append("k12w"),
+                    k12wh=lambda: called.append("k12wh"))
     assert called == [ops._WGRAD_CHOICE[key]] and ops.tuning_timings() == 0
 
 
