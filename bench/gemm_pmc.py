@@ -30,6 +30,8 @@ def main():
             torch.mm(dy.t(), x)
             m.linear_wgrad(dy, x, None, False, 0)
             m.linear_wgrad4(dy, x, None, False, 0)
+            if M % 128 == 0:
+                m.linear_wgrad4h(dy, x, None, False, 0)
         torch.cuda.synchronize()
         return
     x = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
